@@ -1,0 +1,518 @@
+// capi.cpp -- extern "C" boundary (include/dfmi.h) and the PIMPLE orchestration.
+//
+// Host side of the drop-in: what createGPUSolver.H + dfLowMachFoam.C do with the reference's
+// C++ classes (dfMatrixDataBase, dfRhoEqn, dfUEqn, dfYEqn, dfEEqn, dfpEqn, dfThermo) is exposed
+// here as plain C entry points with pointers and sizes. All device work is stream-ordered on one
+// HIP stream per context; the host synchronises only where the reference reads back to the host
+// (solver residual checks, dfmi_get_field, dfmi_sync).
+#include "dfmi_ctx.h"
+#include "../../include/dfmi.h"
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <numeric>
+
+struct dfmi_ctx { dfmi::Ctx x; };
+
+namespace {
+thread_local std::string g_err;
+
+template <class FN> int guard(FN&& fn) {
+  try { fn(); return 0; }
+  catch (std::exception& e) { g_err = e.what(); return 1; }
+  catch (...) { g_err = "unknown error"; return 2; }
+}
+
+using namespace dfmi;
+
+void alloc_field(Ctx& x, const std::string& name, long n, int ncomp, bool boundary) {
+  Field& f = x.fields[name];
+  f.n = n; f.ncomp = ncomp; f.boundary = boundary;
+  f.buf.alloc((size_t)n * ncomp);
+  f.buf.zero(x.stream);
+}
+
+void allocate_fields(Ctx& x) {
+  const long C = x.C, F = x.F, B = x.B;
+  const int S = x.S;
+  for (auto n : {"rho", "rho_old", "p", "p_old", "he", "T", "K", "K_old", "psi", "mu", "alpha", "dpdt", "rAU",
+                 "diffAlphaD", "psip0"}) {
+    alloc_field(x, n, C, 1, false);
+    alloc_field(x, std::string("boundary_") + n, B, 1, true);
+  }
+  for (auto n : {"U", "U_old", "HbyA", "hDiffCorrFlux", "sumYDiffError"}) {
+    alloc_field(x, n, C, 3, false);
+    alloc_field(x, std::string("boundary_") + n, B, 3, true);
+  }
+  alloc_field(x, "tauU", C, 9, false);
+  alloc_field(x, "boundary_tauU", B, 9, true);
+  for (auto n : {"Y", "rhoD", "hai", "RR"}) {
+    alloc_field(x, n, C, S, false);
+    alloc_field(x, std::string("boundary_") + n, B, S, true);
+  }
+  for (auto n : {"phi", "phi_old", "phiUc", "rhorAUf", "phiHbyA"}) {
+    alloc_field(x, n, F, 1, false);
+    alloc_field(x, std::string("boundary_") + n, B, 1, true);
+  }
+  auto mk = [&](Matrix& A, int ns, int nsrc, int nb) {
+    A.nsys = ns;
+    A.lower.alloc((size_t)ns * F); A.upper.alloc((size_t)ns * F); A.diag.alloc((size_t)ns * C);
+    A.source.alloc((size_t)nsrc * C); A.ic.alloc((size_t)nb * B); A.bc.alloc((size_t)nb * B);
+    A.lower.zero(x.stream); A.upper.zero(x.stream); A.diag.zero(x.stream); A.source.zero(x.stream);
+    A.ic.zero(x.stream); A.bc.zero(x.stream);
+  };
+  mk(x.mU, 1, 3, 3);
+  x.mU.source_solve.alloc(3 * C);
+  mk(x.mY, S, S, S);
+  mk(x.mE, 1, 1, 1);
+  mk(x.mP, 1, 1, 1);
+  for (auto e : {"U", "Y", "E"}) if (!x.solver.count(e)) x.solver[e] = SolverCfg{20, 1e-5, 0.0};   // amgxUOptions
+  if (!x.solver.count("p")) x.solver["p"] = SolverCfg{1000, 1e-5, 0.0};                          // amgxpOptions
+}
+
+// Build the deterministic gather topology from owner/neighbour and the boundary face cells.
+void build_boundary_topology(Ctx& x) {
+  const int C = x.C, B = x.B;
+  x.poff.assign(x.P + 1, 0);
+  std::vector<int> slot_patch(B, -1);
+  std::vector<int8_t> prim(B, 0);
+  int off = 0;
+  for (int p = 0; p < x.P; ++p) {
+    x.poff[p] = off;
+    const int n = x.psize[p];
+    const int slots = x.pkind[p] == 2 ? 2 * n : n;
+    for (int i = 0; i < slots; ++i) { slot_patch[off + i] = p; prim[off + i] = i < n; }
+    off += slots;
+  }
+  x.poff[x.P] = off;
+  DFMI_CHECK(off == B, "patch sizes / kinds do not add up to num_boundary_surfaces");
+  std::vector<int> partner(B, -1);
+  for (int p = 0; p < x.P; ++p) {
+    if (x.pkind[p] != 1) continue;
+    const int q = x.cyc_nbr.empty() ? -1 : x.cyc_nbr[p];
+    DFMI_CHECK(q >= 0 && q < x.P && x.psize[q] == x.psize[p], "cyclic patch without a matching neighbour patch");
+    for (int i = 0; i < x.psize[p]; ++i) partner[x.poff[p] + i] = x.h_bfc[x.poff[q] + i];
+  }
+  std::vector<int> cnt(C + 1, 0);
+  for (int b = 0; b < B; ++b) if (prim[b]) {
+    const int c = x.h_bfc[b];
+    DFMI_CHECK(c >= 0 && c < C, "boundary face cell out of range");
+    cnt[c + 1]++;
+  }
+  for (int c = 0; c < C; ++c) cnt[c + 1] += cnt[c];
+  std::vector<int> slot(cnt[C]), pos(cnt.begin(), cnt.end() - 1);
+  for (int b = 0; b < B; ++b) if (prim[b]) slot[pos[x.h_bfc[b]]++] = b;
+  x.cbStart.upload(cnt, x.stream);
+  x.cbSlot.upload(slot.empty() ? std::vector<int>{0} : slot, x.stream);
+  x.partner.upload(partner, x.stream);
+  x.sprim.upload(prim.data(), prim.size(), x.stream);
+  x.bfc.upload(x.h_bfc, x.stream);
+}
+
+void set_ptype(Ctx& x, const std::string& field, const int* pt) {
+  std::vector<int> v(pt, pt + x.P);
+  x.ptype[field] = v;
+  std::vector<int8_t> s(x.B, EMPTY);
+  for (int p = 0; p < x.P; ++p) {
+    const int slots = x.pkind[p] == 2 ? 2 * x.psize[p] : x.psize[p];
+    for (int i = 0; i < slots; ++i) s[x.poff[p] + i] = (int8_t)pt[p];
+  }
+  x.stype[field].upload(s.data(), s.size(), x.stream);
+}
+
+void copy_field(Ctx& x, const std::string& name, const double* host, long count, int layout, bool to_dev) {
+  auto it = x.fields.find(name);
+  DFMI_CHECK(it != x.fields.end(), "unknown field '" + name + "'");
+  Field& f = it->second;
+  DFMI_CHECK(count == f.n, "field '" + name + "': expected " + std::to_string(f.n) + " values per component, got " +
+                               std::to_string(count));
+  const size_t tot = (size_t)f.n * f.ncomp;
+  const bool perm = layout == DFMI_AOS && (f.ncomp == 3 || f.ncomp == 9);
+  std::vector<double> tmp;
+  if (to_dev) {
+    const double* src = host;
+    if (perm) {
+      tmp.resize(tot);
+      for (long i = 0; i < f.n; ++i) for (int k = 0; k < f.ncomp; ++k) tmp[(size_t)k * f.n + i] = host[i * f.ncomp + k];
+      src = tmp.data();
+    }
+    DFMI_HIP(hipMemcpyAsync(f.buf.p, src, tot * sizeof(double), hipMemcpyHostToDevice, x.stream));
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  } else {
+    double* dst = const_cast<double*>(host);
+    if (perm) { tmp.resize(tot); dst = tmp.data(); }
+    DFMI_HIP(hipMemcpyAsync(dst, f.buf.p, tot * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    if (perm) {
+      double* out = const_cast<double*>(host);
+      for (long i = 0; i < f.n; ++i) for (int k = 0; k < f.ncomp; ++k) out[i * f.ncomp + k] = tmp[(size_t)k * f.n + i];
+    }
+  }
+}
+
+void require_ready(Ctx& x) {
+  DFMI_CHECK(x.have_sizes && x.have_topo && x.have_geom && x.have_bgeom, "mesh not fully initialised");
+}
+
+// ---- equation drivers
+void do_U(Ctx& x) {
+  u_assemble(x);
+  Matrix& A = x.mU;
+  solve_bicgstab(x, "U", 3, nullptr, A.lower, 0, A.upper, 0, A.diag, 0, A.source_solve, x.C, A.ic, A.bc, x.B, "U",
+                 x.f("U"), x.C, x.solver["U"]);
+  u_post_solve(x);
+}
+void do_Y(Ctx& x) {
+  DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
+  y_prep(x);
+  y_assemble(x);
+  Matrix& A = x.mY;
+  std::vector<int> map;
+  for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
+  solve_bicgstab(x, "Y", (int)map.size(), map.data(), A.lower, x.F, A.upper, x.F, A.diag, x.C, A.source, x.C, A.ic,
+                 A.bc, x.B, "Y", x.f("Y"), x.C, x.solver["Y"]);
+  y_post_solve(x);
+}
+void do_E(Ctx& x) {
+  e_assemble(x);
+  Matrix& A = x.mE;
+  solve_bicgstab(x, "E", 1, nullptr, A.lower, 0, A.upper, 0, A.diag, 0, A.source, 0, A.ic, A.bc, 0, "he", x.f("he"), 0,
+                 x.solver["E"]);
+  e_post_solve(x);
+}
+void do_p(Ctx& x) {
+  p_assemble(x);
+  Matrix& A = x.mP;
+  solve_pcg(x, "p", A.lower, A.upper, A.diag, A.source, A.ic, A.bc, "p", x.f("p"), x.f("boundary_p"), x.solver["p"]);
+  p_post_solve(x);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dfmi_version(void) { return "dfmi 0.1 (gfx950)"; }
+
+int dfmi_last_error(char* buf, int len) {
+  if (buf && len > 0) std::snprintf(buf, len, "%s", g_err.c_str());
+  return (int)g_err.size();
+}
+
+int dfmi_create(dfmi_ctx** out, int device) {
+  return guard([&] {
+    DFMI_CHECK(out, "null output pointer");
+    int n = 0;
+    DFMI_HIP(hipGetDeviceCount(&n));
+    DFMI_CHECK(device >= 0 && device < n, "device " + std::to_string(device) + " not available (" + std::to_string(n) + " devices)");
+    DFMI_HIP(hipSetDevice(device));
+    auto* c = new dfmi_ctx();
+    c->x.device = device;
+    DFMI_HIP(hipStreamCreateWithFlags(&c->x.stream, hipStreamNonBlocking));
+    *out = c;
+  });
+}
+
+int dfmi_destroy(dfmi_ctx* ctx) {
+  return guard([&] {
+    if (!ctx) return;
+    DFMI_HIP(hipSetDevice(ctx->x.device));
+    (void)hipStreamSynchronize(ctx->x.stream);
+    hipStream_t s = ctx->x.stream;
+    delete ctx;
+    (void)hipStreamDestroy(s);
+  });
+}
+
+int dfmi_set_constant_values(dfmi_ctx* ctx, int num_cells, int num_total_cells, int num_surfaces,
+                             int num_boundary_surfaces, int num_patches, int num_proc_surfaces,
+                             const int* patch_size, int num_species, double rdelta_t) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(num_cells > 0 && num_surfaces >= 0 && num_boundary_surfaces >= 0 && num_patches >= 0, "bad sizes");
+    DFMI_CHECK(num_species >= 2 && num_species <= 16, "num_species must be in [2,16]");
+    DFMI_CHECK(rdelta_t > 0, "rdelta_t must be positive");
+    x.C = num_cells; x.Ctot = num_total_cells; x.F = num_surfaces; x.B = num_boundary_surfaces; x.P = num_patches;
+    x.nproc_faces = num_proc_surfaces; x.S = num_species; x.rdt = rdelta_t;
+    x.psize.assign(patch_size, patch_size + num_patches);
+    x.pkind.assign(num_patches, 0);
+    x.cyc_nbr.assign(num_patches, -1);
+    x.peer.assign(num_patches, -1);
+    x.have_sizes = true;
+  });
+}
+
+int dfmi_set_cyclic_info(dfmi_ctx* ctx, const int* cyclic_neighbor) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_sizes, "call dfmi_set_constant_values first");
+    x.cyc_nbr.assign(cyclic_neighbor, cyclic_neighbor + x.P);
+  });
+}
+
+int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighbour, const int* proc_rows,
+                              const int* proc_cols, int global_offset) {
+  (void)proc_rows; (void)proc_cols; (void)global_offset;   // global CSR ids are an AmgX concern; halos use patches
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_sizes, "call dfmi_set_constant_values first");
+    const int C = x.C, F = x.F;
+    x.h_own.assign(owner, owner + F);
+    x.h_nei.assign(neighbour, neighbour + F);
+    std::vector<int> ownStart(C + 1, 0), nbrCnt(C + 1, 0);
+    for (int f = 0; f < F; ++f) {
+      const int o = owner[f], n = neighbour[f];
+      DFMI_CHECK(o >= 0 && o < C && n >= 0 && n < C && o < n, "face " + std::to_string(f) + ": owner/neighbour out of range or owner >= neighbour");
+      DFMI_CHECK(f == 0 || owner[f - 1] < o || (owner[f - 1] == o && neighbour[f - 1] < n),
+                 "faces are not in upper-triangular order (sorted by owner, then neighbour)");
+      ownStart[o + 1]++;
+      nbrCnt[n + 1]++;
+    }
+    for (int c = 0; c < C; ++c) { ownStart[c + 1] += ownStart[c]; nbrCnt[c + 1] += nbrCnt[c]; }
+    std::vector<int> nbrFace(std::max(F, 1)), pos(nbrCnt.begin(), nbrCnt.end() - 1);
+    for (int f = 0; f < F; ++f) nbrFace[pos[neighbour[f]]++] = f;   // ascending face order per cell
+    x.own.upload(x.h_own.empty() ? std::vector<int>{0} : x.h_own, x.stream);
+    x.nei.upload(x.h_nei.empty() ? std::vector<int>{0} : x.h_nei, x.stream);
+    x.ownStart.upload(ownStart, x.stream);
+    x.nbrStart.upload(nbrCnt, x.stream);
+    x.nbrFace.upload(nbrFace, x.stream);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.have_topo = true;
+  });
+}
+
+int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const double* mag_sf, const double* weight,
+                                       const double* delta_coeffs, const double* volume, const double* mesh_distance) {
+  (void)mesh_distance;   // used by limitedLinear only (disabled in the reference, dfMatrixOpBase.cu:2540-2600)
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_topo, "call dfmi_set_constant_indexes first");
+    const long F = x.F;
+    std::vector<double> soa(3 * F);
+    for (long f = 0; f < F; ++f) for (int k = 0; k < 3; ++k) soa[k * F + f] = sf[f * 3 + k];   // AoS -> SoA
+    x.Sf.upload(soa, x.stream);
+    x.magSf.upload(mag_sf, F, x.stream);
+    x.w.upload(weight, F, x.stream);
+    x.dc.upload(delta_coeffs, F, x.stream);
+    x.V.upload(volume, x.C, x.stream);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.have_geom = true;
+  });
+}
+
+int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* bsf, const double* bmag, const double* bdelta,
+                                       const double* bweight, const int* bface_cell, const int* ptype_calc,
+                                       const int* ptype_extrap) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_geom, "call dfmi_init_constant_fields_internal first");
+    const long B = x.B;
+    for (int p = 0; p < x.P; ++p) {
+      const int t = ptype_calc[p];
+      x.pkind[p] = (t == CYCLIC) ? 1 : (bc_proc(t) ? 2 : 0);
+    }
+    x.h_bfc.assign(bface_cell, bface_cell + B);
+    std::vector<double> soa(3 * B);
+    for (long b = 0; b < B; ++b) for (int k = 0; k < 3; ++k) soa[k * B + b] = bsf[b * 3 + k];
+    x.bSf.upload(soa.empty() ? std::vector<double>{0.0} : soa, x.stream);
+    x.bmagSf.upload(bmag, B, x.stream);
+    x.bdc.upload(bdelta, B, x.stream);
+    x.bw.upload(bweight, B, x.stream);
+    build_boundary_topology(x);
+    allocate_fields(x);
+    set_ptype(x, "calculated", ptype_calc);
+    set_ptype(x, "extrapolated", ptype_extrap);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.have_bgeom = true;
+  });
+}
+
+int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_bgeom, "call dfmi_init_constant_fields_boundary first");
+    std::string f(field);
+    static const char* ok[] = {"U", "p", "he", "K", "Y", "T", "rho"};
+    DFMI_CHECK(std::find_if(std::begin(ok), std::end(ok), [&](const char* s) { return f == s; }) != std::end(ok),
+               "unknown patch-type field '" + f + "'");
+    for (int p = 0; p < x.P; ++p) {
+      const int t = patch_type[p];
+      DFMI_CHECK(t >= 0 && t <= 10 && t != COUPLED, "patch " + std::to_string(p) + ": unsupported boundary condition code " + std::to_string(t));
+      DFMI_CHECK((x.pkind[p] == 1) == (t == CYCLIC) && (x.pkind[p] == 2) == bc_proc(t),
+                 "patch " + std::to_string(p) + ": field '" + f + "' type disagrees with the mesh patch kind");
+      if (t == GRADIENT_ENERGY) DFMI_CHECK(false, "gradientEnergy boundary not supported yet (energy BCs are a SURVEY 8f item)");
+    }
+    set_ptype(x, f, patch_type);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_set_inert_index(dfmi_ctx* ctx, int inert_index) {
+  return guard([&] {
+    DFMI_CHECK(inert_index >= 0 && inert_index < ctx->x.S, "inert index out of range");
+    ctx->x.inert = inert_index;
+  });
+}
+
+int dfmi_thermo_set_coeffs(dfmi_ctx* ctx, int S, const double* W, const double* nasa, const double* visc,
+                           const double* cond, const double* bdiff) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_sizes && S == x.S, "thermo species count differs from num_species");
+    Thermo& t = x.thermo;
+    t.S = S;
+    t.W.assign(W, W + S); t.nasa.assign(nasa, nasa + 15 * S); t.visc.assign(visc, visc + 5 * S);
+    t.cond.assign(cond, cond + 5 * S); t.bdiff.assign(bdiff, bdiff + 5 * S * S);
+    t.vc1.resize(S * S); t.vc2.resize(S * S);
+    for (int i = 0; i < S; ++i) for (int j = 0; j < S; ++j) {   // init_const_coeff_ptr (dfThermo.cu:22-52)
+      t.vc1[i * S + j] = std::pow((1 + W[i] / W[j]), -0.5);
+      t.vc2[i * S + j] = std::pow(W[j] / W[i], 0.25);
+    }
+    thermo_upload(x);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_thermo_load(dfmi_ctx* ctx, const char* path) {
+  std::vector<double> all;
+  int S = 0;
+  int rc = guard([&] {
+    std::ifstream in(path, std::ios::binary);
+    DFMI_CHECK(in.good(), std::string("cannot open thermo coefficient file ") + path);
+    in.read(reinterpret_cast<char*>(&S), sizeof(int));
+    DFMI_CHECK(S > 0 && S <= 64, "bad species count in thermo file");
+    const size_t n = S + 15 * S + 5 * S + 5 * S + 5 * S * S;
+    all.resize(n);
+    in.read(reinterpret_cast<char*>(all.data()), n * sizeof(double));
+    DFMI_CHECK((size_t)in.gcount() == n * sizeof(double), "truncated thermo coefficient file");
+  });
+  if (rc) return rc;
+  const double* p = all.data();
+  return dfmi_thermo_set_coeffs(ctx, S, p, p + S, p + 16 * S, p + 21 * S, p + 26 * S);
+}
+
+int dfmi_set_field(dfmi_ctx* ctx, const char* name, const double* host, long count, int layout) {
+  return guard([&] { copy_field(ctx->x, name, host, count, layout, true); });
+}
+int dfmi_get_field(dfmi_ctx* ctx, const char* name, double* host, long count, int layout) {
+  return guard([&] { copy_field(ctx->x, name, host, count, layout, false); });
+}
+
+int dfmi_pre_time_step(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); copy_old(ctx->x); }); }
+int dfmi_post_time_step(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); }); }
+int dfmi_rho_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); rho_process(ctx->x, false); }); }
+int dfmi_U_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_U(ctx->x); }); }
+int dfmi_Y_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_Y(ctx->x); }); }
+int dfmi_E_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_E(ctx->x); }); }
+int dfmi_p_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_p(ctx->x); }); }
+int dfmi_U_get_HbyA(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); u_hbya(ctx->x); }); }
+int dfmi_thermo_correct(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); thermo_correct(ctx->x, false); }); }
+int dfmi_thermo_update_energy(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); thermo_correct(ctx->x, true); }); }
+int dfmi_thermo_update_rho(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); thermo_rho_from_psi(ctx->x); }); }
+int dfmi_thermo_psip0(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); thermo_psip0(ctx->x); }); }
+int dfmi_thermo_correct_psip_rho(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); thermo_correct_psip_rho(ctx->x); }); }
+
+// dfLowMachFoam.C:284-531 with nOuterCorrectors = 1 (the configuration every reference GPU case uses)
+int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    copy_old(x);                    // preTimeStep
+    rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
+    do_U(x);                        // UEqn
+    do_Y(x);                        // YEqn
+    do_E(x);                        // EEqn
+    thermo_correct(x, false);       // correctThermo
+    for (int i = 0; i < n_corr; ++i) {   // pEqn_GPU.H
+      thermo_rho_from_psi(x);
+      thermo_psip0(x);
+      u_hbya(x);
+      do_p(x);
+      thermo_correct_psip_rho(x);
+      rho_process(x, false);
+    }
+    thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
+  });
+}
+
+// correct_boundary_conditions_{scalar,vector} of one named field (dfMatrixOpBase.cu:2402-2491)
+int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    std::string f(field);
+    if (f == "Y") k_bc_correct(x, "Y", x.f("Y"), x.f("boundary_Y"), x.S);
+    else if (f == "U") k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
+    else if (f == "p" || f == "he" || f == "T" || f == "rho" || f == "K") k_bc_correct(x, f.c_str(), x.f(f), x.f("boundary_" + f), 1);
+    else throw Error("dfmi_correct_boundary: unsupported field '" + f + "'");
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_sync(dfmi_ctx* ctx) { return guard([&] { DFMI_HIP(hipStreamSynchronize(ctx->x.stream)); }); }
+
+int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    std::string e(eqn);
+    if (e == "rho") {
+      if (!x.fields.count("dbg_rho_diag")) { alloc_field(x, "dbg_rho_diag", x.C, 1, false); alloc_field(x, "dbg_rho_source", x.C, 1, false); }
+      rho_process(x, true);
+    } else if (e == "U") {
+      if (!x.fields.count("dbg_gradU")) alloc_field(x, "dbg_gradU", x.C, 9, false);
+      u_assemble(x);
+    } else if (e == "Y") {
+      if (!x.fields.count("dbg_gradY")) alloc_field(x, "dbg_gradY", x.C, 3 * x.S, false);
+      y_prep(x); y_assemble(x);
+    } else if (e == "E") e_assemble(x);
+    else if (e == "p") p_assemble(x);
+    else if (e == "HbyA") u_hbya(x);
+    else if (e == "p_post") p_post_solve(x);
+    else if (e == "Y_post") y_post_solve(x);
+    else throw Error("unknown equation '" + e + "'");
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    std::string e(eqn), p(part);
+    Matrix* A = e == "U" ? &x.mU : e == "Y" ? &x.mY : e == "E" ? &x.mE : e == "p" ? &x.mP : nullptr;
+    DFMI_CHECK(A, "unknown equation '" + e + "'");
+    DevBuf<double>* b = p == "lower" ? &A->lower : p == "upper" ? &A->upper : p == "diag" ? &A->diag :
+                        p == "source" ? &A->source : p == "source_solve" ? &A->source_solve :
+                        p == "internal_coeffs" ? &A->ic : p == "boundary_coeffs" ? &A->bc : nullptr;
+    DFMI_CHECK(b && b->p, "unknown matrix part '" + p + "'");
+    DFMI_CHECK((size_t)count == b->n, "matrix part size mismatch: expected " + std::to_string(b->n));
+    DFMI_HIP(hipMemcpyAsync(host, b->p, count * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, double abs_tol) {
+  return guard([&] {
+    std::string e(eqn);
+    DFMI_CHECK(e == "U" || e == "Y" || e == "E" || e == "p", "unknown equation '" + e + "'");
+    DFMI_CHECK(max_iter > 0 && tol >= 0 && abs_tol >= 0, "bad solver controls");
+    ctx->x.solver[e] = SolverCfg{max_iter, tol, abs_tol};
+  });
+}
+
+int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel) {
+  return guard([&] {
+    auto it = ctx->x.last_stats.find(eqn);
+    DFMI_CHECK(it != ctx->x.last_stats.end(), std::string("no solve recorded for ") + eqn);
+    if (iters) *iters = it->second.iters;
+    if (res0) *res0 = it->second.res0;
+    if (rel) *rel = it->second.res;
+  });
+}
+
+int dfmi_set_comm_info(dfmi_ctx* ctx, const void* uid, int nranks, int rank, const int* neighb) {
+  (void)uid; (void)nranks; (void)rank; (void)neighb;
+  return guard([&] { DFMI_CHECK(false, "RCCL halo not built in this library"); });
+}
+int dfmi_get_unique_id(void* out) { (void)out; return guard([&] { DFMI_CHECK(false, "RCCL halo not built"); }); }
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// dfmi_common.h -- shared host/device definitions for the MI355X-native dfLowMachFoam hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace dfmi {
+
+// Boundary-condition codes, identical to the reference enum (src_gpu/dfMatrixDataBase.H:81-93)
+enum BC : int8_t {
+  ZERO_GRADIENT = 0, FIXED_VALUE = 1, COUPLED = 2, EMPTY = 3, GRADIENT_ENERGY = 4, CALCULATED = 5,
+  CYCLIC = 6, PROCESSOR = 7, EXTRAPOLATED = 8, FIXED_ENERGY = 9, PROCESSOR_CYCLIC = 10
+};
+
+__host__ __device__ inline bool bc_coupled(int t) { return t == CYCLIC || t == PROCESSOR || t == PROCESSOR_CYCLIC || t == COUPLED; }
+__host__ __device__ inline bool bc_proc(int t) { return t == PROCESSOR || t == PROCESSOR_CYCLIC; }
+__host__ __device__ inline bool bc_fixes_value(int t) { return t == FIXED_VALUE || t == FIXED_ENERGY; }
+
+struct Error : std::runtime_error { using std::runtime_error::runtime_error; };
+
+#define DFMI_HIP(call)                                                                              \
+  do {                                                                                              \
+    hipError_t _e = (call);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      throw ::dfmi::Error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + __FILE__ + \
+                          ":" + std::to_string(__LINE__) + " in " #call);                           \
+  } while (0)
+
+#define DFMI_CHECK(cond, msg) \
+  do { if (!(cond)) throw ::dfmi::Error(std::string("dfmi: ") + (msg)); } while (0)
+
+// Owning device allocation (the reference never frees, dfMatrixDataBase.cu:111; we do).
+template <class T> struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; return *this; }
+  ~DevBuf() { release(); }
+  void release() { if (p) { (void)hipFree(p); p = nullptr; n = 0; } }
+  void alloc(size_t count) {
+    release();
+    n = count;
+    if (count) DFMI_HIP(hipMalloc(&p, count * sizeof(T)));
+  }
+  void zero(hipStream_t s) { if (n) DFMI_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s)); }
+  void upload(const T* h, size_t count, hipStream_t s) {
+    if (count != n) alloc(count);
+    if (count) DFMI_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  void upload(const std::vector<T>& v, hipStream_t s) { upload(v.data(), v.size(), s); }
+  operator T*() const { return p; }
+};
+
+inline int blocks_for(long n, int tpb) { return (int)((n + tpb - 1) / tpb); }
+
+}  // namespace dfmi

@@ -1,0 +1,148 @@
+// dfmi_ctx.h -- the device-resident database (the MI355X counterpart of dfMatrixDataBase,
+// reference src_gpu/dfMatrixDataBase.H:97-324) plus per-equation workspaces.
+//
+// HBM layout (all fp64 values SoA, int32 indices):
+//   cells: scalar [C]; vector [3][C]; tensor [9][C]; species [S][C] (species-major)
+//   faces: [F]; vectors [3][F]
+//   boundary slots: [B] in OpenFOAM patch order, processor patches take 2n slots
+//                   [neighbour values n | patch-internal values n] (createGPUSolver.H:118-123)
+// Topology for deterministic cell gathers (no FP atomics anywhere):
+//   ownStart[C+1]           faces owned by c are [ownStart[c], ownStart[c+1]) (upper-triangular order)
+//   nbrStart[C+1], nbrFace  faces whose neighbour is c, ascending face index (losort)
+//   cbStart[C+1], cbSlot    primary boundary slots of c, ascending slot index
+// Visiting nbrFace, then own faces, then cbSlot is exactly OpenFOAM's sequential face order.
+#pragma once
+#include "dfmi_common.h"
+#include <map>
+#include <memory>
+
+namespace dfmi {
+
+struct MeshView {
+  int C, F, B, S;
+  const int *own, *nei, *ownStart, *nbrStart, *nbrFace, *cbStart, *cbSlot, *bfc, *partner;
+  const int8_t* sprim;   // 1 = primary slot (owner side), 0 = processor [internal n] slot
+  const double *Sf, *magSf, *w, *dc, *V, *bSf, *bmagSf, *bw, *bdc;
+  double rdt;
+};
+
+struct Field {
+  DevBuf<double> buf;
+  long n = 0;       // values per component
+  int ncomp = 1;
+  bool boundary = false;
+};
+
+// one assembled fvMatrix (LDU + boundary coefficients), reference storage convention
+struct Matrix {
+  int nsys = 1;                 // species batch for Y
+  DevBuf<double> lower, upper, diag, source, ic, bc;
+  DevBuf<double> source_solve;  // U only: source incl. -grad(p)
+};
+
+struct SolverCfg {
+  int max_iter = 20;
+  double tol = 1e-5;           // relative to the initial residual (AmgX RELATIVE_INI, amgxUOptions)
+  double abs_tol = 0.0;
+};
+
+struct SolveStats { int iters = 0; double res0 = 0, res = 0; };
+
+struct Thermo {
+  int S = 0;
+  std::vector<double> W, nasa, visc, cond, bdiff, vc1, vc2;
+  DevBuf<double> dW, dnasa, dvisc, dcond, dbdiff, dvc1, dvc2;
+};
+
+struct Halo;   // RCCL processor-patch exchange (halo.cpp)
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // sizes (dfMatrixDataBase::setConstantValues, dfMatrixDataBase.cu:114-147)
+  int C = 0, Ctot = 0, F = 0, B = 0, P = 0, S = 0, nproc_faces = 0;
+  double rdt = 0;
+  int inert = -1;
+  bool have_sizes = false, have_topo = false, have_geom = false, have_bgeom = false;
+  std::vector<int> psize, poff, pkind, cyc_nbr, peer;   // pkind: 0 plain, 1 cyclic, 2 processor
+  std::vector<int> h_bfc, h_own, h_nei;
+  // topology
+  DevBuf<int> own, nei, ownStart, nbrStart, nbrFace, cbStart, cbSlot, bfc, partner;
+  DevBuf<int8_t> sprim;
+  // geometry
+  DevBuf<double> Sf, magSf, w, dc, V, bSf, bmagSf, bw, bdc;
+  // per-field patch types (host, per patch) and per-slot device copies
+  std::map<std::string, std::vector<int>> ptype;
+  std::map<std::string, DevBuf<int8_t>> stype;
+  // fields
+  std::map<std::string, Field> fields;
+  // matrices
+  Matrix mU, mY, mE, mP;
+  std::map<std::string, SolverCfg> solver;
+  std::map<std::string, SolveStats> last_stats;
+  Thermo thermo;
+  // scratch
+  DevBuf<double> scratch;
+  Halo* halo = nullptr;          // owned; freed by halo_destroy()
+  ~Ctx();
+  int n_corr = 2;
+
+  MeshView view() const {
+    MeshView m;
+    m.C = C; m.F = F; m.B = B; m.S = S;
+    m.own = own; m.nei = nei; m.ownStart = ownStart; m.nbrStart = nbrStart; m.nbrFace = nbrFace;
+    m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
+    m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
+    m.rdt = rdt;
+    return m;
+  }
+  double* f(const std::string& name) {
+    auto it = fields.find(name);
+    DFMI_CHECK(it != fields.end(), "unknown field '" + name + "'");
+    return it->second.buf.p;
+  }
+  const int8_t* st(const std::string& field) {
+    auto it = stype.find(field);
+    DFMI_CHECK(it != stype.end(), "patch types not set for field '" + field + "'");
+    return it->second.p;
+  }
+  const std::vector<int>& pt(const std::string& field) {
+    auto it = ptype.find(field);
+    DFMI_CHECK(it != ptype.end(), "patch types not set for field '" + field + "'");
+    return it->second;
+  }
+};
+
+// ---- launchers (fv_kernels.hip)
+void k_bc_correct(Ctx& x, const char* type_field, double* vf, double* bvf, int ncomp);
+void rho_process(Ctx& x, bool write_matrix);
+void u_assemble(Ctx& x);
+void u_post_solve(Ctx& x);
+void u_hbya(Ctx& x);
+void p_assemble(Ctx& x);
+void p_post_solve(Ctx& x);
+void y_prep(Ctx& x);
+void y_assemble(Ctx& x);
+void y_post_solve(Ctx& x);
+void e_assemble(Ctx& x);
+void e_post_solve(Ctx& x);
+void copy_old(Ctx& x);
+void thermo_rho_from_psi(Ctx& x);
+void thermo_psip0(Ctx& x);
+void thermo_correct_psip_rho(Ctx& x);
+// thermo.hip
+void thermo_upload(Ctx& x);
+void thermo_correct(Ctx& x, bool from_T);
+// linsolve.hip
+SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
+                          const double* upper, long ustride, const double* diag, long dstride, const double* source,
+                          long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
+                          double* xsol, long xstride, const SolverCfg& cfg);
+SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
+                     const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
+                     double* bxsol, const SolverCfg& cfg);
+// halo.cpp
+void halo_exchange(Ctx& x, double* bvf, int ncomp, long bstride);
+void halo_destroy(Halo* h);
+
+}  // namespace dfmi

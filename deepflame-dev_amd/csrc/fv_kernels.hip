@@ -1,0 +1,882 @@
+// fv_kernels.hip -- finite-volume assembly for dfLowMachFoam on MI355X (gfx950).
+//
+// Replaces the reference's face-parallel atomicAdd kernels (src_gpu/dfMatrixOpBase.cu:658-2173,
+// dfUEqn.cu, dfYEqn.cu, dfEEqn.cu, dfpEqn.cu, dfRhoEqn.cu) with deterministic cell-centric gathers:
+// one thread per cell walks its faces in OpenFOAM's sequential order (neighbour faces ascending,
+// owned faces ascending, then its boundary slots), keeping one accumulator per fvm/fvc term, so the
+// result is bit-identical to the sequential restatement in oracle/df_oracle.cpp and independent of
+// scheduling. Owned-face coefficients (lower/upper) are written by the owner thread; the neighbour
+// thread recomputes the same face value instead of reading it back (no grid-wide dependency).
+// Whole equations are fused into one or two launches (the reference issues 10-40 per equation).
+//
+// Compiled with -ffp-contract=off: the arithmetic sequence is the oracle's, op for op.
+#include "dfmi_ctx.h"
+
+namespace dfmi {
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ double interp_f(double w, double vo, double vn) { return w * (vo - vn) + vn; }
+__device__ __forceinline__ double interp_b(double w, double vo, double vn) { return w * vo + (1.0 - w) * vn; }
+
+struct BCoef { double vic, vbc, gic, gbc; };
+__device__ __forceinline__ BCoef bcoef(int t, double bval, double w, double bdc, double egrad = 0.0) {
+  switch (t) {
+    case ZERO_GRADIENT: case EXTRAPOLATED: return {1., 0., 0., 0.};
+    case FIXED_VALUE: case FIXED_ENERGY: return {0., bval, -1 * bdc, bdc * bval};
+    case GRADIENT_ENERGY: return {1., egrad / bdc, 0., egrad};
+    default: return {w, 1.0 - w, -1 * bdc, bdc};
+  }
+}
+
+// coupled neighbour-side cell value: cyclic partner cell, or the processor halo value in the slot
+__device__ __forceinline__ double nbrv(const MeshView& m, const double* vf, const double* bvf, int b) {
+  int pc = m.partner[b];
+  return pc >= 0 ? vf[pc] : bvf[b];
+}
+__device__ __forceinline__ double bface(const MeshView& m, int t, const double* vf, const double* bvf, int b, int c) {
+  return bc_coupled(t) ? interp_b(m.bw[b], vf[c], nbrv(m, vf, bvf, b)) : bvf[b];
+}
+
+// visit faces of cell c in sequential order: fn(face, other_cell, is_owner)
+template <class FN> __device__ __forceinline__ void each_face(const MeshView& m, int c, FN&& fn) {
+  const int e1 = m.nbrStart[c + 1];
+  for (int k = m.nbrStart[c]; k < e1; ++k) { const int f = m.nbrFace[k]; fn(f, m.own[f], false); }
+  const int e2 = m.ownStart[c + 1];
+  for (int f = m.ownStart[c]; f < e2; ++f) fn(f, m.nei[f], true);
+}
+// visit primary, non-empty boundary slots of c in slot order: fn(slot, type)
+template <class FN> __device__ __forceinline__ void each_slot(const MeshView& m, const int8_t* ty, int c, FN&& fn) {
+  const int e = m.cbStart[c + 1];
+  for (int k = m.cbStart[c]; k < e; ++k) {
+    const int b = m.cbSlot[k];
+    const int t = ty[b];
+    if (t == EMPTY) continue;
+    fn(b, t);
+  }
+}
+
+// ------------------------------------------------------------------ boundary correction
+// correct_boundary_conditions_scalar/vector (dfMatrixOpBase.cu:2402-2491)
+__global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
+                             double* __restrict__ bvf, int ncomp) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const int t = ty[b];
+  const int c = m.bfc[b];
+  for (int k = 0; k < ncomp; ++k) {
+    const double* v = vf + (long)k * m.C;
+    double* bv = bvf + (long)k * m.B;
+    if (t == ZERO_GRADIENT || t == EXTRAPOLATED) bv[b] = v[c];
+    else if (t == CYCLIC) bv[b] = interp_b(m.bw[b], v[c], v[m.partner[b]]);
+    else if (bc_proc(t) && !m.sprim[b]) bv[b] = v[c];
+  }
+}
+
+// ------------------------------------------------------------------ rhoEqn (dfRhoEqn.cu:41-92)
+__global__ void k_rho(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ rho_old,
+                      const double* __restrict__ phi, const double* __restrict__ bphi, double* __restrict__ rho,
+                      double* __restrict__ odiag, double* __restrict__ osrc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  double div = 0.0;
+  each_face(m, c, [&](int f, int, bool own) { if (own) div += phi[f]; else div -= phi[f]; });
+  each_slot(m, ty, c, [&](int b, int) { div += bphi[b]; });
+  const double diag = m.rdt * m.V[c];
+  double src = m.rdt * rho_old[c] * m.V[c];
+  src = src - div;
+  rho[c] = src / diag;
+  if (odiag) { odiag[c] = diag; osrc[c] = src; }
+}
+
+// ------------------------------------------------------------------ UEqn
+// gradU (fvc_grad_vector :944-1107) -> T = mu*dev2(T(gradU)) (scale_dev2t_tensor_kernel :623) for
+// cells, and for the cell's non-coupled slots the corrected boundary gradient (:1239-1327) -> bT.
+__device__ __forceinline__ void dev2T(double sc, const double* v, double* o) {
+  const double tr = (2. / 3.) * (v[0] + v[4] + v[8]);
+  o[0] = sc * (v[0] - tr); o[1] = sc * v[3]; o[2] = sc * v[6];
+  o[3] = sc * v[1]; o[4] = sc * (v[4] - tr); o[5] = sc * v[7];
+  o[6] = sc * v[2]; o[7] = sc * v[5]; o[8] = sc * (v[8] - tr);
+}
+
+__global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
+                         const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
+                         double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double s[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) s[k] = 0.0;
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double w = m.w[f];
+    double uf[3], sf[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) uf[j] = interp_f(w, U[j * C + o], U[j * C + n]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sf[i] = m.Sf[i * F + f];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { const double v = sf[i] * uf[j]; if (own) s[i * 3 + j] += v; else s[i * 3 + j] -= v; }
+  });
+  each_slot(m, ty, c, [&](int b, int t) {
+    double uf[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) uf[j] = bface(m, t, U + j * C, bU + j * B, b, c);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) s[i * 3 + j] += m.bSf[i * B + b] * uf[j];
+  });
+  const double vol = m.V[c];
+  double g[9], o[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) g[k] = s[k] / vol;
+  if (gout) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) gout[k * C + c] = g[k];
+  }
+  dev2T(mu[c], g, o);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) T[k * C + c] = o[k];
+  each_slot(m, ty, c, [&](int b, int t) {
+    if (bc_coupled(t)) return;
+    const double ms = m.bmagSf[b];
+    const double nv[3] = {m.bSf[b] / ms, m.bSf[B + b] / ms, m.bSf[2 * B + b] / ms};
+    double bg[9], bo[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double sn = (t == FIXED_VALUE) ? m.bdc[b] * (bU[j * B + b] - U[j * C + c]) : 0.0;
+      const double corr = sn - (nv[0] * g[0 * 3 + j] + nv[1] * g[1 * 3 + j] + nv[2] * g[2 * 3 + j]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bg[i * 3 + j] = g[i * 3 + j] + nv[i] * corr;
+    }
+    dev2T(bmu[b], bg, bo);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) bT[k * B + b] = bo[k];
+  });
+}
+
+// UEqn matrix (UEqn.H:3-20): ddt(rho,U) + div(phi,U) - laplacian(mu,U) - div(mu dev2 T(gradU)),
+// plus source_solve = source - grad(p) and rAU (dfUEqn.cu:721-738).
+__global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
+    const double* __restrict__ rho, const double* __restrict__ rho_old, const double* __restrict__ U_old,
+    const double* __restrict__ bU, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ mu, const double* __restrict__ bmu, const double* __restrict__ p,
+    const double* __restrict__ bp, const double* __restrict__ T, const double* __restrict__ bT,
+    double* __restrict__ lower, double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src,
+    double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double d1 = 0.0, dL = 0.0;
+  double dT[3] = {0.0, 0.0, 0.0}, gp[3] = {0.0, 0.0, 0.0};
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double w = m.w[f], ph = phi[f];
+    const double L1 = -w * ph;
+    const double U1 = L1 + ph;
+    const double UL = m.dc[f] * (interp_f(w, mu[o], mu[n]) * m.magSf[f]);
+    if (own) { d1 -= L1; lower[f] = L1 + (-UL); upper[f] = U1 + (-UL); }
+    else d1 -= U1;
+    dL -= UL;
+    const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double v = sf0 * interp_f(w, T[(0 + j) * C + o], T[(0 + j) * C + n]) +
+                       sf1 * interp_f(w, T[(3 + j) * C + o], T[(3 + j) * C + n]) +
+                       sf2 * interp_f(w, T[(6 + j) * C + o], T[(6 + j) * C + n]);
+      if (own) dT[j] += v; else dT[j] -= v;
+    }
+    const double pf = interp_f(w, p[o], p[n]);
+    const double g0 = sf0 * pf, g1 = sf1 * pf, g2 = sf2 * pf;
+    if (own) { gp[0] += g0; gp[1] += g1; gp[2] += g2; } else { gp[0] -= g0; gp[1] -= g1; gp[2] -= g2; }
+  });
+  // boundary contributions: explicit tensor divergence and the pressure gradient
+  each_slot(m, tyU, c, [&](int b, int t) {
+    double tt[9];
+    if (bc_coupled(t)) {
+      const int pc = m.partner[b];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) tt[k] = interp_b(m.bw[b], T[k * C + c], pc >= 0 ? T[k * C + pc] : bT[k * B + b]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) tt[k] = bT[k * B + b];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dT[j] += m.bSf[b] * tt[0 + j] + m.bSf[B + b] * tt[3 + j] + m.bSf[2 * B + b] * tt[6 + j];
+  });
+  each_slot(m, tyP, c, [&](int b, int t) {
+    const double pf = bface(m, t, p, bp, b, c);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gp[k] += m.bSf[k * B + b] * pf;
+  });
+  const double vol = m.V[c];
+  const double dg = (m.rdt * rho[c] * vol + d1) + (-dL);
+  diag[c] = dg;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double s = m.rdt * rho_old[c] * U_old[k * C + c] * vol + dT[k];
+    src[k * C + c] = s;
+    srcs[k * C + c] = s - gp[k];
+  }
+  double r = dg;
+  each_slot(m, tyU, c, [&](int b, int t) {
+    const double gam = bc_coupled(t) ? interp_b(m.bw[b], mu[c], nbrv(m, mu, bmu, b)) : bmu[b];
+    const double pG = gam * m.bmagSf[b];
+    double icv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const BCoef q = bcoef(t, bU[k * B + b], m.bw[b], m.bdc[b]);
+      icv[k] = bphi[b] * q.vic + (-(pG * q.gic));
+      ic[k * B + b] = icv[k];
+      bc[k * B + b] = -bphi[b] * q.vbc + (-(-pG * q.gbc));
+    }
+    r += (icv[0] + icv[1] + icv[2]) / 3;
+  });
+  rAU[c] = 1 / (r / vol);
+}
+
+// K = 0.5*magSqr(U) on cells (boundary K is done per slot below)
+__global__ void k_kinetic(int C, const double* __restrict__ U, double* __restrict__ K) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double x = U[c], y = U[(long)C + c], z = U[2L * C + c];
+  K[c] = 0.5 * (x * x + y * y + z * z);
+}
+
+// HbyA: fvMatrix::H() / V (dfUEqn.cu:753-822), unscaled; rAU scaling and constrainHbyA follow.
+__global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __restrict__ tyU, const double* __restrict__ U,
+    const double* __restrict__ bU, const double* __restrict__ lower, const double* __restrict__ upper,
+    const double* __restrict__ src, const double* __restrict__ ic, const double* __restrict__ bc,
+    double* __restrict__ H) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, B = m.B;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double* Uk = U + k * C;
+    double bd = 0.0;
+    each_slot(m, tyU, c, [&](int b, int) { bd += ic[k * B + b]; });
+    bd = -bd;
+    each_slot(m, tyU, c, [&](int b, int) { bd += (ic[b] + ic[B + b] + ic[2 * B + b]) / 3; });
+    double Hl = 0.0;
+    each_face(m, c, [&](int f, int oc, bool own) {
+      if (own) Hl -= upper[f] * Uk[oc]; else Hl -= lower[f] * Uk[oc];
+    });
+    double h = bd * Uk[c] + (Hl + src[k * C + c]);
+    each_slot(m, tyU, c, [&](int b, int t) {
+      h += bc_coupled(t) ? bc[k * B + b] * nbrv(m, Uk, bU + k * B, b) : bc[k * B + b];
+    });
+    H[k * C + c] = h / m.V[c];
+  }
+}
+
+__global__ void k_hbya_scale_cells(int C, const double* __restrict__ rAU, double* __restrict__ H) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) H[(long)k * C + c] = rAU[c] * H[(long)k * C + c];
+}
+__global__ void k_hbya_scale_slots(int B, const int8_t* __restrict__ tyU, const double* __restrict__ brAU,
+                                   const double* __restrict__ bU, double* __restrict__ bH) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double v = brAU[b] * bH[(long)k * B + b];
+    if (tyU[b] == FIXED_VALUE) v = bU[(long)k * B + b];   // constrainHbyA
+    bH[(long)k * B + b] = v;
+  }
+}
+
+// ------------------------------------------------------------------ pEqn (dfpEqn.cu:379-546)
+// per face: rhorAUf = interpolate(rho*rAU); phiHbyA = interpolate(rho)*flux(HbyA) + rhorAUf*ddtCorr;
+// symmetric laplacian coefficients lower = upper = -dc*(rhorAUf*magSf).
+__global__ void k_p_face(MeshView m, const double* __restrict__ rho, const double* __restrict__ rAU,
+                         const double* __restrict__ rho_old, const double* __restrict__ U_old,
+                         const double* __restrict__ phi_old, const double* __restrict__ H,
+                         double* __restrict__ rf, double* __restrict__ ph, double* __restrict__ lower,
+                         double* __restrict__ upper) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const long C = m.C, F = m.F;
+  const int o = m.own[f], n = m.nei[f];
+  const double w = m.w[f];
+  const double r = interp_f(w, rho[o] * rAU[o], rho[n] * rAU[n]);
+  rf[f] = r;
+  const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+  const double ro = rho_old[o], rn = rho_old[n];
+  const double phiCorr = phi_old[f] - (sf0 * interp_f(w, ro * U_old[o], rn * U_old[n]) +
+                                       sf1 * interp_f(w, ro * U_old[C + o], rn * U_old[C + n]) +
+                                       sf2 * interp_f(w, ro * U_old[2 * C + o], rn * U_old[2 * C + n]));
+  const double coeff = 1.0 - fmin(fabs(phiCorr) / (fabs(phi_old[f]) + 1e-15), 1.0);
+  const double ddtCorr = coeff * m.rdt * phiCorr;
+  const double fl = sf0 * interp_f(w, H[o], H[n]) + sf1 * interp_f(w, H[C + o], H[C + n]) +
+                    sf2 * interp_f(w, H[2 * C + o], H[2 * C + n]);
+  ph[f] = interp_f(w, rho[o], rho[n]) * fl + r * ddtCorr;
+  const double UL = m.dc[f] * (r * m.magSf[f]);
+  lower[f] = -UL;
+  upper[f] = -UL;
+}
+
+__global__ void k_p_slot(MeshView m, const int8_t* __restrict__ tyP, const int8_t* __restrict__ tyU,
+                         const double* __restrict__ rho, const double* __restrict__ brho, const double* __restrict__ rAU,
+                         const double* __restrict__ brAU, const double* __restrict__ rho_old,
+                         const double* __restrict__ brho_old, const double* __restrict__ U_old,
+                         const double* __restrict__ bU_old, const double* __restrict__ bphi_old,
+                         const double* __restrict__ H, const double* __restrict__ bH, const double* __restrict__ bp,
+                         double* __restrict__ brf, double* __restrict__ bph, double* __restrict__ ic,
+                         double* __restrict__ bc) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = tyP[b];
+  if (!m.sprim[b] || t == EMPTY) { brf[b] = 0.0; bph[b] = 0.0; ic[b] = 0.0; bc[b] = 0.0; return; }
+  const int c = m.bfc[b], pc = m.partner[b];
+  const double bw = m.bw[b];
+  double r;
+  if (bc_coupled(t)) r = interp_b(bw, rho[c] * rAU[c], pc >= 0 ? rho[pc] * rAU[pc] : brho[b] * brAU[b]);
+  else r = brho[b] * brAU[b];
+  brf[b] = r;
+  const int tu = tyU[b];
+  double ruo[3], Hb[3], rb;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (bc_coupled(tu)) {
+      const double rn = pc >= 0 ? rho_old[pc] * U_old[k * C + pc] : brho_old[b] * bU_old[k * B + b];
+      ruo[k] = interp_b(bw, rho_old[c] * U_old[k * C + c], rn);
+      Hb[k] = interp_b(bw, H[k * C + c], pc >= 0 ? H[k * C + pc] : bH[k * B + b]);
+    } else { ruo[k] = brho_old[b] * bU_old[k * B + b]; Hb[k] = bH[k * B + b]; }
+  }
+  rb = bc_coupled(tu) ? interp_b(bw, rho[c], pc >= 0 ? rho[pc] : brho[b]) : brho[b];
+  const double s0 = m.bSf[b], s1 = m.bSf[B + b], s2 = m.bSf[2 * B + b];
+  const double phiCorr = bphi_old[b] - (s0 * ruo[0] + s1 * ruo[1] + s2 * ruo[2]);
+  const double coeff = bc_fixes_value(tu) ? 0.0 : 1.0 - fmin(fabs(phiCorr) / (fabs(bphi_old[b]) + 1e-15), 1.0);
+  const double fl = s0 * Hb[0] + s1 * Hb[1] + s2 * Hb[2];
+  bph[b] = rb * fl + r * (coeff * m.rdt * phiCorr);
+  const BCoef q = bcoef(t, bp[b], bw, m.bdc[b]);
+  const double pG = r * m.bmagSf[b];
+  ic[b] = -(pG * q.gic);
+  bc[b] = -(-pG * q.gbc);
+}
+
+__global__ void k_p_cell(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ lower,
+                         const double* __restrict__ ph, const double* __restrict__ bph, const double* __restrict__ p,
+                         const double* __restrict__ p_old, const double* __restrict__ psi, const double* __restrict__ rho,
+                         const double* __restrict__ rho_old, double* __restrict__ diag, double* __restrict__ src) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  double dL = 0.0, div = 0.0;
+  each_face(m, c, [&](int f, int, bool own) {
+    dL -= -lower[f];
+    if (own) div += ph[f]; else div -= ph[f];
+  });
+  each_slot(m, tyP, c, [&](int b, int) { div += bph[b]; });
+  const double vol = m.V[c];
+  double dg = m.rdt * vol;
+  double sr = m.rdt * p_old[c] * vol;
+  const double APsi = -dg * p[c] + sr;
+  sr = sr - APsi;
+  sr = sr * psi[c];
+  dg = dg * psi[c];
+  sr = sr - vol * (m.rdt * (rho[c] - rho_old[c]));
+  sr = sr - div;
+  src[c] = sr;
+  diag[c] = dg - dL;
+}
+
+// after the p solve: phi = phiHbyA + pEqn.flux() (lduMatrix::faceH + fvMatrix::flux boundary)
+__global__ void k_p_flux_face(MeshView m, const double* __restrict__ ph, const double* __restrict__ lower,
+                              const double* __restrict__ upper, const double* __restrict__ p, double* __restrict__ phi) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  phi[f] = ph[f] + (upper[f] * p[m.nei[f]] - lower[f] * p[m.own[f]]);
+}
+__global__ void k_p_flux_slot(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ bph,
+                              const double* __restrict__ ic, const double* __restrict__ bc, const double* __restrict__ p,
+                              const double* __restrict__ bp, double* __restrict__ bphi) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const int t = tyP[b];
+  if (!m.sprim[b]) { bphi[b] = 0.0; return; }
+  if (t == EMPTY) return;
+  const int c = m.bfc[b];
+  const double fl = bc_coupled(t) ? ic[b] * p[c] - bc[b] * nbrv(m, p, bp, b) : ic[b] * p[c] - bc[b];
+  bphi[b] = bph[b] + fl;
+}
+// U = HbyA - rAU*grad(p); K; dpdt
+__global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ p,
+                              const double* __restrict__ bp, const double* __restrict__ p_old,
+                              const double* __restrict__ H, const double* __restrict__ rAU, double* __restrict__ U,
+                              double* __restrict__ K, double* __restrict__ dpdt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double g[3] = {0.0, 0.0, 0.0};
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double pf = interp_f(m.w[f], p[o], p[n]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { const double v = m.Sf[k * F + f] * pf; if (own) g[k] += v; else g[k] -= v; }
+  });
+  each_slot(m, tyP, c, [&](int b, int t) {
+    const double pf = bface(m, t, p, bp, b, c);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k] += m.bSf[k * B + b] * pf;
+  });
+  const double vol = m.V[c];
+  double u[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { u[k] = H[k * C + c] - rAU[c] * (g[k] / vol); U[k * C + c] = u[k]; }
+  K[c] = 0.5 * (u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  dpdt[c] = m.rdt * (p[c] - p_old[c]);
+}
+__global__ void k_kinetic_slots(int B, const double* __restrict__ bU, double* __restrict__ bK) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const double x = bU[b], y = bU[(long)B + b], z = bU[2L * B + b];
+  bK[b] = 0.5 * (x * x + y * y + z * z);
+}
+
+// ------------------------------------------------------------------ YEqn preparation (YEqn.H:24-118)
+// per cell: grad(Y_s), sumYDiffError, hDiffCorrFlux, diffAlphaD; per non-coupled slot of the cell:
+// corrected boundary gradients -> boundary sumYDiffError / hDiffCorrFlux.
+template <int S>
+__global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
+    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
+    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
+    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double g[S][3];
+#pragma unroll
+  for (int s = 0; s < S; ++s) { g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; }
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double yf = interp_f(w, Y[s * C + o], Y[s * C + n]);
+      const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+      if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; }
+      else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; }
+    }
+  });
+  each_slot(m, tyY, c, [&](int b, int t) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[s][k] += m.bSf[k * B + b] * yf;
+    }
+  });
+  const double vol = m.V[c];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[s][k] = g[s][k] / vol;
+  if (gout) {
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gout[(3L * s + k) * C + c] = g[s][k];
+  }
+  double se[3], hd[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double a = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) a += rhoD[s * C + c] * g[s][k];
+    se[k] = a;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double a = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) a += hai[s * C + c] * (rhoD[s * C + c] * g[s][k] - Y[s * C + c] * se[k]);
+    hd[k] = a;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { sumE[k * C + c] = se[k]; hD[k * C + c] = hd[k]; }
+  // diffAlphaD = sum_s laplacian(alpha*hai_s, Y_s)
+  double dad = 0.0;
+  const double ac = alpha[c];
+  for (int s = 0; s < S; ++s) {
+    const double* ys = Y + s * C;
+    const double* hs = hai + s * C;
+    double lap = 0.0;
+    each_face(m, c, [&](int f, int o2, bool own) {
+      const int o = own ? c : o2, n = own ? o2 : c;
+      const double v = interp_f(m.w[f], alpha[o] * hs[o], alpha[n] * hs[n]) * m.magSf[f] * (m.dc[f] * (ys[n] - ys[o]));
+      if (own) lap += v; else lap -= v;
+    });
+    each_slot(m, tyY, c, [&](int b, int t) {
+      double v;
+      if (bc_coupled(t)) {
+        const int pc = m.partner[b];
+        const double an = pc >= 0 ? alpha[pc] * hs[pc] : balpha[b] * bhai[s * B + b];
+        v = interp_b(m.bw[b], ac * hs[c], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, ys, bY + s * B, b) - ys[c]));
+      } else {
+        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - ys[c]) : 0.0;
+        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+      }
+      lap += v;
+    });
+    dad = dad + lap / vol;
+  }
+  dAD[c] = dad;
+  // boundary fields of the non-coupled slots (coupled slots interpolate cell values downstream)
+  each_slot(m, tyY, c, [&](int b, int t) {
+    if (bc_coupled(t)) return;
+    const double ms = m.bmagSf[b];
+    const double nv[3] = {m.bSf[b] / ms, m.bSf[B + b] / ms, m.bSf[2 * B + b] / ms};
+    double bg[S][3];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
+      const double corr = sn - (nv[0] * g[s][0] + nv[1] * g[s][1] + nv[2] * g[s][2]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bg[s][k] = g[s][k] + nv[k] * corr;
+    }
+    double bse[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s) a += brhoD[s * B + b] * bg[s][k];
+      bse[k] = a;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        a += bhai[s * B + b] * (brhoD[s * B + b] * bg[s][k] - bY[s * B + b] * bse[k]);
+      bsumE[k * B + b] = bse[k];
+      bhD[k * B + b] = a;
+    }
+  });
+}
+
+// phiUc = linearInterpolate(sumYDiffError) & Sf
+__global__ void k_phiuc_face(MeshView m, const double* __restrict__ sumE, double* __restrict__ phiUc) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const long C = m.C, F = m.F;
+  const int o = m.own[f], n = m.nei[f];
+  const double w = m.w[f];
+  phiUc[f] = m.Sf[f] * interp_f(w, sumE[o], sumE[n]) + m.Sf[F + f] * interp_f(w, sumE[C + o], sumE[C + n]) +
+             m.Sf[2 * F + f] * interp_f(w, sumE[2 * C + o], sumE[2 * C + n]);
+}
+__global__ void k_phiuc_slot(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ sumE,
+                             const double* __restrict__ bsumE, double* __restrict__ bphiUc) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = tyY[b];
+  if (!m.sprim[b] || t == EMPTY) { bphiUc[b] = 0.0; return; }
+  const int c = m.bfc[b];
+  double e[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    e[k] = bc_coupled(t) ? interp_b(m.bw[b], sumE[k * C + c], nbrv(m, sumE + k * C, bsumE + k * B, b)) : bsumE[k * B + b];
+  bphiUc[b] = m.bSf[b] * e[0] + m.bSf[B + b] * e[1] + m.bSf[2 * B + b] * e[2];
+}
+
+// Y species matrices, all non-inert species in one pass (dfYEqn.cu:571-638 fused and batched):
+// fvm::ddt(rho,Yi) + div(phi,Yi) + div(phiUc,Yi) == laplacian(rhoD_i,Yi) + RR_i
+template <int S>
+__global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __restrict__ tyY, int inert,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
+    double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
+    double* __restrict__ bc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double d1 = 0.0, d2 = 0.0;
+  double dL[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) dL[s] = 0.0;
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double ph = phi[f], pu = phiUc[f];
+    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double L1 = -wu * ph, U1 = L1 + ph;
+    const double L2 = -wu * pu, U2 = L2 + pu;
+    if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+    const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
+    const double Ls = L1 + L2, Us = U1 + U2;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == inert) continue;
+      const double UL = dcf * (interp_f(w, rhoD[s * C + o], rhoD[s * C + n]) * ms);
+      dL[s] -= UL;
+      if (own) { lower[s * F + f] = Ls - UL; upper[s * F + f] = Us - UL; }
+    }
+  });
+  const double vol = m.V[c];
+  const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+  const double ro = m.rdt * rho_old[c];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s == inert) continue;
+    diag[s * C + c] = dd - dL[s];
+    src[s * C + c] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
+  }
+  each_slot(m, tyY, c, [&](int b, int t) {
+    const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == inert) continue;
+      const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
+      const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+      const double gam = bc_coupled(t) ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+      const double pG = gam * m.bmagSf[b];
+      ic[s * B + b] = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+      bc[s * B + b] = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+    }
+  });
+}
+
+template <int S>
+__global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sum = 0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s == inert) continue;
+    double yi = Y[(long)s * C + c];
+    yi = yi > 0 ? yi : 0;
+    Y[(long)s * C + c] = yi;
+    sum += yi;
+  }
+  sum = 1 - sum;
+  Y[(long)inert * C + c] = sum > 0 ? sum : 0;
+}
+
+// ------------------------------------------------------------------ EEqn (EEqn.H:12-45; dfEEqn.cu:108-264)
+__global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __restrict__ tyH, const int8_t* __restrict__ tyK,
+    const double* __restrict__ he, const double* __restrict__ bhe, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ K, const double* __restrict__ K_old,
+    const double* __restrict__ bK, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ alpha, const double* __restrict__ balpha, const double* __restrict__ hD,
+    const double* __restrict__ bhD, const double* __restrict__ dpdt, const double* __restrict__ dAD,
+    const double* __restrict__ egrad, double* __restrict__ lower, double* __restrict__ upper,
+    double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic, double* __restrict__ bc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  double d1 = 0.0, dL = 0.0, divK = 0.0, divh = 0.0;
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const int o = own ? c : o2, n = own ? o2 : c;
+    const double ph = phi[f], w = m.w[f];
+    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double L1 = -wu * ph, U1 = L1 + ph;
+    const double UL = m.dc[f] * (interp_f(w, alpha[o], alpha[n]) * m.magSf[f]);
+    if (own) { d1 -= L1; lower[f] = L1 - UL; upper[f] = U1 - UL; } else d1 -= U1;
+    dL -= UL;
+    const double vk = ph * interp_f(w, K[o], K[n]);
+    const double vh = m.Sf[f] * interp_f(w, hD[o], hD[n]) + m.Sf[F + f] * interp_f(w, hD[C + o], hD[C + n]) +
+                      m.Sf[2 * F + f] * interp_f(w, hD[2 * C + o], hD[2 * C + n]);
+    if (own) { divK += vk; divh += vh; } else { divK -= vk; divh -= vh; }
+  });
+  each_slot(m, tyK, c, [&](int b, int t) { divK += bphi[b] * bface(m, t, K, bK, b, c); });
+  each_slot(m, tyH, c, [&](int b, int t) {
+    double h[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) h[k] = bface(m, t, hD + k * C, bhD + k * B, b, c);
+    divh += m.bSf[b] * h[0] + m.bSf[B + b] * h[1] + m.bSf[2 * B + b] * h[2];
+  });
+  const double vol = m.V[c];
+  diag[c] = (m.rdt * rho[c] * vol + d1) - dL;
+  double sL = m.rdt * rho_old[c] * he[c] * vol;
+  sL = sL - vol * (m.rdt * (rho[c] * K[c] - rho_old[c] * K_old[c]));
+  sL = sL - divK;
+  sL = sL + vol * dpdt[c];
+  double sR = vol * dAD[c];
+  sR = sR - divh;
+  src[c] = sL - sR;
+  each_slot(m, tyH, c, [&](int b, int t) {
+    const double eg = egrad ? egrad[b] : 0.0;
+    const BCoef qc = bcoef(t, bhe[b], bphi[b] >= 0 ? 1.0 : 0.0, m.bdc[b], eg);
+    const BCoef ql = bcoef(t, bhe[b], m.bw[b], m.bdc[b], eg);
+    const double gam = bc_coupled(t) ? interp_b(m.bw[b], alpha[c], nbrv(m, alpha, balpha, b)) : balpha[b];
+    const double pG = gam * m.bmagSf[b];
+    ic[b] = bphi[b] * qc.vic - pG * ql.gic;
+    bc[b] = -bphi[b] * qc.vbc - (-pG * ql.gbc);
+  });
+}
+
+// ------------------------------------------------------------------ elementwise thermo bookkeeping
+__global__ void k_mul(long n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] * b[i];
+}
+__global__ void k_add_psip(long n, const double* __restrict__ p, const double* __restrict__ psi,
+                           const double* __restrict__ psip0, double* __restrict__ rho) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < n) rho[i] += psi[i] * p[i] - psip0[i];
+}
+
+template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim3 b, hipStream_t st, A... a);
+
+}  // namespace
+
+// ====================================================================== launchers
+#define LAUNCH(kernel, n, ...) \
+  do { if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
+       DFMI_HIP(hipGetLastError()); } while (0)
+
+void k_bc_correct(Ctx& x, const char* tf, double* vf, double* bvf, int ncomp) {
+  LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp);
+}
+
+void copy_old(Ctx& x) {   // dfMatrixDataBase::preTimeStep (dfMatrixDataBase.cu:503-517)
+  const char* pairs[][2] = {{"rho_old", "rho"}, {"boundary_rho_old", "boundary_rho"}, {"phi_old", "phi"},
+                            {"boundary_phi_old", "boundary_phi"}, {"U_old", "U"}, {"boundary_U_old", "boundary_U"},
+                            {"K_old", "K"}, {"p_old", "p"}, {"boundary_p_old", "boundary_p"}};
+  for (auto& pr : pairs) {
+    Field& dst = x.fields.at(pr[0]);
+    DFMI_HIP(hipMemcpyAsync(dst.buf.p, x.f(pr[1]), dst.buf.n * sizeof(double), hipMemcpyDeviceToDevice, x.stream));
+  }
+}
+
+void rho_process(Ctx& x, bool write_matrix) {
+  double* od = write_matrix ? x.f("dbg_rho_diag") : nullptr;
+  double* os = write_matrix ? x.f("dbg_rho_source") : nullptr;
+  LAUNCH(k_rho, x.C, x.view(), x.st("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("rho"), od, os);
+  halo_exchange(x, nullptr, 0, 0);
+  k_bc_correct(x, "rho", x.f("rho"), x.f("boundary_rho"), 1);
+}
+
+void u_assemble(Ctx& x) {
+  Matrix& A = x.mU;
+  double* gout = x.fields.count("dbg_gradU") ? x.f("dbg_gradU") : nullptr;
+  LAUNCH(k_u_grad, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), x.f("mu"), x.f("boundary_mu"),
+         x.f("tauU"), x.f("boundary_tauU"), gout);
+  LAUNCH(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
+         x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
+         x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
+         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"));
+  k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
+}
+
+void u_post_solve(Ctx& x) {
+  k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
+  LAUNCH(k_kinetic, x.C, x.C, x.f("U"), x.f("K"));
+  LAUNCH(k_kinetic_slots, x.B, x.B, x.f("boundary_U"), x.f("boundary_K"));
+}
+
+void u_hbya(Ctx& x) {
+  Matrix& A = x.mU;
+  LAUNCH(k_u_hbya, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), A.lower.p, A.upper.p, A.source.p,
+         A.ic.p, A.bc.p, x.f("HbyA"));
+  k_bc_correct(x, "extrapolated", x.f("HbyA"), x.f("boundary_HbyA"), 3);
+  LAUNCH(k_hbya_scale_cells, x.C, x.C, x.f("rAU"), x.f("HbyA"));
+  LAUNCH(k_hbya_scale_slots, x.B, x.B, x.st("U"), x.f("boundary_rAU"), x.f("boundary_U"), x.f("boundary_HbyA"));
+}
+
+void p_assemble(Ctx& x) {
+  Matrix& A = x.mP;
+  MeshView m = x.view();
+  LAUNCH(k_p_face, x.F, m, x.f("rho"), x.f("rAU"), x.f("rho_old"), x.f("U_old"), x.f("phi_old"), x.f("HbyA"),
+         x.f("rhorAUf"), x.f("phiHbyA"), A.lower.p, A.upper.p);
+  LAUNCH(k_p_slot, x.B, m, x.st("p"), x.st("U"), x.f("rho"), x.f("boundary_rho"), x.f("rAU"), x.f("boundary_rAU"),
+         x.f("rho_old"), x.f("boundary_rho_old"), x.f("U_old"), x.f("boundary_U_old"), x.f("boundary_phi_old"),
+         x.f("HbyA"), x.f("boundary_HbyA"), x.f("boundary_p"), x.f("boundary_rhorAUf"), x.f("boundary_phiHbyA"),
+         A.ic.p, A.bc.p);
+  LAUNCH(k_p_cell, x.C, m, x.st("p"), A.lower.p, x.f("phiHbyA"), x.f("boundary_phiHbyA"), x.f("p"), x.f("p_old"),
+         x.f("psi"), x.f("rho"), x.f("rho_old"), A.diag.p, A.source.p);
+}
+
+void p_post_solve(Ctx& x) {
+  Matrix& A = x.mP;
+  MeshView m = x.view();
+  k_bc_correct(x, "p", x.f("p"), x.f("boundary_p"), 1);
+  LAUNCH(k_p_flux_face, x.F, m, x.f("phiHbyA"), A.lower.p, A.upper.p, x.f("p"), x.f("phi"));
+  LAUNCH(k_p_flux_slot, x.B, m, x.st("p"), x.f("boundary_phiHbyA"), A.ic.p, A.bc.p, x.f("p"), x.f("boundary_p"),
+         x.f("boundary_phi"));
+  LAUNCH(k_p_cell_post, x.C, m, x.st("p"), x.f("p"), x.f("boundary_p"), x.f("p_old"), x.f("HbyA"), x.f("rAU"),
+         x.f("U"), x.f("K"), x.f("dpdt"));
+  k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
+  LAUNCH(k_kinetic_slots, x.B, x.B, x.f("boundary_U"), x.f("boundary_K"));
+}
+
+#define DFMI_SWITCH_S(S, CALL)                                                                   \
+  switch (S) {                                                                                   \
+    case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break; \
+    case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break; \
+    case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break;                  \
+    case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break;                  \
+    case 16: CALL(16); break;                                                                      \
+    default: throw Error("dfmi: species count " + std::to_string(S) + " not instantiated (2..16)"); \
+  }
+
+void y_prep(Ctx& x) {
+  MeshView m = x.view();
+  double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
+#define CALL(NS) LAUNCH(k_y_prep<NS>, x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
+                        x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),    \
+                        x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"),         \
+                        x.f("diffAlphaD"), gout)
+  DFMI_SWITCH_S(x.S, CALL)
+#undef CALL
+  LAUNCH(k_phiuc_face, x.F, m, x.f("sumYDiffError"), x.f("phiUc"));
+  LAUNCH(k_phiuc_slot, x.B, m, x.st("Y"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("boundary_phiUc"));
+}
+
+void y_assemble(Ctx& x) {
+  Matrix& A = x.mY;
+  MeshView m = x.view();
+#define CALL(NS) LAUNCH(k_y_assemble<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
+                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
+                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p)
+  DFMI_SWITCH_S(x.S, CALL)
+#undef CALL
+}
+
+void y_post_solve(Ctx& x) {
+#define CALL(NS) LAUNCH(k_y_inert<NS>, x.C, x.C, x.inert, x.f("Y"))
+  DFMI_SWITCH_S(x.S, CALL)
+#undef CALL
+  k_bc_correct(x, "Y", x.f("Y"), x.f("boundary_Y"), x.S);
+}
+
+void e_assemble(Ctx& x) {
+  Matrix& A = x.mE;
+  MeshView m = x.view();
+  k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
+  const double* eg = x.fields.count("boundary_heGradient") ? x.f("boundary_heGradient") : nullptr;
+  LAUNCH(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
+         x.f("K"), x.f("K_old"), x.f("boundary_K"), x.f("phi"), x.f("boundary_phi"), x.f("alpha"),
+         x.f("boundary_alpha"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("dpdt"), x.f("diffAlphaD"),
+         eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p);
+}
+
+void e_post_solve(Ctx& x) { k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1); }
+
+void thermo_rho_from_psi(Ctx& x) {   // dfThermo::updateRho (dfThermo.cu:673-679)
+  LAUNCH(k_mul, x.C, (long)x.C, x.f("p"), x.f("psi"), x.f("rho"));
+  LAUNCH(k_mul, x.B, (long)x.B, x.f("boundary_p"), x.f("boundary_psi"), x.f("boundary_rho"));
+}
+void thermo_psip0(Ctx& x) {          // dfThermo::psip0 (:681-686)
+  LAUNCH(k_mul, x.C, (long)x.C, x.f("psi"), x.f("p"), x.f("psip0"));
+  LAUNCH(k_mul, x.B, (long)x.B, x.f("boundary_psi"), x.f("boundary_p"), x.f("boundary_psip0"));
+}
+void thermo_correct_psip_rho(Ctx& x) {   // dfThermo::correctPsipRho (:688-695)
+  LAUNCH(k_add_psip, x.C, (long)x.C, x.f("p"), x.f("psi"), x.f("psip0"), x.f("rho"));
+  LAUNCH(k_add_psip, x.B, (long)x.B, x.f("boundary_p"), x.f("boundary_psi"), x.f("boundary_psip0"), x.f("boundary_rho"));
+}
+
+}  // namespace dfmi

@@ -1,0 +1,225 @@
+// thermo.hip -- per-cell thermo/transport update (dfThermo::correctThermo, reference
+// src_gpu/dfThermo.cu:54-357, 572-671; CPU semantics dfChemistryModel.C:419-735).
+//
+// One fused kernel per cell (and one per boundary slot) does what the reference spreads over 8
+// launches with intermediate [S][C] arrays: Y->X, mean W, Newton T(h) (atol = rtol = 1e-7, <= 20
+// iterations), psi = W/(R T), rho = p psi, Wilke viscosity, mixture conductivity -> alpha = lambda/cp,
+// mixture-averaged rhoD_i (Cantera getMixDiffCoeffsMass) and hai_i = h_i(T) (the CPU hai that the
+// reference GPU path zeroes, dfYEqn.cu:489-494). The species count is a template parameter so the
+// per-cell species arrays stay in VGPRs (runtime-indexed arrays would go to scratch); the coefficient
+// tables are wave-uniform reads (scalar cache). HBM traffic per cell: read Y[S], he, p, T;
+// write T, he, psi, rho, mu, alpha, rhoD[S], hai[S].
+#include "dfmi_ctx.h"
+#include <cmath>
+
+namespace dfmi {
+namespace {
+
+constexpr double R_GAS = 8314.46261815324;
+constexpr double SQRT8 = 2.8284271247461903;
+
+struct TC {   // coefficient table pointers
+  const double *W, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;
+};
+
+template <int S>
+__device__ __forceinline__ double h_mix(const TC& t, double T, const double* y) {
+  double h = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double* a = t.nasa + i * 15;
+    const int o = (T > a[0]) ? 1 : 8;
+    h += (a[o] + a[o + 1] * T / 2 + a[o + 2] * T * T / 3 + a[o + 3] * T * T * T / 4 + a[o + 4] * T * T * T * T / 5 +
+          a[o + 5] / T) * R_GAS * T / t.W[i] * y[i];
+  }
+  return h;
+}
+template <int S>
+__device__ __forceinline__ double cp_mix(const TC& t, double T, const double* y) {
+  double cp = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double* a = t.nasa + i * 15;
+    const int o = (T > a[0]) ? 1 : 8;
+    cp += y[i] * (a[o] + a[o + 1] * T + a[o + 2] * T * T + a[o + 3] * T * T * T + a[o + 4] * T * T * T * T) * R_GAS / t.W[i];
+  }
+  return cp;
+}
+
+// state (T or he), p, Y -> T, he, psi, rho, mu, alpha, rhoD[S], hai[S]; mirrors oracle thermo_point
+template <int S>
+__device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, double& he, double p, const double* y,
+                                             double& psi, double& rho, double& mu, double& alpha, double* rhoD,
+                                             double* hai) {
+  double X[S];
+  double sum = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) sum += y[i] / t.W[i];
+  double Wm = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) { X[i] = y[i] / (t.W[i] * sum); Wm += X[i] * t.W[i]; }
+  if (fixT) he = h_mix<S>(t, T, y);
+  else {
+    double tt = T;
+    for (int n = 0; n < 20; ++n) {
+      const double h = h_mix<S>(t, tt, y), cp = cp_mix<S>(t, tt, y);
+      const double dT = (h - he) / cp;
+      tt -= dT;
+      if (fabs(h - he) < 1e-7 || fabs(dT / tt) < 1e-7) break;
+    }
+    T = tt;
+  }
+  const double lnT = log(T);
+  double poly[5];
+  poly[0] = 1.0; poly[1] = lnT; poly[2] = poly[1] * poly[1]; poly[3] = poly[1] * poly[2]; poly[4] = poly[2] * poly[2];
+  psi = Wm / (R_GAS * T);
+  rho = p * psi;
+  double sv[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    double dp = 0.;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) dp += t.visc[i * 5 + j] * poly[j];
+    sv[i] = dp;
+  }
+  double mumix = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    double s2 = 0.;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const double tmp = 1.0 + (sv[i] / sv[j]) * t.vc2[i * S + j];
+      s2 += X[j] / SQRT8 * t.vc1[i * S + j] * (tmp * tmp);
+    }
+    mumix += X[i] * (sv[i] * sv[i]) / s2;
+  }
+  const double sT = sqrt(T);
+  mu = mumix * sT;
+  double sc = 0., sic = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    double dp = 0.;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) dp += t.cond[i * 5 + j] * poly[j];
+    const double lam = dp * sT;
+    sc += X[i] * lam;
+    sic += X[i] / lam;
+  }
+  alpha = 0.5 * (sc + 1.0 / sic) / cp_mix<S>(t, T, y);
+  const double powT = T * sT, rdp = rho / p;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (X[i] + 1e-10 > 1.) { rhoD[i] = 0.; continue; }
+    double s1 = 0., s2 = 0.;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (i == j) continue;
+      double tmp = 0.;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) tmp += t.bdiff[(i * S + j) * 5 + k] * poly[k];
+      const double Dl = tmp * powT;
+      s1 += X[j] / Dl;
+      s2 += X[j] * t.W[j] / Dl;
+    }
+    s2 *= X[i] / (Wm - X[i] * t.W[i]);
+    rhoD[i] = 1 / (s1 + s2) * rdp;
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double* a = t.nasa + i * 15;
+    const int o = (T > a[0]) ? 1 : 8;
+    hai[i] = (a[o] + a[o + 1] * T / 2 + a[o + 2] * T * T / 3 + a[o + 3] * T * T * T / 4 + a[o + 4] * T * T * T * T / 5 +
+              a[o + 5] / T) * R_GAS * T / t.W[i];
+  }
+}
+
+template <int S>
+__global__ void __launch_bounds__(256) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
+    const double* __restrict__ p, const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho,
+    double* __restrict__ mu, double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  double y[S], rd[S], ha[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) y[i] = Y[(long)i * n + c];
+  double Tc = T[c], hc = he[c], ps, r, m, a;
+  thermo_point<S>(t, fixT != 0, Tc, hc, p[c], y, ps, r, m, a, rd, ha);
+  T[c] = Tc; he[c] = hc; psi[c] = ps; rho[c] = r; mu[c] = m; alpha[c] = a;
+#pragma unroll
+  for (int i = 0; i < S; ++i) { rhoD[(long)i * n + c] = rd[i]; hai[(long)i * n + c] = ha[i]; }
+}
+
+// boundary slots: fixedValue T patches evaluate from T (he from T), others from he (CPU
+// correctThermo boundary loop, dfChemistryModel.C:560-727); processor [internal n] slots copy cells.
+template <int S>
+__global__ void __launch_bounds__(256) k_thermo_slots(MeshView m, TC t, const int8_t* __restrict__ tyT, int fromT,
+    const double* __restrict__ cT, const double* __restrict__ che, const double* __restrict__ cpsi,
+    const double* __restrict__ crho, const double* __restrict__ cmu, const double* __restrict__ calpha,
+    const double* __restrict__ crhoD, const double* __restrict__ chai, double* __restrict__ T, double* __restrict__ he,
+    const double* __restrict__ p, const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho,
+    double* __restrict__ mu, double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int B = m.B;
+  if (b >= B) return;
+  const int ty = tyT[b];
+  if (ty == EMPTY) return;
+  if (bc_proc(ty) && !m.sprim[b]) {
+    const int c = m.bfc[b];
+    const long C = m.C;
+    T[b] = cT[c]; he[b] = che[c]; psi[b] = cpsi[c]; rho[b] = crho[c]; mu[b] = cmu[c]; alpha[b] = calpha[c];
+#pragma unroll
+    for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = crhoD[i * C + c]; hai[(long)i * B + b] = chai[i * C + c]; }
+    return;
+  }
+  double y[S], rd[S], ha[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) y[i] = Y[(long)i * B + b];
+  double Tb = T[b], hb = he[b], ps, r, mm, a;
+  thermo_point<S>(t, fromT != 0 || bc_fixes_value(ty), Tb, hb, p[b], y, ps, r, mm, a, rd, ha);
+  T[b] = Tb; he[b] = hb; psi[b] = ps; rho[b] = r; mu[b] = mm; alpha[b] = a;
+#pragma unroll
+  for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = rd[i]; hai[(long)i * B + b] = ha[i]; }
+}
+
+}  // namespace
+
+void thermo_upload(Ctx& x) {
+  Thermo& t = x.thermo;
+  t.dW.upload(t.W, x.stream);
+  t.dnasa.upload(t.nasa, x.stream);
+  t.dvisc.upload(t.visc, x.stream);
+  t.dcond.upload(t.cond, x.stream);
+  t.dbdiff.upload(t.bdiff, x.stream);
+  t.dvc1.upload(t.vc1, x.stream);
+  t.dvc2.upload(t.vc2, x.stream);
+}
+
+void thermo_correct(Ctx& x, bool from_T) {
+  Thermo& th = x.thermo;
+  DFMI_CHECK(th.S == x.S, "thermo coefficients not set or species count mismatch");
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2};
+  MeshView m = x.view();
+#define CALL(NS)                                                                                                   \
+  do {                                                                                                            \
+    if (x.C > 0) hipLaunchKernelGGL(k_thermo_cells<NS>, dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t, \
+                       (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"),    \
+                       x.f("alpha"), x.f("rhoD"), x.f("hai"));                                                    \
+    DFMI_HIP(hipGetLastError());                                                                                  \
+    if (x.B > 0) hipLaunchKernelGGL(k_thermo_slots<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t,  \
+                       x.st("T"), (int)from_T, x.f("T"), x.f("he"), x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), \
+                       x.f("rhoD"), x.f("hai"), x.f("boundary_T"), x.f("boundary_he"), x.f("boundary_p"),          \
+                       x.f("boundary_Y"), x.f("boundary_psi"), x.f("boundary_rho"), x.f("boundary_mu"),            \
+                       x.f("boundary_alpha"), x.f("boundary_rhoD"), x.f("boundary_hai"));                         \
+    DFMI_HIP(hipGetLastError());                                                                                  \
+  } while (0)
+  switch (x.S) {
+    case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break;
+    case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break;
+    case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break; case 13: CALL(13); break;
+    case 14: CALL(14); break; case 15: CALL(15); break; case 16: CALL(16); break;
+    default: throw Error("dfmi: thermo species count " + std::to_string(x.S) + " not instantiated (2..16)");
+  }
+#undef CALL
+}
+
+}  // namespace dfmi

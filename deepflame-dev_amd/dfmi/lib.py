@@ -1,0 +1,217 @@
+"""ctypes binding of libdfmi.so (include/dfmi.h).
+
+The library is the product: there is no CPU fallback. Importing this module on a machine
+where libdfmi.so is missing raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdfmi.so")
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libdfmi.so not found at {LIB_PATH}; run __graft_entry__.build()")
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+_P = C.c_void_p
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int)
+
+SIGNATURES = {
+    "dfmi_create": [C.POINTER(_P), C.c_int],
+    "dfmi_destroy": [_P],
+    "dfmi_last_error": [C.c_char_p, C.c_int],
+    "dfmi_set_constant_values": [_P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _IP, C.c_int, C.c_double],
+    "dfmi_set_cyclic_info": [_P, _IP],
+    "dfmi_set_comm_info": [_P, C.c_void_p, C.c_int, C.c_int, _IP],
+    "dfmi_get_unique_id": [C.c_void_p],
+    "dfmi_set_constant_indexes": [_P, _IP, _IP, _IP, _IP, C.c_int],
+    "dfmi_init_constant_fields_internal": [_P, _DP, _DP, _DP, _DP, _DP, _DP],
+    "dfmi_init_constant_fields_boundary": [_P, _DP, _DP, _DP, _DP, _IP, _IP, _IP],
+    "dfmi_set_patch_types": [_P, C.c_char_p, _IP],
+    "dfmi_set_inert_index": [_P, C.c_int],
+    "dfmi_thermo_set_coeffs": [_P, C.c_int, _DP, _DP, _DP, _DP, _DP],
+    "dfmi_thermo_load": [_P, C.c_char_p],
+    "dfmi_set_field": [_P, C.c_char_p, _DP, C.c_long, C.c_int],
+    "dfmi_get_field": [_P, C.c_char_p, _DP, C.c_long, C.c_int],
+    "dfmi_pre_time_step": [_P], "dfmi_rho_process": [_P], "dfmi_U_process": [_P], "dfmi_Y_process": [_P],
+    "dfmi_E_process": [_P], "dfmi_thermo_correct": [_P], "dfmi_thermo_update_energy": [_P],
+    "dfmi_thermo_update_rho": [_P], "dfmi_thermo_psip0": [_P], "dfmi_thermo_correct_psip_rho": [_P],
+    "dfmi_U_get_HbyA": [_P], "dfmi_p_process": [_P], "dfmi_post_time_step": [_P],
+    "dfmi_time_step": [_P, C.c_int], "dfmi_sync": [_P],
+    "dfmi_assemble": [_P, C.c_char_p],
+    "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
+    "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
+    "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
+    "dfmi_correct_boundary": [_P, C.c_char_p],
+    "dfmi_chem_set_mechanism": None,   # optional (declared if present)
+}
+
+
+def _declare(lib):
+    for name, args in SIGNATURES.items():
+        if not hasattr(lib, name):
+            continue
+        fn = getattr(lib, name)
+        fn.restype = C.c_int
+        if args is not None:
+            fn.argtypes = args
+    lib.dfmi_version.restype = C.c_char_p
+
+
+def exported_symbols() -> list:
+    return [n for n in SIGNATURES if n != "dfmi_chem_set_mechanism"] + ["dfmi_version"]
+
+
+class DfmiError(RuntimeError):
+    pass
+
+
+def _dp(a):
+    return a.ctypes.data_as(_DP)
+
+
+def _ip(a):
+    return a.ctypes.data_as(_IP)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class Context:
+    """One device-resident database (one rank, one GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = _P()
+        self._keep = []
+        self._call("dfmi_create", C.byref(h), device)
+        self.h = h
+
+    def _call(self, name, *args):
+        rc = getattr(self.lib, name)(*args)
+        if rc != 0:
+            buf = C.create_string_buffer(4096)
+            self.lib.dfmi_last_error(buf, 4096)
+            raise DfmiError(f"{name}: {buf.value.decode()}")
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.dfmi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- setup
+    def set_constant_values(self, C_, Ctot, F, B, P, nproc, patch_size, S, rdt):
+        ps = _i32(patch_size)
+        self._call("dfmi_set_constant_values", self.h, C_, Ctot, F, B, P, nproc, _ip(ps), S, float(rdt))
+
+    def set_cyclic_info(self, cyc):
+        a = _i32(cyc); self._call("dfmi_set_cyclic_info", self.h, _ip(a))
+
+    def set_comm_info(self, uid: bytes, nranks, rank, neighb):
+        a = _i32(neighb)
+        buf = C.create_string_buffer(uid, 128)
+        self._call("dfmi_set_comm_info", self.h, buf, nranks, rank, _ip(a))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load()
+        buf = C.create_string_buffer(128)
+        if lib.dfmi_get_unique_id(buf) != 0:
+            e = C.create_string_buffer(4096); lib.dfmi_last_error(e, 4096)
+            raise DfmiError(e.value.decode())
+        return buf.raw
+
+    def set_constant_indexes(self, owner, neighbour, proc_rows, proc_cols, global_offset):
+        o, n, r, c = _i32(owner), _i32(neighbour), _i32(proc_rows), _i32(proc_cols)
+        if r.size == 0:
+            r = np.zeros(1, np.int32); c = np.zeros(1, np.int32)
+        self._call("dfmi_set_constant_indexes", self.h, _ip(o), _ip(n), _ip(r), _ip(c), int(global_offset))
+
+    def init_constant_fields_internal(self, sf, mag_sf, weight, delta, volume, mesh_dist):
+        arrs = [_f64(x) for x in (sf, mag_sf, weight, delta, volume, mesh_dist)]
+        self._call("dfmi_init_constant_fields_internal", self.h, *[_dp(a) for a in arrs])
+
+    def init_constant_fields_boundary(self, bsf, bmag, bdelta, bweight, bfc, ptype_calc, ptype_extrap):
+        arrs = [_f64(x) for x in (bsf, bmag, bdelta, bweight)]
+        for i, a in enumerate(arrs):
+            if a.size == 0:
+                arrs[i] = np.zeros(3)
+        fc = _i32(bfc) if np.size(bfc) else np.zeros(1, np.int32)
+        pc, pe = _i32(ptype_calc), _i32(ptype_extrap)
+        self._call("dfmi_init_constant_fields_boundary", self.h, *[_dp(a) for a in arrs], _ip(fc), _ip(pc), _ip(pe))
+
+    def set_patch_types(self, field, types):
+        a = _i32(types); self._call("dfmi_set_patch_types", self.h, field.encode(), _ip(a))
+
+    def set_inert_index(self, i):
+        self._call("dfmi_set_inert_index", self.h, int(i))
+
+    def thermo_set_coeffs(self, t):
+        arrs = [_f64(x) for x in (t.W, t.nasa, t.visc, t.cond, t.bdiff)]
+        self._call("dfmi_thermo_set_coeffs", self.h, t.S, *[_dp(a) for a in arrs])
+
+    # --- fields
+    def set_field(self, name, arr, layout=0):
+        a = _f64(arr)
+        count = a.shape[0] if (layout == 1 and a.ndim == 2) else (a.shape[-1] if a.ndim == 2 else a.shape[0])
+        self._call("dfmi_set_field", self.h, name.encode(), _dp(a), int(count), layout)
+
+    def get_field(self, name, shape, layout=0):
+        out = np.empty(shape, dtype=np.float64)
+        count = shape[0] if (layout == 1 and len(shape) == 2) else (shape[-1] if len(shape) == 2 else shape[0])
+        self._call("dfmi_get_field", self.h, name.encode(), _dp(out), int(count), layout)
+        return out
+
+    def get_matrix(self, eqn, part, n):
+        out = np.empty(n, dtype=np.float64)
+        self._call("dfmi_get_matrix", self.h, eqn.encode(), part.encode(), _dp(out), int(n))
+        return out
+
+    # --- processes
+    def call(self, name, *args):
+        self._call("dfmi_" + name, self.h, *args)
+
+    def assemble(self, eqn):
+        self._call("dfmi_assemble", self.h, eqn.encode())
+
+    def correct_boundary(self, field):
+        self._call("dfmi_correct_boundary", self.h, field.encode())
+
+    def set_solver(self, eqn, max_iter, tol, abs_tol=0.0):
+        self._call("dfmi_set_solver", self.h, eqn.encode(), int(max_iter), float(tol), float(abs_tol))
+
+    def solver_stats(self, eqn):
+        it = C.c_int(); r0 = C.c_double(); rel = C.c_double()
+        self._call("dfmi_solver_stats", self.h, eqn.encode(), C.byref(it), C.byref(r0), C.byref(rel))
+        return it.value, r0.value, rel.value
+
+    def time_step(self, n_corr=2):
+        self._call("dfmi_time_step", self.h, int(n_corr))
+
+    def sync(self):
+        self._call("dfmi_sync", self.h)

@@ -1,0 +1,125 @@
+/* dfmi.h -- C ABI of the MI355X-native dfLowMachFoam GPU hot path.
+ *
+ * Drop-in replacement for the C++ class surface of the reference libdfMatrix.so
+ * (show-me-code/deepflame-dev src_gpu/ *.H headers, driven from applications/solvers/dfLowMachFoam/
+ * createGPUSolver.H and *_GPU.H). Each entry point names the reference method it replaces.
+ *
+ * Conventions (same as the reference):
+ *  - host arrays are copied during the call, never retained;
+ *  - vector/tensor fields: layout DFMI_AOS = OpenFOAM [n][3] / [n][9] (the reference permutes
+ *    with permute_vector_h2d, dfMatrixOpBase.cu:18-38), DFMI_SOA = [3][n] / [9][n];
+ *  - species fields are species-major [S][n] (createGPUSolver.H:482-500);
+ *  - boundary arrays are concatenated in OpenFOAM patch order; a processor/processorCyclic patch
+ *    takes 2n slots [neighbour values | patch-internal values] (createGPUSolver.H:118-123);
+ *  - patch type codes: zeroGradient 0, fixedValue 1, coupled 2, empty 3, gradientEnergy 4,
+ *    calculated 5, cyclic 6, processor 7, extrapolated 8, fixedEnergy 9, processorCyclic 10
+ *    (dfMatrixDataBase.H:81-93);
+ *  - every call returns 0 on success, non-zero on error, and never exits the process
+ *    (the reference exit()s, dfMatrixDataBase.H:40-50); dfmi_last_error() gives the message.
+ */
+#ifndef DFMI_H
+#define DFMI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dfmi_ctx dfmi_ctx;
+
+enum { DFMI_SOA = 0, DFMI_AOS = 1 };
+
+/* ---- lifetime ------------------------------------------------------------------------- */
+/* dfMatrixDataBase(), prepareCudaResources (dfMatrixDataBase.cu:88,103): binds `device`, one stream */
+int dfmi_create(dfmi_ctx** ctx, int device);
+/* ~dfMatrixDataBase + cleanCudaResources (dfMatrixDataBase.cu:90,107); frees all device memory */
+int dfmi_destroy(dfmi_ctx* ctx);
+/* copy of the last error message of this thread; returns its length */
+int dfmi_last_error(char* buf, int len);
+/* library version string */
+const char* dfmi_version(void);
+
+/* ---- dfMatrixDataBase setup (createGPUBase, createGPUSolver.H:103-351) ------------------- */
+/* dfMatrixDataBase::setConstantValues (dfMatrixDataBase.cu:114-147); rdelta_t = 1/deltaT */
+int dfmi_set_constant_values(dfmi_ctx* ctx, int num_cells, int num_total_cells, int num_surfaces,
+                             int num_boundary_surfaces, int num_patches, int num_proc_surfaces,
+                             const int* patch_size, int num_species, double rdelta_t);
+/* dfMatrixDataBase::setCyclicInfo (dfMatrixDataBase.cu:179-182): partner patch index or -1 */
+int dfmi_set_cyclic_info(dfmi_ctx* ctx, const int* cyclic_neighbor);
+/* dfMatrixDataBase::setCommInfo + ncclInit (dfMatrixDataBase.cu:92-101, dfNcclBase.cu:23-65):
+ * nccl_unique_id is the 128-byte RCCL id (rank 0 creates it, the caller broadcasts it),
+ * neighb_proc_no[num_patches] the peer rank of each processor patch (-1 otherwise) */
+int dfmi_set_comm_info(dfmi_ctx* ctx, const void* nccl_unique_id, int nranks, int rank,
+                       const int* neighb_proc_no);
+/* rank-0 helper: create a fresh RCCL unique id (128 bytes) */
+int dfmi_get_unique_id(void* nccl_unique_id_out);
+/* dfMatrixDataBase::setConstantIndexes (dfMatrixDataBase.cu:184-277) */
+int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighbour, const int* proc_rows,
+                              const int* proc_cols, int global_offset);
+/* dfMatrixDataBase::initConstantFieldsInternal (dfMatrixDataBase.cu:316-333); sf/mesh_distance AoS */
+int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const double* mag_sf,
+                                       const double* weight, const double* delta_coeffs,
+                                       const double* volume, const double* mesh_distance);
+/* dfMatrixDataBase::initConstantFieldsBoundary (dfMatrixDataBase.cu:335-351); boundary_sf AoS */
+int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* boundary_sf, const double* boundary_mag_sf,
+                                       const double* boundary_delta_coeffs, const double* boundary_weight,
+                                       const int* boundary_face_cell, const int* patch_type_calculated,
+                                       const int* patch_type_extrapolated);
+
+/* ---- per-equation patch types ------------------------------------------------------------ */
+/* dfUEqn/dfYEqn/dfEEqn/dfpEqn/dfRhoEqn/dfThermo::setConstantFields (e.g. dfUEqn.cu:364-379,
+ * dfEEqn.cu setConstantFields, dfThermo.cu setConstantFields). field in
+ * {"U","p","he","K","Y","T","rho"}; patch_type[num_patches] */
+int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type);
+/* dfYEqn inertIndex (YEqn.H:119-131) */
+int dfmi_set_inert_index(dfmi_ctx* ctx, int inert_index);
+
+/* ---- thermo (dfThermo::setConstantValue, dfThermo.cu:361-435) ---------------------------- */
+/* coefficient table in memory: W[S], nasa[S][15], visc[S][5], cond[S][5], bdiff[S][S][5] */
+int dfmi_thermo_set_coeffs(dfmi_ctx* ctx, int num_species, const double* W, const double* nasa,
+                           const double* visc, const double* cond, const double* bdiff);
+/* read the reference's binary thermo_<mech>.txt */
+int dfmi_thermo_load(dfmi_ctx* ctx, const char* thermo_coeff_file);
+
+/* ---- fields (initNonConstantFields*, getFieldPointer dfMatrixDataBase.cu:521-539) ---------- */
+/* names: cells  rho rho_old p p_old he T K K_old psi mu alpha dpdt rAU diffAlphaD psip0
+ *        vector U U_old HbyA hDiffCorrFlux sumYDiffError     species Y rhoD hai RR
+ *        faces  phi phi_old phiUc rhorAUf phiHbyA
+ *        boundary_<name> for the boundary counterparts. count = values per component. */
+int dfmi_set_field(dfmi_ctx* ctx, const char* name, const double* host, long count, int layout);
+int dfmi_get_field(dfmi_ctx* ctx, const char* name, double* host, long count, int layout);
+
+/* ---- one outer iteration (dfLowMachFoam.C:284-531, pEqn_GPU.H) --------------------------- */
+int dfmi_pre_time_step(dfmi_ctx* ctx);          /* dfMatrixDataBase::preTimeStep (:503-517) */
+int dfmi_rho_process(dfmi_ctx* ctx);            /* dfRhoEqn::process (dfRhoEqn.cu:41-92) */
+int dfmi_U_process(dfmi_ctx* ctx);              /* dfUEqn::process (dfUEqn.cu:487-689) */
+int dfmi_Y_process(dfmi_ctx* ctx);              /* dfYEqn::process (dfYEqn.cu:443-695); RR from dfmi_set_field("RR") or the chemistry */
+int dfmi_E_process(dfmi_ctx* ctx);              /* dfEEqn::process (dfEEqn.cu:108-264) */
+int dfmi_thermo_correct(dfmi_ctx* ctx);         /* dfThermo::correctThermo (dfThermo.cu:572-671) */
+int dfmi_thermo_update_energy(dfmi_ctx* ctx);   /* he, psi, rho, transport from T (dfThermo::updateEnergy) */
+int dfmi_thermo_update_rho(dfmi_ctx* ctx);      /* dfThermo::updateRho (:673-679) */
+int dfmi_thermo_psip0(dfmi_ctx* ctx);           /* dfThermo::psip0 (:681-686) */
+int dfmi_thermo_correct_psip_rho(dfmi_ctx* ctx);/* dfThermo::correctPsipRho (:688-695) */
+int dfmi_U_get_HbyA(dfmi_ctx* ctx);             /* dfUEqn::getHbyA (dfUEqn.cu:824-834) */
+int dfmi_p_process(dfmi_ctx* ctx);              /* dfpEqn::process (dfpEqn.cu:379-546) */
+int dfmi_post_time_step(dfmi_ctx* ctx);         /* dfMatrixDataBase::postTimeStep (:519) */
+/* the whole loop body above with n_corr pressure correctors */
+int dfmi_time_step(dfmi_ctx* ctx, int n_corr);
+int dfmi_sync(dfmi_ctx* ctx);
+/* correct_boundary_conditions_{scalar,vector} (dfMatrixOpBase.cu:2402-2491) for field in
+ * {"U","p","he","T","rho","K","Y"} using that field's patch types */
+int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field);
+
+/* ---- matrix inspection (the reference DEBUG_CHECK_LDU / compareResult path, dfYEqn.cu:566-572) */
+/* eqn in {"rho","U","Y","E","p"}: run that equation's assembly only (no solve) */
+int dfmi_assemble(dfmi_ctx* ctx, const char* eqn);
+/* part in {"lower","upper","diag","source","source_solve","internal_coeffs","boundary_coeffs"} */
+int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count);
+/* solver controls (amgxUOptions / amgxpOptions): eqn in {"U","Y","E","p"} */
+int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, double abs_tol);
+/* last solve: iterations and final relative residual */
+int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFMI_H */
