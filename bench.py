@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""dfLowMachFoam outer-iteration throughput on MI355X (BASELINE.json metric: cell-updates/s).
+
+One step = one dfLowMachFoam outer iteration (nOuter = 1, nCorr = 2: rhoEqn, UEqn + solve,
+YEqn + solves, EEqn + solve, thermo correct, 2 x {HbyA, pEqn + solve, flux/U/K update, rhoEqn})
+over the whole mesh, all inputs resident in HBM. Workload: BASELINE.json configs[2], the 3D
+periodic box of 128^3 = 2,097,152 hex cells (reacting Taylor-Green vortex, H2/air).
+
+N GPUs (torchrun, one process per GPU): every rank owns its own 128^3 box (weak scaling).
+
+Output: one JSON line (rank 0) with the driver's contract fields plus
+  roofline      -- the dominant kernel's algorithmic bytes / its mean HIP-event duration,
+  cpu_baseline  -- the CPU oracle (sequential C++ restatement + direct sparse solves) timed on
+                   a bounded sample of the same workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+
+MECHS = {
+    "es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt"),
+}
+
+
+def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int) -> float:
+    """Bytes a kernel must move at minimum (each input read once, each output written once;
+    fp64 values, int32 indices). DESIGN.md 'Kernels' lists the per-unit figures."""
+    Sa = S - 1                                     # solved species (inert excluded)
+    if kernel == "k_y_assemble":
+        # cells: Y, rhoD, RR in (Sa each), rho, rho_old, V in, diag/source out (Sa each)
+        # faces: phi, phiUc, w, deltaCoeffs, magSf, owner, neighbour in; lower/upper out (Sa each)
+        return C * (8 * 5 * Sa + 24) + F * (5 * 8 + 8 + 16 * Sa) + B * (8 * 8 + 16 * Sa)
+    if kernel == "k_cg_spmv":
+        # cells: p, dS in, q out; faces: lower, upper, owner, neighbour
+        return C * 24 + F * 24 + B * 16
+    if kernel == "k_bcg_spmv":
+        return C * 24 + F * 24 + B * 16
+    if kernel == "k_thermo_cells":
+        # T, he, p in; Y in (S); T, psi, rho, mu, alpha out; rhoD, hai out (S each)
+        return C * 8 * (3 + S + 5 + 2 * S)
+    raise KeyError(kernel)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
+    ap.add_argument("--mech", default="es80", choices=sorted(MECHS))
+    ap.add_argument("--ncorr", type=int, default=2)
+    ap.add_argument("--dt", type=float, default=1e-7)
+    ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
+    ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, table, ym, inert):
+    """The oracle (TEST INFRASTRUCTURE, the checker) timed on a bounded sample on the host."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from dfmi.mesh import hex_box
+    from dfmi import case
+    n = args.cpu_n
+    m = hex_box(n, n, n)
+    pt = case.default_patch_types(m)
+    f = case.tgv_fields(m, ym["species"])
+    st = host_state(m, table, f)
+    o = O.Oracle(m, table, st, pt, inert, 1.0 / args.dt)
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        o.time_step(args.ncorr)
+        steps += 1
+        if time.perf_counter() - t0 > 10.0 or steps >= 5:
+            break
+    el = time.perf_counter() - t0
+    return {"value": m.n_cells * steps / el, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/df_oracle.cpp (sequential C++ restatement) + scipy spsolve, {n}^3 = {m.n_cells} "
+                      f"cells periodic TGV, {table.S} species, {steps} outer iterations in {el:.1f} s"}
+
+
+def host_state(m, table, f):
+    """Initial state computed by the oracle's own thermo (no GPU) for the CPU baseline."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from dfmi import case
+    C_, F, B, S = m.n_cells, m.n_faces, m.n_boundary_slots, table.S
+    st = {}
+    for nme in case.SCALARS:
+        st[nme] = np.zeros(C_); st["boundary_" + nme] = np.zeros(B)
+    for nme in case.VECTORS:
+        st[nme] = np.zeros((3, C_)); st["boundary_" + nme] = np.zeros((3, B))
+    for nme in case.SPECIES:
+        st[nme] = np.zeros((S, C_)); st["boundary_" + nme] = np.zeros((S, B))
+    for nme in case.FACES:
+        st[nme] = np.zeros(F); st["boundary_" + nme] = np.zeros(B)
+    st["T"] = f["T"].copy(); st["p"] = f["p"].copy(); st["U"] = f["U"].copy(); st["Y"] = f["Y"].copy()
+    for k in ("T", "p", "U", "Y"):
+        st["boundary_" + k] = case.boundary_values(m, st[k])
+    o = O.Oracle(m, table, st, case.default_patch_types(m), 0, 1e7)
+    o.thermo_correct(True)
+    s = {k: v.copy() for k, v in o.arr.items() if k in st}
+    s["phi"], s["boundary_phi"] = case.face_flux(m, s["rho"], s["U"], s["boundary_rho"], s["boundary_U"])
+    s["K"] = 0.5 * (s["U"] ** 2).sum(axis=0)
+    s["boundary_K"] = 0.5 * (s["boundary_U"] ** 2).sum(axis=0)
+    return s
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch                                   # loads the HIP runtime first: one runtime per process
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    golden = os.path.join(ROOT, "tests", "golden")
+    yml, tab = MECHS[args.mech]
+    ym = read_yaml_mechanism(os.path.join(golden, yml))
+    table = read_thermo_table(os.path.join(golden, tab), ym["species"])
+    inert = ym["species"].index("N2")
+
+    n = args.n
+    m = hex_box(n, n, n)
+    ctx = Context(local)
+    case.setup_context(ctx, m, table, inert, args.dt)
+    f = case.tgv_fields(m, ym["species"])
+    case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
+    del f
+
+    for _ in range(args.warmup):
+        ctx.time_step(args.ncorr)
+    ctx.sync()
+    if world > 1:
+        dist.barrier()
+    ctx.kernel_timer(args.kernel)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.time_step(args.ncorr)
+    ctx.sync()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    k_ms, k_n = ctx.kernel_time()
+    ctx.kernel_timer("")
+    el = t1 - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    stats = {e: ctx.solver_stats(e) for e in ("U", "Y", "E", "p")}
+    T = ctx.get_field("T", (m.n_cells,))
+    finite = bool(np.isfinite(T).all())
+
+    cells_total = m.n_cells * world
+    value = cells_total * args.steps / el
+    kbytes = algorithmic_bytes(args.kernel, m.n_cells, m.n_faces, m.n_boundary_slots, table.S)
+    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
+    achieved = kbytes / k_avg_s / 1e9 if k_n else None
+    out = {
+        "metric": "cell-updates/s (dfLowMachFoam outer iter)",
+        "value": value,
+        "unit": "cell-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (reacting Taylor-Green vortex initial state, hex box generated in-process)",
+        "config": {"workload": f"dfLowMachFoam 3D periodic box {n}^3 = {m.n_cells} hex cells per GPU, "
+                               f"H2/air {table.S} species ({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
+                   "cells_per_gpu": m.n_cells, "species": table.S, "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
+        "solver_iters": {e: s[0] for e, s in stats.items()},
+        "finite": finite,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args, table, ym, inert)
+        out["cpu_baseline"]["ratio"] = value / out["cpu_baseline"]["value"]
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -448,6 +448,32 @@ int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
   });
 }
 
+int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernel) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.ktimer.target = kernel ? kernel : "";
+    x.ktimer.used = 0;
+  });
+}
+
+int dfmi_kernel_time(dfmi_ctx* ctx, double* total_ms, int* launches) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    double tot = 0;
+    KernelTimer& k = x.ktimer;
+    for (size_t i = 0; i + 1 < k.used; i += 2) {
+      float ms = 0;
+      DFMI_HIP(hipEventElapsedTime(&ms, k.pool[i], k.pool[i + 1]));
+      tot += ms;
+    }
+    *total_ms = tot;
+    *launches = (int)(k.used / 2);
+    k.used = 0;
+  });
+}
+
 int dfmi_sync(dfmi_ctx* ctx) { return guard([&] { DFMI_HIP(hipStreamSynchronize(ctx->x.stream)); }); }
 
 int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {

@@ -56,6 +56,22 @@ struct Thermo {
 
 struct Halo;   // RCCL processor-patch exchange (halo.cpp)
 
+// HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)
+struct KernelTimer {
+  std::string target;
+  std::vector<hipEvent_t> pool;   // pairs (start, end)
+  size_t used = 0;
+  ~KernelTimer() { for (auto e : pool) (void)hipEventDestroy(e); }
+  hipEvent_t next() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      DFMI_HIP(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -84,6 +100,7 @@ struct Ctx {
   // scratch
   DevBuf<double> scratch;
   Halo* halo = nullptr;          // owned; freed by halo_destroy()
+  KernelTimer ktimer;
   ~Ctx();
   int n_corr = 2;
 
@@ -111,6 +128,21 @@ struct Ctx {
     DFMI_CHECK(it != ptype.end(), "patch types not set for field '" + field + "'");
     return it->second;
   }
+};
+
+// Records a start/end event pair around a launch when `name` is the armed kernel.
+struct KScope {
+  Ctx& x;
+  bool on;
+  static bool match(const std::string& t, const char* name) {   // template arguments ignored
+    size_t n = 0;
+    while (name[n] && name[n] != '<') ++n;
+    return !t.empty() && t.size() == n && t.compare(0, n, name, n) == 0;
+  }
+  KScope(Ctx& c, const char* name) : x(c), on(match(c.ktimer.target, name)) {
+    if (on) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream));
+  }
+  ~KScope() noexcept(false) { if (on) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream)); }
 };
 
 // ---- launchers (fv_kernels.hip)

@@ -735,7 +735,7 @@ template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim
 
 // ====================================================================== launchers
 #define LAUNCH(kernel, n, ...) \
-  do { if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
+  do { KScope _ks(x, #kernel); if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
        DFMI_HIP(hipGetLastError()); } while (0)
 
 void k_bc_correct(Ctx& x, const char* tf, double* vf, double* bvf, int ncomp) {

@@ -366,9 +366,9 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk, nsys), bl(TPB);
-  hipLaunchKernelGGL(k_setup, g, bl, 0, x.stream, m, ty, q, dS, rhs, smap);
-  hipLaunchKernelGGL(k_bcg_init, g, bl, 0, x.stream, m, ty, q, smap, dS, rhs, r, r0, p, v, partial, nblk);
-  hipLaunchKernelGGL(k_bcg_init_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol);
+  { KScope _ks(x, "k_setup"); hipLaunchKernelGGL(k_setup, g, bl, 0, x.stream, m, ty, q, dS, rhs, smap); }
+  { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init, g, bl, 0, x.stream, m, ty, q, smap, dS, rhs, r, r0, p, v, partial, nblk); }
+  { KScope _ks(x, "k_bcg_init_fin"); hipLaunchKernelGGL(k_bcg_init_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol); }
   DFMI_HIP(hipGetLastError());
   W.hscal.resize(nsys * 8);
   int it = 0;
@@ -376,14 +376,14 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   bool synced = false;
   while (it < cfg.max_iter) {
     for (int k = 0; k < check && it < cfg.max_iter; ++k, ++it) {
-      hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, (int)C, W.scal.p, r, p, v, dS, phat);
-      hipLaunchKernelGGL(k_bcg_spmv<1>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, phat, v, r0, partial, nblk);
-      hipLaunchKernelGGL(k_bcg_alpha, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p);
-      hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, (int)C, W.scal.p, r, v, dS, sv, shat);
-      hipLaunchKernelGGL(k_bcg_spmv<2>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, shat, t, sv, partial, nblk);
-      hipLaunchKernelGGL(k_bcg_omega, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p);
-      hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, (int)C, q, smap, W.scal.p, phat, shat, sv, t, r, r0, partial, nblk);
-      hipLaunchKernelGGL(k_bcg_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter);
+      { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, (int)C, W.scal.p, r, p, v, dS, phat); }
+      { KScope _ks(x, "k_bcg_spmv"); hipLaunchKernelGGL(k_bcg_spmv<1>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, phat, v, r0, partial, nblk); }
+      { KScope _ks(x, "k_bcg_alpha"); hipLaunchKernelGGL(k_bcg_alpha, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p); }
+      { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, (int)C, W.scal.p, r, v, dS, sv, shat); }
+      { KScope _ks(x, "k_bcg_spmv"); hipLaunchKernelGGL(k_bcg_spmv<2>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, shat, t, sv, partial, nblk); }
+      { KScope _ks(x, "k_bcg_omega"); hipLaunchKernelGGL(k_bcg_omega, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p); }
+      { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, (int)C, q, smap, W.scal.p, phat, shat, sv, t, r, r0, partial, nblk); }
+      { KScope _ks(x, "k_bcg_fin"); hipLaunchKernelGGL(k_bcg_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter); }
     }
     DFMI_HIP(hipGetLastError());
     DFMI_HIP(hipMemcpyAsync(W.hscal.data(), W.scal.p, nsys * 8 * sizeof(double), hipMemcpyDeviceToHost, x.stream));
@@ -422,20 +422,20 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk), bl(TPB);
-  hipLaunchKernelGGL(k_setup, dim3(nblk, 1), bl, 0, x.stream, m, ty, q, dS, rhs, (const int*)nullptr);
-  hipLaunchKernelGGL(k_cg_init, g, bl, 0, x.stream, m, ty, q, dS, rhs, r, z, p, partial, nblk);
-  hipLaunchKernelGGL(k_cg_init_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.abs_tol);
+  { KScope _ks(x, "k_setup"); hipLaunchKernelGGL(k_setup, dim3(nblk, 1), bl, 0, x.stream, m, ty, q, dS, rhs, (const int*)nullptr); }
+  { KScope _ks(x, "k_cg_init"); hipLaunchKernelGGL(k_cg_init, g, bl, 0, x.stream, m, ty, q, dS, rhs, r, z, p, partial, nblk); }
+  { KScope _ks(x, "k_cg_init_fin"); hipLaunchKernelGGL(k_cg_init_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.abs_tol); }
   DFMI_HIP(hipGetLastError());
   W.hscal.resize(8);
   int it = 0;
   const int check = 8;
   while (it < cfg.max_iter) {
     for (int k = 0; k < check && it < cfg.max_iter; ++k, ++it) {
-      hipLaunchKernelGGL(k_cg_spmv, g, bl, 0, x.stream, m, ty, q, W.scal.p, dS, p, qv, partial, nblk);
-      hipLaunchKernelGGL(k_cg_alpha, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p);
-      hipLaunchKernelGGL(k_cg_x, g, bl, 0, x.stream, (int)C, xsol, W.scal.p, p, qv, r, z, dS, partial, nblk);
-      hipLaunchKernelGGL(k_cg_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter);
-      hipLaunchKernelGGL(k_cg_p, g, bl, 0, x.stream, (int)C, W.scal.p, z, p);
+      { KScope _ks(x, "k_cg_spmv"); hipLaunchKernelGGL(k_cg_spmv, g, bl, 0, x.stream, m, ty, q, W.scal.p, dS, p, qv, partial, nblk); }
+      { KScope _ks(x, "k_cg_alpha"); hipLaunchKernelGGL(k_cg_alpha, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p); }
+      { KScope _ks(x, "k_cg_x"); hipLaunchKernelGGL(k_cg_x, g, bl, 0, x.stream, (int)C, xsol, W.scal.p, p, qv, r, z, dS, partial, nblk); }
+      { KScope _ks(x, "k_cg_fin"); hipLaunchKernelGGL(k_cg_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter); }
+      { KScope _ks(x, "k_cg_p"); hipLaunchKernelGGL(k_cg_p, g, bl, 0, x.stream, (int)C, W.scal.p, z, p); }
     }
     DFMI_HIP(hipGetLastError());
     DFMI_HIP(hipMemcpyAsync(W.hscal.data(), W.scal.p, 8 * sizeof(double), hipMemcpyDeviceToHost, x.stream));

@@ -201,9 +201,9 @@ void thermo_correct(Ctx& x, bool from_T) {
   MeshView m = x.view();
 #define CALL(NS)                                                                                                   \
   do {                                                                                                            \
-    if (x.C > 0) hipLaunchKernelGGL(k_thermo_cells<NS>, dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t, \
+    if (x.C > 0) { KScope _ks(x, "k_thermo_cells"); hipLaunchKernelGGL(k_thermo_cells<NS>, dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t, \
                        (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"),    \
-                       x.f("alpha"), x.f("rhoD"), x.f("hai"));                                                    \
+                       x.f("alpha"), x.f("rhoD"), x.f("hai")); }                                                  \
     DFMI_HIP(hipGetLastError());                                                                                  \
     if (x.B > 0) hipLaunchKernelGGL(k_thermo_slots<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t,  \
                        x.st("T"), (int)from_T, x.f("T"), x.f("he"), x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), \

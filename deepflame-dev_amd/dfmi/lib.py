@@ -56,6 +56,8 @@ SIGNATURES = {
     "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
+    "dfmi_kernel_timer": [_P, C.c_char_p],
+    "dfmi_kernel_time": [_P, _DP, _IP],
     "dfmi_chem_set_mechanism": None,   # optional (declared if present)
 }
 
@@ -212,6 +214,16 @@ class Context:
 
     def time_step(self, n_corr=2):
         self._call("dfmi_time_step", self.h, int(n_corr))
+
+    def kernel_timer(self, kernel: str):
+        """Arm HIP-event timing of every launch of `kernel` on this context's stream."""
+        self._call("dfmi_kernel_timer", self.h, kernel.encode())
+
+    def kernel_time(self):
+        """(total_ms, launches) of the armed kernel since the last call."""
+        ms = C.c_double(); n = C.c_int()
+        self._call("dfmi_kernel_time", self.h, C.byref(ms), C.byref(n))
+        return ms.value, n.value
 
     def sync(self):
         self._call("dfmi_sync", self.h)

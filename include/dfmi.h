@@ -119,6 +119,14 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
 
+/* ---- kernel timing (the reference's TICK_START_EVENT / TICK_END_EVENT cudaEvent pairs,
+ * src_gpu/dfMatrixOpBase.H:46-60): arm HIP-event timing of every launch of one kernel
+ * (name as in the source, e.g. "k_y_assemble"; "" disarms), recorded on the context stream */
+int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernel);
+/* synchronise and return the summed duration and count of the armed kernel's launches since
+ * the last call (then reset) */
+int dfmi_kernel_time(dfmi_ctx* ctx, double* total_ms, int* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+ROOT = ROOT
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
