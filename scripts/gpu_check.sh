@@ -11,7 +11,7 @@ timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py ${BENCH_ARGS} > gpurun_out/b
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
 [ -n "$SKIP_PROF" ] && exit 0
 export TMPDIR=/tmp
-timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py ${BENCH_ARGS} --no-cpu > gpurun_out/prof.log 2>&1
+timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py ${BENCH_ARGS} --no-cpu > gpurun_out/prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log
 find gpurun_out/prof -name "*stats*" | head
 exit $rc
