@@ -33,7 +33,7 @@ def main(d, out=None):
              f"# total kernel time {tot / 1e6:.3f} ms",
              "share%,calls,total_ms,avg_us,min_us,max_us,kernel"]
     for n, k, t, a, mn, mx in rows:
-        short = n.split("(")[0].replace("dfmi::(anonymous namespace)::", "").replace("void ", "")
+        short = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         lines.append(f"{100 * t / tot:.2f},{k},{t / 1e6:.4f},{a / 1e3:.2f},{mn / 1e3:.2f},{mx / 1e3:.2f},{short}")
     txt = "\n".join(lines) + "\n"
     if out:
