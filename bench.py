@@ -6,7 +6,9 @@ YEqn + solves, EEqn + solve, thermo correct, 2 x {HbyA, pEqn + solve, flux/U/K u
 over the whole mesh, all inputs resident in HBM. Workload: BASELINE.json configs[2], the 3D
 periodic box of 128^3 = 2,097,152 hex cells (reacting Taylor-Green vortex, H2/air).
 
-N GPUs (torchrun, one process per GPU): every rank owns its own 128^3 box (weak scaling).
+N GPUs (torchrun, one process per GPU): the box is decomposed 2x1x1 / 2x2x1 / 2x2x2 (decomposePar-
+style blocks), every rank owns a 128^3 block (weak scaling: N=8 is BASELINE config 5, 256^3 = 16.8M
+cells), processor-patch halos and solver reductions go over RCCL (xGMI).
 
 Output: one JSON line (rank 0) with the driver's contract fields plus
   roofline      -- the dominant kernel's algorithmic bytes / its mean HIP-event duration,
@@ -58,7 +60,7 @@ def parse():
     ap.add_argument("--n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
     ap.add_argument("--mech", default="es80", choices=sorted(MECHS))
     ap.add_argument("--ncorr", type=int, default=2)
-    ap.add_argument("--dt", type=float, default=1e-7)
+    ap.add_argument("--dt", type=float, default=1e-6)
     ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -142,9 +144,19 @@ def main():
     inert = ym["species"].index("N2")
 
     n = args.n
-    m = hex_box(n, n, n)
+    decomp = {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}.get(world)
+    if decomp is None:
+        decomp = (world, 1, 1)
+    L = 6.283185307179586e-3
+    m = hex_box(n * decomp[0], n * decomp[1], n * decomp[2], lengths=(L * decomp[0], L * decomp[1], L * decomp[2]),
+                decomp=decomp, rank=rank)
     ctx = Context(local)
-    case.setup_context(ctx, m, table, inert, args.dt)
+    comm = None
+    if world > 1:
+        uid = [Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = {"uid": uid[0], "nranks": world, "rank": rank}
+    case.setup_context(ctx, m, table, inert, args.dt, comm=comm)
     f = case.tgv_fields(m, ym["species"])
     case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
     del f
@@ -191,9 +203,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reacting Taylor-Green vortex initial state, hex box generated in-process)",
-        "config": {"workload": f"dfLowMachFoam 3D periodic box {n}^3 = {m.n_cells} hex cells per GPU, "
-                               f"H2/air {table.S} species ({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
-                   "cells_per_gpu": m.n_cells, "species": table.S, "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "config": {"workload": f"dfLowMachFoam 3D periodic box {n * decomp[0]}x{n * decomp[1]}x{n * decomp[2]} = "
+                               f"{cells_total} hex cells ({m.n_cells} per GPU), H2/air {table.S} species "
+                               f"({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
+                   "cells_per_gpu": m.n_cells, "species": table.S,
+                   "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
+                   else "single"},
         "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
                      "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},

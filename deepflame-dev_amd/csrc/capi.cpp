@@ -154,6 +154,8 @@ void require_ready(Ctx& x) {
   DFMI_CHECK(x.have_sizes && x.have_topo && x.have_geom && x.have_bgeom, "mesh not fully initialised");
 }
 
+void maybe_setup_halo(Ctx& x);
+
 // ---- equation drivers
 void do_U(Ctx& x) {
   u_assemble(x);
@@ -251,10 +253,12 @@ int dfmi_set_cyclic_info(dfmi_ctx* ctx, const int* cyclic_neighbor) {
 
 int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighbour, const int* proc_rows,
                               const int* proc_cols, int global_offset) {
-  (void)proc_rows; (void)proc_cols; (void)global_offset;   // global CSR ids are an AmgX concern; halos use patches
+  (void)proc_rows;   // global CSR row ids are an AmgX concern; the halo pairs patches by procCols
   return guard([&] {
     Ctx& x = ctx->x;
     DFMI_CHECK(x.have_sizes, "call dfmi_set_constant_values first");
+    x.global_offset = global_offset;
+    x.h_proc_cols.assign(proc_cols, proc_cols + x.nproc_faces);
     const int C = x.C, F = x.F;
     x.h_own.assign(owner, owner + F);
     x.h_nei.assign(neighbour, neighbour + F);
@@ -323,6 +327,7 @@ int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* bsf, const d
     set_ptype(x, "extrapolated", ptype_extrap);
     DFMI_HIP(hipStreamSynchronize(x.stream));
     x.have_bgeom = true;
+    maybe_setup_halo(x);
   });
 }
 
@@ -444,6 +449,7 @@ int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
     else if (f == "U") k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
     else if (f == "p" || f == "he" || f == "T" || f == "rho" || f == "K") k_bc_correct(x, f.c_str(), x.f(f), x.f("boundary_" + f), 1);
     else throw Error("dfmi_correct_boundary: unsupported field '" + f + "'");
+    halo_fields(x, {f.c_str()});
     DFMI_HIP(hipStreamSynchronize(x.stream));
   });
 }
@@ -535,10 +541,43 @@ int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, 
   });
 }
 
-int dfmi_set_comm_info(dfmi_ctx* ctx, const void* uid, int nranks, int rank, const int* neighb) {
-  (void)uid; (void)nranks; (void)rank; (void)neighb;
-  return guard([&] { DFMI_CHECK(false, "RCCL halo not built in this library"); });
+namespace {
+void set_comm(Ctx& x, int nranks, int rank, const int* neighb) {
+  DFMI_CHECK(x.have_sizes, "call dfmi_set_constant_values first");
+  DFMI_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / nranks");
+  x.nranks = nranks;
+  x.rank = rank;
+  x.peer.assign(neighb, neighb + x.P);
 }
-int dfmi_get_unique_id(void* out) { (void)out; return guard([&] { DFMI_CHECK(false, "RCCL halo not built"); }); }
+// the exchange lists need the boundary topology: built now, or at the end of
+// dfmi_init_constant_fields_boundary (every rank reaches both points in the same order)
+void maybe_setup_halo(Ctx& x) {
+  if (!x.halo || !x.have_bgeom) return;
+  int nproc = 0;
+  for (int p = 0; p < x.P; ++p) if (x.pkind[p] == 2) nproc += x.psize[p];
+  DFMI_CHECK(nproc == x.nproc_faces, "num_proc_surfaces differs from the processor patch sizes");
+  halo_setup(x);
+}
+}  // namespace
+
+int dfmi_set_comm_info(dfmi_ctx* ctx, const void* uid, int nranks, int rank, const int* neighb) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    set_comm(x, nranks, rank, neighb);
+    halo_init_rccl(x, uid, nranks, rank);
+    maybe_setup_halo(x);
+  });
+}
+
+int dfmi_set_comm_local(dfmi_ctx* ctx, int hub_id, int nranks, int rank, const int* neighb) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    set_comm(x, nranks, rank, neighb);
+    halo_init_local(x, hub_id, nranks, rank);
+    maybe_setup_halo(x);
+  });
+}
+
+int dfmi_get_unique_id(void* out) { return guard([&] { rccl_unique_id(out); }); }
 
 }  // extern "C"

@@ -99,7 +99,24 @@ struct Ctx {
   Thermo thermo;
   // scratch
   DevBuf<double> scratch;
+  // domain decomposition (halo.cpp): processor patches exchange [neighbour n] slot values
+  int nranks = 1, rank = 0, global_offset = 0;
+  std::vector<int> h_proc_cols;  // procCols: global id of the cell across each processor face (patch order)
+  int H = 0;                     // processor faces = halo values per component
+  std::vector<int> h_hidx;       // per boundary slot: halo index of a primary processor slot, else -1
   Halo* halo = nullptr;          // owned; freed by halo_destroy()
+  // solver gather (linsolve.hip): per cell W coupling entries, [W][C] (coalesced)
+  struct Ell {
+    int W = 0;
+    bool ready = false;
+    DevBuf<int> col;             // column: cell id, or C + halo index for a processor face
+    DevBuf<int> src;             // coefficient: 2f = lower[f], 2f+1 = upper[f], -(b+1) = -boundaryCoeffs[b]
+  } ell;
+  struct SolverWs {
+    DevBuf<double> buf, scal, red_local, red_all;
+    DevBuf<int> sysmap;
+    std::vector<double> hscal;
+  } ws;
   KernelTimer ktimer;
   ~Ctx();
   int n_corr = 2;
@@ -174,7 +191,33 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg);
 // halo.cpp
-void halo_exchange(Ctx& x, double* bvf, int ncomp, long bstride);
+// One exchange point: cell values of each item's components are sent across processor faces and land
+// in the receiver's neighbour slots (to_slots) or in the extended vector region [C, C+H) (solver vectors).
+struct HaloItem {
+  const double* cell;
+  double* dst;
+  int ncomp;
+  long cstride, dstride;
+  bool to_slots;
+};
+bool halo_active(const Ctx& x);
+void halo_update(Ctx& x, const HaloItem* items, int n);
+inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
+  if (!halo_active(x)) return;
+  std::vector<HaloItem> it;
+  for (const char* n : names) {
+    const Field& f = x.fields.at(n);
+    const Field& bf = x.fields.at(std::string("boundary_") + n);
+    it.push_back({f.buf.p, bf.buf.p, f.ncomp, f.n, bf.n, true});
+  }
+  halo_update(x, it.data(), (int)it.size());
+}
+// allgather of `count` doubles per rank: recv[r * count + i]
+void halo_allgather(Ctx& x, const double* send, double* recv, long count);
+void halo_setup(Ctx& x);   // builds the exchange lists after dfmi_set_comm_info / dfmi_set_comm_local
+void halo_init_rccl(Ctx& x, const void* uid, int nranks, int rank);
+void halo_init_local(Ctx& x, int hub_id, int nranks, int rank);
+void rccl_unique_id(void* out);
 void halo_destroy(Halo* h);
 
 }  // namespace dfmi

@@ -756,8 +756,8 @@ void rho_process(Ctx& x, bool write_matrix) {
   double* od = write_matrix ? x.f("dbg_rho_diag") : nullptr;
   double* os = write_matrix ? x.f("dbg_rho_source") : nullptr;
   LAUNCH(k_rho, x.C, x.view(), x.st("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("rho"), od, os);
-  halo_exchange(x, nullptr, 0, 0);
   k_bc_correct(x, "rho", x.f("rho"), x.f("boundary_rho"), 1);
+  halo_fields(x, {"rho"});
 }
 
 void u_assemble(Ctx& x) {
@@ -765,15 +765,18 @@ void u_assemble(Ctx& x) {
   double* gout = x.fields.count("dbg_gradU") ? x.f("dbg_gradU") : nullptr;
   LAUNCH(k_u_grad, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), x.f("mu"), x.f("boundary_mu"),
          x.f("tauU"), x.f("boundary_tauU"), gout);
+  halo_fields(x, {"tauU"});   // fvc_grad_vector_correctBC_processor (dfMatrixOpBase.cu:1366-1389)
   LAUNCH(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
          x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
          x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
          A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"));
   k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
+  halo_fields(x, {"rAU"});
 }
 
 void u_post_solve(Ctx& x) {
   k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
+  halo_fields(x, {"U"});
   LAUNCH(k_kinetic, x.C, x.C, x.f("U"), x.f("K"));
   LAUNCH(k_kinetic_slots, x.B, x.B, x.f("boundary_U"), x.f("boundary_K"));
 }
@@ -785,6 +788,7 @@ void u_hbya(Ctx& x) {
   k_bc_correct(x, "extrapolated", x.f("HbyA"), x.f("boundary_HbyA"), 3);
   LAUNCH(k_hbya_scale_cells, x.C, x.C, x.f("rAU"), x.f("HbyA"));
   LAUNCH(k_hbya_scale_slots, x.B, x.B, x.st("U"), x.f("boundary_rAU"), x.f("boundary_U"), x.f("boundary_HbyA"));
+  halo_fields(x, {"HbyA"});
 }
 
 void p_assemble(Ctx& x) {
@@ -804,12 +808,14 @@ void p_post_solve(Ctx& x) {
   Matrix& A = x.mP;
   MeshView m = x.view();
   k_bc_correct(x, "p", x.f("p"), x.f("boundary_p"), 1);
+  halo_fields(x, {"p"});
   LAUNCH(k_p_flux_face, x.F, m, x.f("phiHbyA"), A.lower.p, A.upper.p, x.f("p"), x.f("phi"));
   LAUNCH(k_p_flux_slot, x.B, m, x.st("p"), x.f("boundary_phiHbyA"), A.ic.p, A.bc.p, x.f("p"), x.f("boundary_p"),
          x.f("boundary_phi"));
   LAUNCH(k_p_cell_post, x.C, m, x.st("p"), x.f("p"), x.f("boundary_p"), x.f("p_old"), x.f("HbyA"), x.f("rAU"),
          x.f("U"), x.f("K"), x.f("dpdt"));
   k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
+  halo_fields(x, {"U"});
   LAUNCH(k_kinetic_slots, x.B, x.B, x.f("boundary_U"), x.f("boundary_K"));
 }
 
@@ -832,6 +838,7 @@ void y_prep(Ctx& x) {
                         x.f("diffAlphaD"), gout)
   DFMI_SWITCH_S(x.S, CALL)
 #undef CALL
+  halo_fields(x, {"sumYDiffError", "hDiffCorrFlux"});
   LAUNCH(k_phiuc_face, x.F, m, x.f("sumYDiffError"), x.f("phiUc"));
   LAUNCH(k_phiuc_slot, x.B, m, x.st("Y"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("boundary_phiUc"));
 }
@@ -851,6 +858,7 @@ void y_post_solve(Ctx& x) {
   DFMI_SWITCH_S(x.S, CALL)
 #undef CALL
   k_bc_correct(x, "Y", x.f("Y"), x.f("boundary_Y"), x.S);
+  halo_fields(x, {"Y"});
 }
 
 void e_assemble(Ctx& x) {
@@ -864,7 +872,10 @@ void e_assemble(Ctx& x) {
          eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p);
 }
 
-void e_post_solve(Ctx& x) { k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1); }
+void e_post_solve(Ctx& x) {
+  k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
+  halo_fields(x, {"he"});
+}
 
 void thermo_rho_from_psi(Ctx& x) {   // dfThermo::updateRho (dfThermo.cu:673-679)
   LAUNCH(k_mul, x.C, (long)x.C, x.f("p"), x.f("psi"), x.f("rho"));

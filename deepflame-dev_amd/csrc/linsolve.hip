@@ -1,16 +1,24 @@
-// linsolve.hip -- Krylov solvers on LDU storage (replaces the AmgX path, reference
-// src_gpu/AmgXSolver.cu:184-340 and dfMatrixDataBase.cu:166-177, and the per-matrix
-// ldu_to_csr gathers dfMatrixOpBase.cu:2276-2352 / dfUEqn.cu:836-894).
+// linsolve.hip -- Krylov solvers on the assembled LDU systems (replaces the AmgX path, reference
+// src_gpu/AmgXSolver.cu:184-340 and dfMatrixDataBase.cu:166-177, and the per-matrix ldu_to_csr
+// gathers dfMatrixOpBase.cu:2276-2352 / dfUEqn.cu:836-894).
 //
-// The SpMV gathers directly from lower/upper/diag plus the coupled boundary coefficients (cyclic
-// partner cells, processor halo values), so no 20 B x nnz CSR copy is made per matrix. Systems that
-// share the sparsity pattern are solved as one batch (grid.y = system): the 3 U components, and all
-// non-inert species of the Y equation (their matrices are independent, so the reference's sequential
-// species loop is a batch here). Preconditioner: Jacobi on diag + internalCoeffs. Convergence: AmgX
-// RELATIVE_INI L2 (||r|| <= tol ||r0||), per system. All reductions are two-stage and fixed-order,
-// hence deterministic. Scalars live on the device; the host reads only the per-system residual and
-// active flag every `check` iterations (inactive systems turn every kernel into a no-op).
+// Storage: a static ELL gather built once from the mesh, [W][C] (coalesced): per cell W coupling
+// entries in OpenFOAM's sequential order -- faces where the cell is neighbour (lower), faces it owns
+// (upper), then its coupled boundary slots (cyclic partner cell, or processor halo entry C + h). Per
+// solve one pass folds lower/upper/-boundaryCoeffs into ELL values and diag + internalCoeffs into the
+// diagonal (fvMatrix::addBoundaryDiag / addBoundarySource, the work ldu_to_csr does in the reference).
+// Systems sharing a sparsity pattern run as one batch (grid.y = system): the 3 U components, and all
+// non-inert species of the Y equation (independent matrices; the reference's sequential species loop
+// becomes a batch).
+//
+// Iterations have no single-block "finalise" kernels: every kernel that needs a global dot product
+// reduces the previous kernel's per-block partials itself in its prologue (fixed order, identical in
+// every block, so bitwise deterministic), and block 0 records the scalars for the host. Across ranks
+// the per-rank sums are all-gathered (RCCL) and summed in rank order. Jacobi preconditioning on
+// diag + internalCoeffs; convergence AmgX RELATIVE_INI L2 (||r|| <= tol ||r0||), per system; the host
+// reads the per-system state every `check` iterations (inactive systems turn every kernel into a no-op).
 #include "dfmi_ctx.h"
+#include <climits>
 #include <cmath>
 
 namespace dfmi {
@@ -18,327 +26,409 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr int NW = TPB / 64;
-
-struct Sys {
-  int nsys;
-  const double *lower, *upper, *diag, *source, *ic, *bc;
-  long lstride, ustride, dstride, sstride, bstride;
-  double* x; long xstride;
-  const double* xhalo;   // processor neighbour values of x, [nsys][B] (may be null)
-};
+constexpr int MAX_BLOCKS = 2048;
+constexpr int PAD = INT_MIN;
+constexpr int NSCAL = 16;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
   return v;
 }
-// block-reduce NV values into partial[(s*nblk + blk)*NV + k]
-template <int NV> __device__ __forceinline__ void block_partials(double (&v)[NV], double* partial, int s, int nblk) {
-  __shared__ double red[NW][NV];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) { const double r = wave_sum(v[k]); if (lane == 0) red[wid][k] = r; }
-  __syncthreads();
-  if (threadIdx.x < NV) {
-    double a = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) a += red[w][threadIdx.x];
-    partial[((long)s * nblk + blockIdx.x) * NV + threadIdx.x] = a;
-  }
-}
-// fixed-order sum of the block partials of system s (one block per system)
-template <int NV> __device__ __forceinline__ void finalize_sums(const double* partial, int s, int nblk, double (&out)[NV]) {
-  __shared__ double red[NW][NV];
+
+// value(s, i, k) = p[i * si + s * ss + k], i < np: the per-block partials (single rank) or the
+// all-gathered per-rank sums (multi-rank)
+struct Red { const double* p; int np; long si, ss; };
+
+// fixed-order block-wide sum, result in every thread
+template <int NV> __device__ __forceinline__ void red_sum(const Red& r, int s, double (&out)[NV]) {
+  __shared__ double sh[NW][NV];
   double v[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = 0.0;
-  for (int i = threadIdx.x; i < nblk; i += TPB)
+  for (int i = threadIdx.x; i < r.np; i += TPB)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] += partial[((long)s * nblk + i) * NV + k];
+    for (int k = 0; k < NV; ++k) v[k] += r.p[(long)i * r.si + (long)s * r.ss + k];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) { const double r = wave_sum(v[k]); if (lane == 0) red[wid][k] = r; }
+  for (int k = 0; k < NV; ++k) { const double t = wave_sum(v[k]); if (lane == 0) sh[wid][k] = t; }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     double a = 0.0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) a += red[w][k];
+    for (int w = 0; w < NW; ++w) a += sh[w][k];
     out[k] = a;
+  }
+  __syncthreads();
+}
+
+// block partial of NV values -> partial[(s * nblk + blockIdx.x) * NV + k]
+template <int NV> __device__ __forceinline__ void block_partials(double (&v)[NV], double* partial, int s) {
+  __shared__ double sh[NW][NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) { const double t = wave_sum(v[k]); if (lane == 0) sh[wid][k] = t; }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double a = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) a += sh[w][threadIdx.x];
+    partial[((long)s * gridDim.x + blockIdx.x) * NV + threadIdx.x] = a;
   }
 }
 
-// y = A x for system s: diag + internalCoeffs on the diagonal, lower/upper off-diagonal, and
-// -boundaryCoeffs * x_neighbour across coupled slots (lduMatrix::Amul + updateMatrixInterfaces)
-__device__ __forceinline__ double amul(const MeshView& m, const int8_t* ty, const Sys& q, int s, const double* dS,
-                                       const double* xv, int c) {
-  const double* L = q.lower + s * q.lstride;
-  const double* U = q.upper + s * q.ustride;
-  const double* bc = q.bc + s * q.bstride;
-  double y = dS[c] * xv[c];
-  const int e1 = m.nbrStart[c + 1];
-  for (int k = m.nbrStart[c]; k < e1; ++k) { const int f = m.nbrFace[k]; y += L[f] * xv[m.own[f]]; }
-  const int e2 = m.ownStart[c + 1];
-  for (int f = m.ownStart[c]; f < e2; ++f) y += U[f] * xv[m.nei[f]];
-  const int e3 = m.cbStart[c + 1];
-  for (int k = m.cbStart[c]; k < e3; ++k) {
-    const int b = m.cbSlot[k];
-    const int t = ty[b];
-    if (!bc_coupled(t)) continue;
-    const int pc = m.partner[b];
-    const double xn = pc >= 0 ? xv[pc] : q.xhalo[(long)s * m.B + b];
-    y -= bc[b] * xn;
-  }
+template <int NV> __global__ void k_red_local(const double* partial, int nblk, double* out) {
+  const int s = blockIdx.x;
+  double v[NV];
+  red_sum<NV>(Red{partial, nblk, NV, (long)nblk * NV}, s, v);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[s * NV + k] = v[k];
+}
+
+__device__ __forceinline__ bool leader() { return blockIdx.x == 0 && threadIdx.x == 0; }
+
+// y = dS x + sum_k val[k] x[col[k]]  (lduMatrix::Amul + updateMatrixInterfaces, same order)
+template <int WT> __device__ __forceinline__ double ell_mv(int W_, long C, const int* __restrict__ col,
+                                                            const double* __restrict__ val, double d,
+                                                            const double* __restrict__ xv, int c) {
+  const int W = WT > 0 ? WT : W_;
+  double y = d * xv[c];
+#pragma unroll
+  for (int k = 0; k < W; ++k) y += val[k * C + c] * xv[col[k * C + c]];
   return y;
 }
 
-// dS = diag + sum internalCoeffs (fvMatrix::addBoundaryDiag), rhs = source + non-coupled boundaryCoeffs
-// (fvMatrix::addBoundarySource(source, false)), in slot order
-__global__ void k_setup(MeshView m, const int8_t* ty, Sys q, double* dS, double* rhs, const int* sys_map) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+struct Sys {
+  const double *lower, *upper, *diag, *source, *ic, *bc;
+  long lstride, ustride, dstride, sstride, bstride;
+  double* x; long xstride;
+};
+
+// per system: ELL values, dS = diag + sum internalCoeffs, rhs = source + non-coupled boundaryCoeffs
+// (fvMatrix::addBoundaryDiag / addBoundarySource(source, false)), slot order as the sequential code
+__global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, const int* __restrict__ sys_map, int W,
+                            const int* __restrict__ esrc, long Ce, double* __restrict__ val, double* __restrict__ dS,
+                            double* __restrict__ rhs) {
   const int s = blockIdx.y;
-  if (c >= m.C) return;
   const int ms = sys_map ? sys_map[s] : s;
+  const long C = m.C;
+  const double* L = q.lower + ms * q.lstride;
+  const double* U = q.upper + ms * q.ustride;
   const double* ic = q.ic + ms * q.bstride;
   const double* bc = q.bc + ms * q.bstride;
-  double d = q.diag[ms * q.dstride + c];
-  double r = q.source[ms * q.sstride + c];
-  const int e3 = m.cbStart[c + 1];
-  for (int k = m.cbStart[c]; k < e3; ++k) {
-    const int b = m.cbSlot[k];
-    const int t = ty[b];
-    if (t == EMPTY) continue;
-    d += ic[b];
+  double* vs = val + (long)s * W * C;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
+    for (int k = 0; k < W; ++k) {
+      const int e = esrc[k * C + c];
+      double v;
+      if (e == PAD) v = 0.0;
+      else if (e >= 0) v = (e & 1) ? U[e >> 1] : L[e >> 1];
+      else v = -bc[-e - 1];
+      vs[k * C + c] = v;
+    }
+    double d = q.diag[ms * q.dstride + c];
+    double r = q.source[ms * q.sstride + c];
+    const int e3 = m.cbStart[c + 1];
+    for (int k = m.cbStart[c]; k < e3; ++k) {
+      const int b = m.cbSlot[k];
+      if (ty[b] == EMPTY) continue;
+      d += ic[b];
+    }
+    for (int k = m.cbStart[c]; k < e3; ++k) {
+      const int b = m.cbSlot[k];
+      const int t = ty[b];
+      if (t == EMPTY || bc_coupled(t)) continue;
+      r += bc[b];
+    }
+    dS[s * Ce + c] = d;
+    rhs[s * Ce + c] = r;
   }
-  for (int k = m.cbStart[c]; k < e3; ++k) {
-    const int b = m.cbSlot[k];
-    const int t = ty[b];
-    if (t == EMPTY || bc_coupled(t)) continue;
-    r += bc[b];
-  }
-  dS[(long)s * m.C + c] = d;
-  rhs[(long)s * m.C + c] = r;
 }
 
-// ---- BiCGStab kernels. State per system (scal[s*8+k]): 0 rho, 1 rho_old, 2 alpha, 3 omega,
-// 4 res0, 5 res, 6 active, 7 iters.
-__global__ void k_bcg_init(MeshView m, const int8_t* ty, Sys q, const int* sys_map, const double* dS, const double* rhs,
-                           double* r, double* r0, double* p, double* v, double* partial, int nblk) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// copy the current solution into a work vector (its halo region is filled by the exchange)
+__global__ void k_copy_x(long C, long Ce, Sys q, const int* __restrict__ sys_map, double* __restrict__ xw) {
   const int s = blockIdx.y;
-  const long C = m.C;
+  const int ms = sys_map ? sys_map[s] : s;
+  for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < C; c += (long)gridDim.x * blockDim.x)
+    xw[s * Ce + c] = q.x[ms * q.xstride + c];
+}
+
+// ============================================================== BiCGStab (AmgX PBiCGStab semantics)
+// scal[s*16 + k]: 0 rho, 1 rho_old, 2 alpha, 3 omega, 4 res0, 5 res, 6 active, 7 iters
+struct BV { double *dS, *rhs, *r, *r0, *p, *v, *phat, *sv, *shat, *t, *xw; };
+
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const int* __restrict__ col,
+                                                  const double* __restrict__ val, BV b, double* partial) {
+  const int s = blockIdx.y;
+  const double* vs = val + (long)s * W * C;
   double acc[2] = {0.0, 0.0};
-  if (c < m.C) {
-    const int ms = sys_map ? sys_map[s] : s;
-    const double* xv = q.x + ms * q.xstride;
-    const double ax = amul(m, ty, q, ms, dS + s * C, xv, c);
-    const double rr = rhs[s * C + c] - ax;
-    r[s * C + c] = rr; r0[s * C + c] = rr; p[s * C + c] = 0.0; v[s * C + c] = 0.0;
-    acc[0] = rr * rr;
-    acc[1] = rr * rr;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double ax = ell_mv<WT>(W, C, col, vs, b.dS[i], b.xw + s * Ce, c);
+    const double rr = b.rhs[i] - ax;
+    b.r[i] = rr; b.r0[i] = rr; b.p[i] = 0.0; b.v[i] = 0.0;
+    acc[0] += rr * rr;
+    acc[1] += rr * rr;
   }
-  block_partials<2>(acc, partial, s, nblk);
+  block_partials<2>(acc, partial, s);
 }
-__global__ void k_bcg_init_fin(double* partial, int nblk, double* scal, double tol, double abs_tol) {
-  const int s = blockIdx.x;
+
+// prologue: res, rho from (r.r, r0.r); convergence; p = r + beta (p - omega v); phat = p / dS
+__global__ void __launch_bounds__(TPB) k_bcg_p(long C, long Ce, int it, int max_iter, double tol, double abs_tol,
+                                               Red red, double* scal, BV b) {
+  const int s = blockIdx.y;
+  double* st = scal + s * NSCAL;
   double v[2];
-  finalize_sums<2>(partial, s, nblk, v);
-  if (threadIdx.x == 0) {
-    double* st = scal + s * 8;
-    const double res = sqrt(v[0]);
-    st[0] = v[1]; st[1] = 1.0; st[2] = 1.0; st[3] = 1.0; st[4] = res; st[5] = res; st[7] = 0;
-    st[6] = (res > abs_tol && res > 0.0) ? 1.0 : 0.0;
+  red_sum<2>(red, s, v);
+  const double res = sqrt(v[0]), rho = v[1];
+  const double res0 = it == 0 ? res : st[4];
+  const double omega = st[3];
+  const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || omega == 0.0));
+  if (leader()) {
+    if (it == 0) st[4] = res;
+    if (it == 0 || st[6] != 0.0) { st[5] = res; st[7] = it; }
+    st[6] = stop ? 0.0 : 1.0;
+    st[0] = rho;
+  }
+  if (stop) return;
+  const double beta = it == 0 ? 0.0 : (rho / st[1]) * (st[2] / omega);
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double pv = it == 0 ? b.r[i] : b.r[i] + beta * (b.p[i] - omega * b.v[i]);
+    b.p[i] = pv;
+    b.phat[i] = pv / b.dS[i];
   }
 }
-// p = r + beta (p - omega v); phat = p / dS; then v = A phat needs a separate pass
-__global__ void k_bcg_p(int C, const double* scal, const double* r, double* p, const double* v, const double* dS,
-                        double* phat) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+
+// out = A in; partial dots (NV = 1: r0.out; NV = 2: out.sv, out.out)
+template <int WT, int NV>
+__global__ void __launch_bounds__(TPB) k_bcg_spmv(long C, long Ce, int W, const int* __restrict__ col,
+                                                  const double* __restrict__ val, const double* scal,
+                                                  const double* __restrict__ dS, const double* __restrict__ in,
+                                                  double* __restrict__ out, const double* __restrict__ dotv,
+                                                  double* partial) {
   const int s = blockIdx.y;
-  const double* st = scal + s * 8;
-  if (c >= C || st[6] == 0.0) return;
-  const long i = (long)s * C + c;
-  const double beta = (st[0] / st[1]) * (st[2] / st[3]);
-  const double pv = r[i] + beta * (p[i] - st[3] * v[i]);
-  p[i] = pv;
-  phat[i] = pv / dS[i];
-}
-// out = A in, plus partial dots: (r0, out) [NV=1] or (out, sv), (out, out) [NV=2]
-template <int NV>
-__global__ void k_bcg_spmv(MeshView m, const int8_t* ty, Sys q, const int* sys_map, const double* scal,
-                           const double* dS, const double* in, double* out, const double* dotv, double* partial,
-                           int nblk) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = blockIdx.y;
-  const long C = m.C;
+  if (scal[s * NSCAL + 6] == 0.0) return;   // uniform per block
+  const double* vs = val + (long)s * W * C;
   double acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-  if (scal[s * 8 + 6] == 0.0) return;   // uniform per block
-  if (c < m.C) {
-    const int ms = sys_map ? sys_map[s] : s;
-    const double y = amul(m, ty, q, ms, dS + s * C, in + s * C, c);
-    out[s * C + c] = y;
-    if (NV == 1) acc[0] = dotv[s * C + c] * y;
-    else { acc[0] = y * dotv[s * C + c]; if (NV > 1) acc[NV - 1] = y * y; }
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double y = ell_mv<WT>(W, C, col, vs, dS[i], in + s * Ce, c);
+    out[i] = y;
+    if (NV == 1) acc[0] += dotv[i] * y;
+    else { acc[0] += y * dotv[i]; acc[NV - 1] += y * y; }
   }
-  block_partials<NV>(acc, partial, s, nblk);
+  block_partials<NV>(acc, partial, s);
 }
-__global__ void k_bcg_alpha(double* partial, int nblk, double* scal) {
-  const int s = blockIdx.x;
-  if (scal[s * 8 + 6] == 0.0) return;
-  double v[1];
-  finalize_sums<1>(partial, s, nblk, v);
-  if (threadIdx.x == 0) {
-    double* st = scal + s * 8;
-    if (v[0] == 0.0) { st[6] = 0.0; return; }
-    st[2] = st[0] / v[0];
-  }
-}
-// s = r - alpha v; shat = s / dS
-__global__ void k_bcg_s(int C, const double* scal, const double* r, const double* v, const double* dS, double* sv,
-                        double* shat) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+
+// prologue: alpha = rho / (r0.v); s = r - alpha v; shat = s / dS
+__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b) {
   const int s = blockIdx.y;
-  const double* st = scal + s * 8;
-  if (c >= C || st[6] == 0.0) return;
-  const long i = (long)s * C + c;
-  const double ss = r[i] - st[2] * v[i];
-  sv[i] = ss;
-  shat[i] = ss / dS[i];
-}
-__global__ void k_bcg_omega(double* partial, int nblk, double* scal) {
-  const int s = blockIdx.x;
-  if (scal[s * 8 + 6] == 0.0) return;
-  double v[2];
-  finalize_sums<2>(partial, s, nblk, v);
-  if (threadIdx.x == 0) {
-    double* st = scal + s * 8;
-    st[3] = v[1] != 0.0 ? v[0] / v[1] : 0.0;
-  }
-}
-// x += alpha phat + omega shat; r = s - omega t; partials (r,r), (r0,r)
-__global__ void k_bcg_x(int C, Sys q, const int* sys_map, const double* scal, const double* phat, const double* shat,
-                        const double* sv, const double* t, double* r, const double* r0, double* partial, int nblk) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int s = blockIdx.y;
-  const double* st = scal + s * 8;
+  double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
-  double acc[2] = {0.0, 0.0};
-  if (c < C) {
-    const long i = (long)s * C + c;
-    const int ms = sys_map ? sys_map[s] : s;
-    double* xv = q.x + ms * q.xstride;
-    xv[c] = xv[c] + st[2] * phat[i] + st[3] * shat[i];
-    const double rr = sv[i] - st[3] * t[i];
-    r[i] = rr;
-    acc[0] = rr * rr;
-    acc[1] = r0[i] * rr;
-  }
-  block_partials<2>(acc, partial, s, nblk);
-}
-__global__ void k_bcg_fin(double* partial, int nblk, double* scal, double tol, double abs_tol, int max_iter) {
-  const int s = blockIdx.x;
-  if (scal[s * 8 + 6] == 0.0) return;
-  double v[2];
-  finalize_sums<2>(partial, s, nblk, v);
-  if (threadIdx.x == 0) {
-    double* st = scal + s * 8;
-    const double res = sqrt(v[0]);
-    st[5] = res;
-    st[7] += 1.0;
-    st[1] = st[0];
-    st[0] = v[1];
-    if (res <= tol * st[4] || res <= abs_tol || st[7] >= max_iter || st[0] == 0.0 || st[3] == 0.0) st[6] = 0.0;
-  }
-}
-
-// ---- PCG (Jacobi) for the symmetric pressure matrix. scal: 0 rz, 1 alpha, 2 beta, 4 res0, 5 res, 6 active, 7 iters
-__global__ void k_cg_init(MeshView m, const int8_t* ty, Sys q, const double* dS, const double* rhs, double* r, double* z,
-                          double* p, double* partial, int nblk) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  double acc[2] = {0.0, 0.0};
-  if (c < m.C) {
-    const double ax = amul(m, ty, q, 0, dS, q.x, c);
-    const double rr = rhs[c] - ax;
-    const double zz = rr / dS[c];
-    r[c] = rr; z[c] = zz; p[c] = zz;
-    acc[0] = rr * zz; acc[1] = rr * rr;
-  }
-  block_partials<2>(acc, partial, 0, nblk);
-}
-__global__ void k_cg_init_fin(double* partial, int nblk, double* scal, double abs_tol) {
-  double v[2];
-  finalize_sums<2>(partial, 0, nblk, v);
-  if (threadIdx.x == 0) {
-    const double res = sqrt(v[1]);
-    scal[0] = v[0]; scal[4] = res; scal[5] = res; scal[7] = 0;
-    scal[6] = (res > abs_tol && res > 0.0) ? 1.0 : 0.0;
-  }
-}
-__global__ void k_cg_spmv(MeshView m, const int8_t* ty, Sys q, const double* scal, const double* dS, const double* p,
-                          double* qv, double* partial, int nblk) {
-  if (scal[6] == 0.0) return;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  double acc[1] = {0.0};
-  if (c < m.C) {
-    const double y = amul(m, ty, q, 0, dS, p, c);
-    qv[c] = y;
-    acc[0] = p[c] * y;
-  }
-  block_partials<1>(acc, partial, 0, nblk);
-}
-__global__ void k_cg_alpha(double* partial, int nblk, double* scal) {
-  if (scal[6] == 0.0) return;
   double v[1];
-  finalize_sums<1>(partial, 0, nblk, v);
-  if (threadIdx.x == 0) { if (v[0] == 0.0) { scal[6] = 0.0; return; } scal[1] = scal[0] / v[0]; }
-}
-__global__ void k_cg_x(int C, double* x, const double* scal, const double* p, const double* qv, double* r, double* z,
-                       const double* dS, double* partial, int nblk) {
-  if (scal[6] == 0.0) return;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  double acc[2] = {0.0, 0.0};
-  if (c < C) {
-    const double a = scal[1];
-    x[c] = x[c] + a * p[c];
-    const double rr = r[c] - a * qv[c];
-    r[c] = rr;
-    const double zz = rr / dS[c];
-    z[c] = zz;
-    acc[0] = rr * zz; acc[1] = rr * rr;
+  red_sum<1>(red, s, v);
+  const double rho = st[0];
+  const double alpha = v[0] != 0.0 ? rho / v[0] : 0.0;
+  if (leader()) { st[2] = alpha; st[1] = rho; }
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double ss = b.r[i] - alpha * b.v[i];
+    b.sv[i] = ss;
+    b.shat[i] = ss / b.dS[i];
   }
-  block_partials<2>(acc, partial, 0, nblk);
-}
-__global__ void k_cg_fin(double* partial, int nblk, double* scal, double tol, double abs_tol, int max_iter) {
-  if (scal[6] == 0.0) return;
-  double v[2];
-  finalize_sums<2>(partial, 0, nblk, v);
-  if (threadIdx.x == 0) {
-    const double res = sqrt(v[1]);
-    scal[5] = res;
-    scal[7] += 1.0;
-    scal[2] = scal[0] != 0.0 ? v[0] / scal[0] : 0.0;
-    scal[0] = v[0];
-    if (res <= tol * scal[4] || res <= abs_tol || scal[7] >= max_iter) scal[6] = 0.0;
-  }
-}
-__global__ void k_cg_p(int C, const double* scal, const double* z, double* p) {
-  if (scal[6] == 0.0) return;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  p[c] = z[c] + scal[2] * p[c];
 }
 
-struct Workspace {
-  DevBuf<double> buf;
-  DevBuf<double> scal;
-  DevBuf<int> sysmap;
-  std::vector<double> hscal;
+// prologue: omega = (t.s)/(t.t); x += alpha phat + omega shat; r = s - omega t; partials (r.r, r0.r)
+__global__ void __launch_bounds__(TPB) k_bcg_x(long C, long Ce, Red red, Sys q, const int* __restrict__ sys_map,
+                                               double* scal, BV b, double* partial) {
+  const int s = blockIdx.y;
+  double* st = scal + s * NSCAL;
+  if (st[6] == 0.0) return;
+  double v[2];
+  red_sum<2>(red, s, v);
+  const double omega = v[1] != 0.0 ? v[0] / v[1] : 0.0;
+  const double alpha = st[2];
+  if (leader()) st[3] = omega;
+  const int ms = sys_map ? sys_map[s] : s;
+  double* xv = q.x + ms * q.xstride;
+  double acc[2] = {0.0, 0.0};
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    xv[c] = xv[c] + alpha * b.phat[i] + omega * b.shat[i];
+    const double rr = b.sv[i] - omega * b.t[i];
+    b.r[i] = rr;
+    acc[0] += rr * rr;
+    acc[1] += b.r0[i] * rr;
+  }
+  block_partials<2>(acc, partial, s);
+}
+
+// ============================================================== PCG (Jacobi) for the symmetric p matrix
+// scal: 0 rz, 1 rz_prev, 2 alpha, 4 res0, 5 res, 6 active, 7 iters
+struct CV { double *dS, *rhs, *r, *z, *pa, *pb, *q, *xw; };
+
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, const int* __restrict__ col,
+                                                 const double* __restrict__ val, CV v, double* partial) {
+  double acc[2] = {0.0, 0.0};
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const double ax = ell_mv<WT>(W, C, col, val, v.dS[c], v.xw, c);
+    const double rr = v.rhs[c] - ax;
+    const double zz = rr / v.dS[c];
+    v.r[c] = rr; v.z[c] = zz; v.pa[c] = 0.0; v.pb[c] = 0.0;
+    acc[0] += rr * zz; acc[1] += rr * rr;
+  }
+  block_partials<2>(acc, partial, 0);
+}
+
+// prologue: rz, res, convergence, beta; p_new = z + beta p_old (own and, on the fly, neighbours);
+// q = A p_new; partial p_new.q
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __restrict__ col,
+                                                 const double* __restrict__ val, int it, int max_iter, double tol,
+                                                 double abs_tol, Red red, double* scal, CV v,
+                                                 const double* __restrict__ pold, double* __restrict__ pnew,
+                                                 double* partial) {
+  double rv[2];
+  red_sum<2>(red, 0, rv);
+  const double rz = rv[0], res = sqrt(rv[1]);
+  const double res0 = it == 0 ? res : scal[4];
+  const double rzp = scal[1];
+  const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && rzp == 0.0);
+  if (leader()) {
+    if (it == 0) scal[4] = res;
+    if (it == 0 || scal[6] != 0.0) { scal[5] = res; scal[7] = it; }
+    scal[6] = stop ? 0.0 : 1.0;
+    scal[0] = rz;
+  }
+  if (stop) return;
+  const double beta = it == 0 ? 0.0 : rz / rzp;
+  const double* z = v.z;
+  const int Wr = WT > 0 ? WT : W;
+  double acc[1] = {0.0};
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const double pc = z[c] + beta * pold[c];
+    pnew[c] = pc;
+    double y = v.dS[c] * pc;
+#pragma unroll
+    for (int k = 0; k < Wr; ++k) {
+      const int j = col[k * C + c];
+      y += val[k * C + c] * (z[j] + beta * pold[j]);
+    }
+    v.q[c] = y;
+    acc[0] += pc * y;
+  }
+  block_partials<1>(acc, partial, 0);
+}
+
+// prologue: alpha = rz / (p.q); x += alpha p; r -= alpha q; z = r / dS; partials (r.z, r.r)
+__global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, double* __restrict__ x, CV v,
+                                              const double* __restrict__ pnew, double* partial) {
+  if (scal[6] == 0.0) return;
+  double pv[1];
+  red_sum<1>(red, 0, pv);
+  const double rz = scal[0];
+  const double alpha = pv[0] != 0.0 ? rz / pv[0] : 0.0;
+  if (leader()) { scal[2] = alpha; scal[1] = rz; }
+  double acc[2] = {0.0, 0.0};
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    x[c] = x[c] + alpha * pnew[c];
+    const double rr = v.r[c] - alpha * v.q[c];
+    v.r[c] = rr;
+    const double zz = rr / v.dS[c];
+    v.z[c] = zz;
+    acc[0] += rr * zz; acc[1] += rr * rr;
+  }
+  block_partials<2>(acc, partial, 0);
+}
+
+// ------------------------------------------------------------------ host side
+void build_ell(Ctx& x) {
+  const int C = x.C;
+  std::vector<int> own = x.h_own, nei = x.h_nei;
+  std::vector<std::vector<std::pair<int, int>>> ent(C);   // (col, src)
+  std::vector<std::vector<int>> nbrf(C);
+  for (int f = 0; f < x.F; ++f) nbrf[nei[f]].push_back(f);
+  for (int c = 0; c < C; ++c) for (int f : nbrf[c]) ent[c].push_back({own[f], 2 * f});
+  for (int f = 0; f < x.F; ++f) ent[own[f]].push_back({nei[f], 2 * f + 1});
+  // owned faces were appended in ascending face order after the neighbour faces: matches each_face
+  std::vector<int> partner(x.B, -1);
+  for (int p = 0; p < x.P; ++p) {
+    if (x.pkind[p] != 1) continue;
+    const int q = x.cyc_nbr[p];
+    for (int i = 0; i < x.psize[p]; ++i) partner[x.poff[p] + i] = x.h_bfc[x.poff[q] + i];
+  }
+  for (int p = 0; p < x.P; ++p) {   // coupled primary slots in slot order (= cbSlot order per cell)
+    if (x.pkind[p] == 0) continue;
+    for (int i = 0; i < x.psize[p]; ++i) {
+      const int b = x.poff[p] + i;
+      const int c = x.h_bfc[b];
+      int colv;
+      if (x.pkind[p] == 1) colv = partner[b];
+      else {
+        DFMI_CHECK(halo_active(x) && b < (int)x.h_hidx.size() && x.h_hidx[b] >= 0,
+                   "processor patches need dfmi_set_comm_info before the first solve");
+        colv = C + x.h_hidx[b];
+      }
+      ent[c].push_back({colv, -(b + 1)});
+    }
+  }
+  int W = 0;
+  for (auto& e : ent) W = std::max(W, (int)e.size());
+  W = std::max(W, 1);
+  std::vector<int> col((size_t)W * C), src((size_t)W * C);
+  for (int c = 0; c < C; ++c)
+    for (int k = 0; k < W; ++k) {
+      const bool have = k < (int)ent[c].size();
+      col[(size_t)k * C + c] = have ? ent[c][k].first : c;
+      src[(size_t)k * C + c] = have ? ent[c][k].second : PAD;
+    }
+  x.ell.W = W;
+  x.ell.col.upload(col, x.stream);
+  x.ell.src.upload(src, x.stream);
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  x.ell.ready = true;
+}
+
+struct Launch {
+  Ctx& x;
+  int nblk, nsys;
+  Red after(double* partial, int NV) {   // make the partials of the last kernel readable by the next
+    if (x.nranks == 1) return Red{partial, nblk, NV, (long)nblk * NV};
+    SolverWsRed();
+    if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, x.ws.red_local.p);
+    else hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, x.ws.red_local.p);
+    DFMI_HIP(hipGetLastError());
+    halo_allgather(x, x.ws.red_local.p, x.ws.red_all.p, (long)nsys * NV);
+    return Red{x.ws.red_all.p, x.nranks, (long)nsys * NV, NV};
+  }
+  void SolverWsRed() {
+    const size_t need = (size_t)nsys * 2;
+    if (x.ws.red_local.n < need) x.ws.red_local.alloc(need);
+    if (x.ws.red_all.n < need * x.nranks) x.ws.red_all.alloc(need * x.nranks);
+  }
 };
-Workspace& ws(Ctx& x) {
-  static std::map<Ctx*, Workspace> w;
-  return w[&x];
+
+template <class F> void dispatch_W(int W, F&& f) {
+  switch (W) {
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 5: f(std::integral_constant<int, 5>()); break;
+    case 6: f(std::integral_constant<int, 6>()); break;
+    default: f(std::integral_constant<int, 0>()); break;
+  }
+}
+
+void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce) {
+  if (!halo_active(x)) return;
+  std::vector<HaloItem> it;
+  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false});
+  halo_update(x, it.data(), (int)it.size());
 }
 
 }  // namespace
@@ -347,61 +437,84 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
                           const double* upper, long ustride, const double* diag, long dstride, const double* source,
                           long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
                           double* xsol, long xstride, const SolverCfg& cfg) {
-  const long C = x.C;
-  const int nblk = blocks_for(C, TPB);
-  Workspace& W = ws(x);
-  const size_t need = (size_t)nsys * C * 10 + (size_t)nsys * nblk * 2 + 64;
-  if (W.buf.n < need) W.buf.alloc(need);
-  if (W.scal.n < (size_t)nsys * 8) W.scal.alloc(nsys * 8);
+  if (!x.ell.ready) build_ell(x);
+  const long C = x.C, Ce = (long)x.C + x.H;
+  const int W = x.ell.W;
+  const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
+  auto& WS = x.ws;
+  const size_t nvec = 11;
+  const size_t need = nvec * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 6 + 64;
+  if (WS.buf.n < need) WS.buf.alloc(need);
+  if (WS.scal.n < (size_t)nsys * NSCAL) WS.scal.alloc((size_t)nsys * NSCAL);
   const int* smap = nullptr;
   if (sys_map_host) {
-    W.sysmap.upload(sys_map_host, nsys, x.stream);
-    smap = W.sysmap.p;
+    WS.sysmap.upload(sys_map_host, nsys, x.stream);
+    smap = WS.sysmap.p;
   }
-  const long N = nsys * C;
-  double *dS = W.buf.p, *rhs = dS + N, *r = rhs + N, *r0 = r + N, *p = r0 + N, *v = p + N, *phat = v + N,
-         *sv = phat + N, *shat = sv + N, *t = shat + N, *partial = t + N;
-  Sys q{nsys, lower, upper, diag, source, ic, bc, lstride, ustride, dstride, sstride, bstride, xsol, xstride,
-        x.fields.count("halo_x") ? x.f("halo_x") : nullptr};
+  const long N = nsys * Ce;
+  double* base = WS.buf.p;
+  BV b{base, base + N, base + 2 * N, base + 3 * N, base + 4 * N, base + 5 * N, base + 6 * N, base + 7 * N,
+       base + 8 * N, base + 9 * N, base + 10 * N};
+  double* val = base + 11 * N;
+  // one partial buffer per reduction site, so a converged system's last sums stay intact
+  double* p1 = val + (size_t)nsys * W * C;          // (r.r, r0.r)
+  double* p2 = p1 + (size_t)nsys * nblk * 2;        // r0.v
+  double* p3 = p2 + (size_t)nsys * nblk * 2;        // (t.s, t.t)
+  Sys q{lower, upper, diag, source, ic, bc, lstride, ustride, dstride, sstride, bstride, xsol, xstride};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk, nsys), bl(TPB);
-  { KScope _ks(x, "k_setup"); hipLaunchKernelGGL(k_setup, g, bl, 0, x.stream, m, ty, q, dS, rhs, smap); }
-  { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init, g, bl, 0, x.stream, m, ty, q, smap, dS, rhs, r, r0, p, v, partial, nblk); }
-  { KScope _ks(x, "k_bcg_init_fin"); hipLaunchKernelGGL(k_bcg_init_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol); }
+  Launch L{x, nblk, nsys};
+  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, smap, W, x.ell.src.p, Ce, val, b.dS, b.rhs); }
+  { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, smap, b.xw); }
   DFMI_HIP(hipGetLastError());
-  W.hscal.resize(nsys * 8);
-  int it = 0;
+  halo_vecs(x, {b.xw}, nsys, Ce);
+  dispatch_W(W, [&](auto wt) {
+    constexpr int WT = decltype(wt)::value;
+    { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, b, p1); }
+  });
+  DFMI_HIP(hipGetLastError());
+  Red red = L.after(p1, 2);
+  WS.hscal.resize((size_t)nsys * NSCAL);
   const int check = 2;
-  bool synced = false;
-  while (it < cfg.max_iter) {
-    for (int k = 0; k < check && it < cfg.max_iter; ++k, ++it) {
-      { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, (int)C, W.scal.p, r, p, v, dS, phat); }
-      { KScope _ks(x, "k_bcg_spmv"); hipLaunchKernelGGL(k_bcg_spmv<1>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, phat, v, r0, partial, nblk); }
-      { KScope _ks(x, "k_bcg_alpha"); hipLaunchKernelGGL(k_bcg_alpha, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p); }
-      { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, (int)C, W.scal.p, r, v, dS, sv, shat); }
-      { KScope _ks(x, "k_bcg_spmv"); hipLaunchKernelGGL(k_bcg_spmv<2>, g, bl, 0, x.stream, m, ty, q, smap, W.scal.p, dS, shat, t, sv, partial, nblk); }
-      { KScope _ks(x, "k_bcg_omega"); hipLaunchKernelGGL(k_bcg_omega, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p); }
-      { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, (int)C, q, smap, W.scal.p, phat, shat, sv, t, r, r0, partial, nblk); }
-      { KScope _ks(x, "k_bcg_fin"); hipLaunchKernelGGL(k_bcg_fin, dim3(nsys), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter); }
-    }
+  for (int it = 0;; ++it) {
+    { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, C, Ce, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red, WS.scal.p, b); }
+    if (it >= cfg.max_iter) break;
+    halo_vecs(x, {b.phat}, nsys, Ce);
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_spmv");
+      hipLaunchKernelGGL((k_bcg_spmv<WT, 1>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.phat, b.v, b.r0, p2);
+    });
+    red = L.after(p2, 1);
+    { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
+    halo_vecs(x, {b.shat}, nsys, Ce);
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_spmv");
+      hipLaunchKernelGGL((k_bcg_spmv<WT, 2>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.shat, b.t, b.sv, p3);
+    });
+    red = L.after(p3, 2);
+    { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, C, Ce, red, q, smap, WS.scal.p, b, p1); }
     DFMI_HIP(hipGetLastError());
-    DFMI_HIP(hipMemcpyAsync(W.hscal.data(), W.scal.p, nsys * 8 * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-    DFMI_HIP(hipStreamSynchronize(x.stream));
-    synced = true;
-    bool any = false;
-    for (int s = 0; s < nsys; ++s) any |= W.hscal[s * 8 + 6] != 0.0;
-    if (!any) break;
+    red = L.after(p1, 2);
+    if ((it + 1) % check == 0) {
+      DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      bool any = false;
+      for (int s = 0; s < nsys; ++s) any |= WS.hscal[s * NSCAL + 6] != 0.0;
+      if (!any) break;
+    }
   }
-  if (!synced) {
-    DFMI_HIP(hipMemcpyAsync(W.hscal.data(), W.scal.p, nsys * 8 * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-    DFMI_HIP(hipStreamSynchronize(x.stream));
-  }
+  DFMI_HIP(hipGetLastError());
+  DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipStreamSynchronize(x.stream));
   SolveStats st;
   for (int s = 0; s < nsys; ++s) {
-    st.iters = std::max(st.iters, (int)W.hscal[s * 8 + 7]);
-    st.res0 = std::max(st.res0, W.hscal[s * 8 + 4]);
-    st.res = std::max(st.res, W.hscal[s * 8 + 4] > 0 ? W.hscal[s * 8 + 5] / W.hscal[s * 8 + 4] : 0.0);
+    const double* h = &WS.hscal[s * NSCAL];
+    st.iters = std::max(st.iters, (int)h[7]);
+    st.res0 = std::max(st.res0, h[4]);
+    st.res = std::max(st.res, h[4] > 0 ? h[5] / h[4] : 0.0);
   }
   x.last_stats[eqn] = st;
   return st;
@@ -411,41 +524,66 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg) {
   (void)bxsol;
-  const long C = x.C;
-  const int nblk = blocks_for(C, TPB);
-  Workspace& W = ws(x);
-  const size_t need = (size_t)C * 6 + (size_t)nblk * 2 + 64;
-  if (W.buf.n < need) W.buf.alloc(need);
-  if (W.scal.n < 8) W.scal.alloc(8);
-  double *dS = W.buf.p, *rhs = dS + C, *r = rhs + C, *z = r + C, *p = z + C, *qv = p + C, *partial = qv + C;
-  Sys q{1, lower, upper, diag, source, ic, bc, 0, 0, 0, 0, 0, xsol, 0, x.fields.count("halo_x") ? x.f("halo_x") : nullptr};
+  if (!x.ell.ready) build_ell(x);
+  const long C = x.C, Ce = (long)x.C + x.H;
+  const int W = x.ell.W;
+  const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
+  auto& WS = x.ws;
+  const size_t need = 8 * Ce + (size_t)W * C + (size_t)nblk * 4 + 64;
+  if (WS.buf.n < need) WS.buf.alloc(need);
+  if (WS.scal.n < NSCAL) WS.scal.alloc(NSCAL);
+  double* base = WS.buf.p;
+  CV v{base, base + Ce, base + 2 * Ce, base + 3 * Ce, base + 4 * Ce, base + 5 * Ce, base + 6 * Ce, base + 7 * Ce};
+  double* val = base + 8 * Ce;
+  double* q1 = val + (size_t)W * C;    // p.q
+  double* q2 = q1 + (size_t)nblk * 2;  // (r.z, r.r)
+  Sys q{lower, upper, diag, source, ic, bc, 0, 0, 0, 0, 0, xsol, 0};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk), bl(TPB);
-  { KScope _ks(x, "k_setup"); hipLaunchKernelGGL(k_setup, dim3(nblk, 1), bl, 0, x.stream, m, ty, q, dS, rhs, (const int*)nullptr); }
-  { KScope _ks(x, "k_cg_init"); hipLaunchKernelGGL(k_cg_init, g, bl, 0, x.stream, m, ty, q, dS, rhs, r, z, p, partial, nblk); }
-  { KScope _ks(x, "k_cg_init_fin"); hipLaunchKernelGGL(k_cg_init_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.abs_tol); }
+  Launch L{x, nblk, 1};
+  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs); }
+  { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());
-  W.hscal.resize(8);
-  int it = 0;
+  halo_vecs(x, {v.xw}, 1, Ce);
+  dispatch_W(W, [&](auto wt) {
+    constexpr int WT = decltype(wt)::value;
+    KScope _ks(x, "k_cg_init");
+    hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, v, q2);
+  });
+  DFMI_HIP(hipGetLastError());
+  Red red = L.after(q2, 2);
+  WS.hscal.resize(NSCAL);
   const int check = 8;
-  while (it < cfg.max_iter) {
-    for (int k = 0; k < check && it < cfg.max_iter; ++k, ++it) {
-      { KScope _ks(x, "k_cg_spmv"); hipLaunchKernelGGL(k_cg_spmv, g, bl, 0, x.stream, m, ty, q, W.scal.p, dS, p, qv, partial, nblk); }
-      { KScope _ks(x, "k_cg_alpha"); hipLaunchKernelGGL(k_cg_alpha, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p); }
-      { KScope _ks(x, "k_cg_x"); hipLaunchKernelGGL(k_cg_x, g, bl, 0, x.stream, (int)C, xsol, W.scal.p, p, qv, r, z, dS, partial, nblk); }
-      { KScope _ks(x, "k_cg_fin"); hipLaunchKernelGGL(k_cg_fin, dim3(1), bl, 0, x.stream, partial, nblk, W.scal.p, cfg.tol, cfg.abs_tol, cfg.max_iter); }
-      { KScope _ks(x, "k_cg_p"); hipLaunchKernelGGL(k_cg_p, g, bl, 0, x.stream, (int)C, W.scal.p, z, p); }
-    }
+  double* pold = v.pa;
+  double* pnew = v.pb;
+  for (int it = 0;; ++it) {
+    halo_vecs(x, {v.z, pold}, 1, Ce);
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_cg_spmv");
+      hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
+                         cfg.abs_tol, red, WS.scal.p, v, pold, pnew, q1);
+    });
+    if (it >= cfg.max_iter) break;
+    red = L.after(q1, 1);
+    { KScope _ks(x, "k_cg_x"); hipLaunchKernelGGL(k_cg_x, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2); }
     DFMI_HIP(hipGetLastError());
-    DFMI_HIP(hipMemcpyAsync(W.hscal.data(), W.scal.p, 8 * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-    DFMI_HIP(hipStreamSynchronize(x.stream));
-    if (W.hscal[6] == 0.0) break;
+    red = L.after(q2, 2);
+    std::swap(pold, pnew);
+    if ((it + 1) % check == 0) {
+      DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      if (WS.hscal[6] == 0.0) break;
+    }
   }
+  DFMI_HIP(hipGetLastError());
+  DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipStreamSynchronize(x.stream));
   SolveStats st;
-  st.iters = (int)W.hscal[7];
-  st.res0 = W.hscal[4];
-  st.res = W.hscal[4] > 0 ? W.hscal[5] / W.hscal[4] : 0.0;
+  st.iters = (int)WS.hscal[7];
+  st.res0 = WS.hscal[4];
+  st.res = WS.hscal[4] > 0 ? WS.hscal[5] / WS.hscal[4] : 0.0;
   x.last_stats[eqn] = st;
   return st;
 }

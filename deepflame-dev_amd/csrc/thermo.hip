@@ -220,6 +220,9 @@ void thermo_correct(Ctx& x, bool from_T) {
     default: throw Error("dfmi: thermo species count " + std::to_string(x.S) + " not instantiated (2..16)");
   }
 #undef CALL
+  // neighbour halves of the processor slots carry the neighbour rank's cell values
+  if (from_T) halo_fields(x, {"he", "T", "psi", "rho", "mu", "alpha", "rhoD", "hai"});
+  else halo_fields(x, {"T", "psi", "rho", "mu", "alpha", "rhoD", "hai"});
 }
 
 }  // namespace dfmi

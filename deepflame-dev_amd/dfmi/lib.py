@@ -37,6 +37,7 @@ SIGNATURES = {
     "dfmi_set_cyclic_info": [_P, _IP],
     "dfmi_set_comm_info": [_P, C.c_void_p, C.c_int, C.c_int, _IP],
     "dfmi_get_unique_id": [C.c_void_p],
+    "dfmi_set_comm_local": [_P, C.c_int, C.c_int, C.c_int, _IP],
     "dfmi_set_constant_indexes": [_P, _IP, _IP, _IP, _IP, C.c_int],
     "dfmi_init_constant_fields_internal": [_P, _DP, _DP, _DP, _DP, _DP, _DP],
     "dfmi_init_constant_fields_boundary": [_P, _DP, _DP, _DP, _DP, _IP, _IP, _IP],
@@ -138,6 +139,10 @@ class Context:
         a = _i32(neighb)
         buf = C.create_string_buffer(uid, 128)
         self._call("dfmi_set_comm_info", self.h, buf, nranks, rank, _ip(a))
+
+    def set_comm_local(self, hub_id, nranks, rank, neighb):
+        a = _i32(neighb)
+        self._call("dfmi_set_comm_local", self.h, int(hub_id), nranks, rank, _ip(a))
 
     @staticmethod
     def unique_id() -> bytes:

@@ -52,6 +52,11 @@ int dfmi_set_comm_info(dfmi_ctx* ctx, const void* nccl_unique_id, int nranks, in
                        const int* neighb_proc_no);
 /* rank-0 helper: create a fresh RCCL unique id (128 bytes) */
 int dfmi_get_unique_id(void* nccl_unique_id_out);
+/* Same as dfmi_set_comm_info, with an in-process transport instead of RCCL: the contexts of one
+ * process registered under the same hub_id exchange halos by device copies, each driven by its own
+ * host thread. Lets several ranks share one GPU (RCCL refuses two ranks on one device); no
+ * reference counterpart. */
+int dfmi_set_comm_local(dfmi_ctx* ctx, int hub_id, int nranks, int rank, const int* neighb_proc_no);
 /* dfMatrixDataBase::setConstantIndexes (dfMatrixDataBase.cu:184-277) */
 int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighbour, const int* proc_rows,
                               const int* proc_cols, int global_offset);
