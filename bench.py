@@ -42,8 +42,10 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int) -> float:
         # faces: phi, phiUc, w, deltaCoeffs, magSf, owner, neighbour in; lower/upper out (Sa each)
         return C * (8 * 5 * Sa + 24) + F * (5 * 8 + 8 + 16 * Sa) + B * (8 * 8 + 16 * Sa)
     if kernel == "k_cg_spmv":
-        # cells: p, dS in, q out; faces: lower, upper, owner, neighbour
-        return C * 24 + F * 24 + B * 16
+        # fused PCG step p = z + beta p_old; q = A p: cells z, p_old, dS in, p, q out (40 B);
+        # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
+        # ELL gather stores the same 2 x 12 B per face from the two cells' sides); coupled slots 12 B
+        return C * 40 + F * 24 + B * 12
     if kernel == "k_bcg_spmv":
         return C * 24 + F * 24 + B * 16
     if kernel == "k_thermo_cells":
