@@ -28,7 +28,8 @@ sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 
-MECHS = {
+MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species table made by dfmi.transport_fit
+    "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
     "es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt"),
 }
 
@@ -60,7 +61,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
-    ap.add_argument("--mech", default="es80", choices=sorted(MECHS))
+    ap.add_argument("--mech", default="burke9", choices=sorted(MECHS))
     ap.add_argument("--ncorr", type=int, default=2)
     ap.add_argument("--dt", type=float, default=1e-6)
     ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")

@@ -65,8 +65,8 @@ def read_yaml_mechanism(path: str) -> dict:
     phase = doc["phases"][0]
     names = phase["species"]
     spec = {s["name"]: s for s in doc["species"]}
-    out = {"species": list(names), "W": [], "nasa": [], "transport": [], "composition": [],
-           "reactions": doc.get("reactions", [])}
+    out = {"species": list(names), "W": [], "nasa": [], "transport": [], "composition": [], "trange": [],
+           "reactions": doc.get("reactions", []), "phase": phase}
     for n in names:
         s = spec[n]
         comp = s["composition"]
@@ -77,6 +77,7 @@ def read_yaml_mechanism(path: str) -> dict:
         lo, hi = th["data"]
         row = [float(tr[1])] + [float(x) for x in hi] + [float(x) for x in lo]
         out["nasa"].append(row)
+        out["trange"].append((float(tr[0]), float(tr[-1])))
         out["transport"].append(s.get("transport", {}))
     out["W"] = np.array(out["W"])
     out["nasa"] = np.array(out["nasa"])

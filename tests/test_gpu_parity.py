@@ -15,13 +15,17 @@ from conftest import rel_err, ulp_diff, GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0)):
+MECHS = {"es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt"),
+         "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt")}
+
+
+def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80"):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi.lib import Context
     from dfmi import case
-    ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
-    t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, MECHS[mech][0]))
+    t = read_thermo_table(os.path.join(GOLDEN, MECHS[mech][1]), ym["species"])
     L = 1e-3
     m = hex_box(nx, ny, nz, lengths=(2 * np.pi * L,) * 3, periodic=(periodic,) * 3, gradings=gradings)
     ctx = Context(0)
@@ -53,9 +57,20 @@ def _oracle(m, t, st, pt, inert, dt):
     return O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt)
 
 
-@pytest.fixture(scope="module")
-def periodic():
-    return _case()
+@pytest.fixture(scope="module", params=["es80", "burke9", "walls"])
+def periodic(request):
+    if request.param == "walls":      # non-periodic box: zeroGradient walls (+ fixedValue T/Y/U on two sides)
+        from dfmi.mesh import FIXED_VALUE
+
+        def walls(m):
+            fv = {}
+            for f in ("U", "T", "Y"):
+                t = m.patch_types(0).copy()
+                t[[i for i, p in enumerate(m.patches) if p.name in ("left", "right")]] = FIXED_VALUE
+                fv[f] = t
+            return fv
+        return _case(periodic=False, walls=walls, mech="burke9")
+    return _case(mech=request.param)
 
 
 def _cmp_matrix(ctx, eqn, o, parts, B, nsys=1):
