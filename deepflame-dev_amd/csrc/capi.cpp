@@ -67,7 +67,7 @@ void allocate_fields(Ctx& x) {
   mk(x.mE, 1, 1, 1);
   mk(x.mP, 1, 1, 1);
   for (auto e : {"U", "Y", "E"}) if (!x.solver.count(e)) x.solver[e] = SolverCfg{20, 1e-5, 0.0};   // amgxUOptions
-  if (!x.solver.count("p")) x.solver["p"] = SolverCfg{1000, 1e-5, 0.0};                          // amgxpOptions
+  if (!x.solver.count("p")) x.solver["p"] = SolverCfg{1000, 1e-5, 0.0, 1};   // amgxpOptions: AMG-preconditioned
 }
 
 // Build the deterministic gather topology from owner/neighbour and the boundary face cells.
@@ -527,7 +527,17 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
     std::string e(eqn);
     DFMI_CHECK(e == "U" || e == "Y" || e == "E" || e == "p", "unknown equation '" + e + "'");
     DFMI_CHECK(max_iter > 0 && tol >= 0 && abs_tol >= 0, "bad solver controls");
-    ctx->x.solver[e] = SolverCfg{max_iter, tol, abs_tol};
+    SolverCfg& c = ctx->x.solver[e];
+    c.max_iter = max_iter; c.tol = tol; c.abs_tol = abs_tol;
+  });
+}
+
+int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
+  return guard([&] {
+    std::string e(eqn), n(name);
+    DFMI_CHECK(e == "U" || e == "Y" || e == "E" || e == "p", "unknown equation '" + e + "'");
+    DFMI_CHECK(n == "jacobi" || (n == "amg" && e == "p"), "preconditioner must be 'jacobi' or ('amg' for p)");
+    ctx->x.solver[e].precond = n == "amg" ? 1 : 0;
   });
 }
 

@@ -13,6 +13,7 @@
 // Visiting nbrFace, then own faces, then cbSlot is exactly OpenFOAM's sequential face order.
 #pragma once
 #include "dfmi_common.h"
+#include "amg.h"
 #include <map>
 #include <memory>
 
@@ -44,6 +45,7 @@ struct SolverCfg {
   int max_iter = 20;
   double tol = 1e-5;           // relative to the initial residual (AmgX RELATIVE_INI, amgxUOptions)
   double abs_tol = 0.0;
+  int precond = 0;             // 0 Jacobi, 1 aggregation AMG (p only)
 };
 
 struct SolveStats { int iters = 0; double res0 = 0, res = 0; };
@@ -112,6 +114,7 @@ struct Ctx {
     DevBuf<int> col;             // column: cell id, or C + halo index for a processor face
     DevBuf<int> src;             // coefficient: 2f = lower[f], 2f+1 = upper[f], -(b+1) = -boundaryCoeffs[b]
   } ell;
+  Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
   struct SolverWs {
     DevBuf<double> buf, scal, red_local, red_all;
     DevBuf<int> sysmap;

@@ -292,12 +292,13 @@ __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, const int* __res
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __restrict__ col,
                                                  const double* __restrict__ val, int it, int max_iter, double tol,
-                                                 double abs_tol, Red red, double* scal, CV v,
+                                                 double abs_tol, Red red_rz, Red red_rr, double* scal, CV v,
                                                  const double* __restrict__ pold, double* __restrict__ pnew,
                                                  double* partial) {
-  double rv[2];
-  red_sum<2>(red, 0, rv);
-  const double rz = rv[0], res = sqrt(rv[1]);
+  double a[1], b[1];
+  red_sum<1>(red_rz, 0, a);
+  red_sum<1>(red_rr, 0, b);
+  const double rz = a[0], res = sqrt(b[0]);
   const double res0 = it == 0 ? res : scal[4];
   const double rzp = scal[1];
   const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && rzp == 0.0);
@@ -327,7 +328,9 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
   block_partials<1>(acc, partial, 0);
 }
 
-// prologue: alpha = rz / (p.q); x += alpha p; r -= alpha q; z = r / dS; partials (r.z, r.r)
+// prologue: alpha = rz / (p.q); x += alpha p; r -= alpha q; partials (r.z, r.r); with the Jacobi
+// preconditioner also z = r / dS (AMG computes z separately and writes r.z itself)
+template <bool JAC>
 __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, double* __restrict__ x, CV v,
                                               const double* __restrict__ pnew, double* partial) {
   if (scal[6] == 0.0) return;
@@ -341,9 +344,12 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
     x[c] = x[c] + alpha * pnew[c];
     const double rr = v.r[c] - alpha * v.q[c];
     v.r[c] = rr;
-    const double zz = rr / v.dS[c];
-    v.z[c] = zz;
-    acc[0] += rr * zz; acc[1] += rr * rr;
+    if (JAC) {
+      const double zz = rr / v.dS[c];
+      v.z[c] = zz;
+      acc[0] += rr * zz;
+    }
+    acc[1] += rr * rr;
   }
   block_partials<2>(acc, partial, 0);
 }
@@ -399,19 +405,20 @@ void build_ell(Ctx& x) {
 struct Launch {
   Ctx& x;
   int nblk, nsys;
-  Red after(double* partial, int NV) {   // make the partials of the last kernel readable by the next
+  // make the partials of the last kernel readable by the next (slot: independent buffers for
+  // reductions that are alive at the same time)
+  Red after(double* partial, int NV, int slot = 0) {
     if (x.nranks == 1) return Red{partial, nblk, NV, (long)nblk * NV};
-    SolverWsRed();
-    if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, x.ws.red_local.p);
-    else hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, x.ws.red_local.p);
+    const size_t per = (size_t)nsys * 2;
+    if (x.ws.red_local.n < 2 * per) x.ws.red_local.alloc(2 * per);
+    if (x.ws.red_all.n < 2 * per * x.nranks) x.ws.red_all.alloc(2 * per * x.nranks);
+    double* loc = x.ws.red_local.p + slot * per;
+    double* all = x.ws.red_all.p + slot * per * x.nranks;
+    if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    else hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
     DFMI_HIP(hipGetLastError());
-    halo_allgather(x, x.ws.red_local.p, x.ws.red_all.p, (long)nsys * NV);
-    return Red{x.ws.red_all.p, x.nranks, (long)nsys * NV, NV};
-  }
-  void SolverWsRed() {
-    const size_t need = (size_t)nsys * 2;
-    if (x.ws.red_local.n < need) x.ws.red_local.alloc(need);
-    if (x.ws.red_all.n < need * x.nranks) x.ws.red_all.alloc(need * x.nranks);
+    halo_allgather(x, loc, all, (long)nsys * NV);
+    return Red{all, x.nranks, (long)nsys * NV, NV};
   }
 };
 
@@ -529,22 +536,28 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   auto& WS = x.ws;
-  const size_t need = 8 * Ce + (size_t)W * C + (size_t)nblk * 4 + 64;
+  const size_t need = 8 * Ce + (size_t)W * C + (size_t)nblk * 6 + 64;
   if (WS.buf.n < need) WS.buf.alloc(need);
   if (WS.scal.n < NSCAL) WS.scal.alloc(NSCAL);
   double* base = WS.buf.p;
   CV v{base, base + Ce, base + 2 * Ce, base + 3 * Ce, base + 4 * Ce, base + 5 * Ce, base + 6 * Ce, base + 7 * Ce};
   double* val = base + 8 * Ce;
   double* q1 = val + (size_t)W * C;    // p.q
-  double* q2 = q1 + (size_t)nblk * 2;  // (r.z, r.r)
+  double* q2 = q1 + (size_t)nblk * 2;  // (r.z [Jacobi], r.r)
+  double* q3 = q2 + (size_t)nblk * 2;  // r.z (AMG)
   Sys q{lower, upper, diag, source, ic, bc, 0, 0, 0, 0, 0, xsol, 0};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk), bl(TPB);
   Launch L{x, nblk, 1};
+  const bool amg = cfg.precond == 1;
   { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs); }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());
+  if (amg) {
+    if (!x.amg.ready) amg_setup(x);
+    amg_galerkin(x, val, v.dS);
+  }
   halo_vecs(x, {v.xw}, 1, Ce);
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
@@ -552,9 +565,19 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, v, q2);
   });
   DFMI_HIP(hipGetLastError());
-  Red red = L.after(q2, 2);
+  // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
+  auto reds = [&](Red& rz, Red& rr) {
+    Red r2 = L.after(q2, 2, 0);
+    rr = r2; rr.p += 1;
+    if (amg) {
+      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk);
+      rz = L.after(q3, 1, 1);
+    } else rz = r2;
+  };
+  Red red_rz, red_rr;
+  reds(red_rz, red_rr);
   WS.hscal.resize(NSCAL);
-  const int check = 8;
+  const int check = amg ? 2 : 8;
   double* pold = v.pa;
   double* pnew = v.pb;
   for (int it = 0;; ++it) {
@@ -563,13 +586,17 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_cg_spmv");
       hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
-                         cfg.abs_tol, red, WS.scal.p, v, pold, pnew, q1);
+                         cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1);
     });
     if (it >= cfg.max_iter) break;
-    red = L.after(q1, 1);
-    { KScope _ks(x, "k_cg_x"); hipLaunchKernelGGL(k_cg_x, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2); }
+    Red red = L.after(q1, 1);
+    {
+      KScope _ks(x, "k_cg_x");
+      if (amg) hipLaunchKernelGGL(k_cg_x<false>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
+      else hipLaunchKernelGGL(k_cg_x<true>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
+    }
     DFMI_HIP(hipGetLastError());
-    red = L.after(q2, 2);
+    reds(red_rz, red_rr);
     std::swap(pold, pnew);
     if ((it + 1) % check == 0) {
       DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));

@@ -56,6 +56,7 @@ SIGNATURES = {
     "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
     "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
+    "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
@@ -211,6 +212,9 @@ class Context:
 
     def set_solver(self, eqn, max_iter, tol, abs_tol=0.0):
         self._call("dfmi_set_solver", self.h, eqn.encode(), int(max_iter), float(tol), float(abs_tol))
+
+    def set_preconditioner(self, eqn, name):
+        self._call("dfmi_set_preconditioner", self.h, eqn.encode(), name.encode())
 
     def solver_stats(self, eqn):
         it = C.c_int(); r0 = C.c_double(); rel = C.c_double()

@@ -121,6 +121,9 @@ int dfmi_assemble(dfmi_ctx* ctx, const char* eqn);
 int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count);
 /* solver controls (amgxUOptions / amgxpOptions): eqn in {"U","Y","E","p"} */
 int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, double abs_tol);
+/* preconditioner: "jacobi" (all) or "amg" (p; aggregation AMG V-cycle, the amgxpOptions
+ * AGGREGATION solver's role) -- p defaults to "amg", U/Y/E to "jacobi" */
+int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
 

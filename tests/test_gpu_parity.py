@@ -205,3 +205,28 @@ def test_full_outer_iteration(periodic):
     for e in ("U", "Y", "E"):
         ctx.set_solver(e, 20, 1e-5)
     ctx.set_solver("p", 1000, 1e-5)
+
+
+@pytest.mark.parametrize("coarsest", ["16", "4096"])
+def test_amg_pcg_full_step(coarsest, monkeypatch):
+    """AMG-preconditioned p solves (multi-level hierarchy forced on a small mesh) reach the oracle's
+    exact solution; AMG needs fewer iterations than Jacobi."""
+    monkeypatch.setenv("DFMI_AMG_COARSEST", coarsest)
+    ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
+    for e in ("U", "Y", "E"):
+        ctx.set_solver(e, 300, 1e-15, 1e-300)
+    ctx.set_solver("p", 3000, 1e-14, 1e-300)
+    o = _oracle(m, t, st, pt, inert, dt)
+    o.time_step(2)
+    ctx.time_step(2)
+    it_amg = ctx.solver_stats("p")[0]
+    for n, tl in {"T": 1e-10, "p": 1e-11, "rho": 1e-10}.items():
+        got = ctx.get_field(n, (m.n_cells,))
+        assert rel_err(got, o[n]) < tl, (n, rel_err(got, o[n]))
+    assert rel_err(ctx.get_field("U", (3, m.n_cells)), o["U"]) < 1e-9
+    from dfmi import case
+    case.push_state(ctx, st)
+    ctx.set_preconditioner("p", "jacobi")
+    ctx.time_step(2)
+    it_jac = ctx.solver_stats("p")[0]
+    assert it_amg < it_jac, (it_amg, it_jac)
