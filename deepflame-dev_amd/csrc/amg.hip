@@ -24,7 +24,7 @@ namespace dfmi {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int COARSEST = 4096;   // LDS capacity of k_coarsest (doubles, two buffers)
+constexpr int COARSEST = 1024;   // k_coarsest capacity (cells); also n * W <= LDS_ENT
 constexpr int CTPB = 1024;
 
 // ---------------------------------------------------------------- kernels
@@ -47,13 +47,17 @@ __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, co
 }
 
 // x = omega b / D (first sweep from zero); r = b - A x   (columns >= n: other ranks, dropped)
-__global__ void k_smooth_res(int n, int W, const int* __restrict__ col, const double* __restrict__ val,
-                             const double* __restrict__ D, const double* __restrict__ b, double omega,
-                             double* __restrict__ x, double* __restrict__ r) {
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __restrict__ col,
+                                                    const double* __restrict__ val, const double* __restrict__ D,
+                                                    const double* __restrict__ b, double omega,
+                                                    double* __restrict__ x, double* __restrict__ r) {
+  const int W = WT > 0 ? WT : W_;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
   const double xc = omega * b[c] / D[c];
   double y = D[c] * xc;
+#pragma unroll
   for (int k = 0; k < W; ++k) {
     const int j = col[(long)k * n + c];
     if (j < n) y += val[(long)k * n + c] * (omega * b[j] / D[j]);
@@ -72,16 +76,19 @@ __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __
 }
 
 // y = x + P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z)
-__global__ void k_prolong_smooth(int n, int W, const int* __restrict__ col, const double* __restrict__ val,
-                                 const double* __restrict__ D, const double* __restrict__ b,
-                                 const double* __restrict__ x, const int* __restrict__ agg,
-                                 const double* __restrict__ xc, double omega, double* __restrict__ out,
-                                 double* partial) {
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int* __restrict__ col,
+                                                        const double* __restrict__ val, const double* __restrict__ D,
+                                                        const double* __restrict__ b, const double* __restrict__ x,
+                                                        const int* __restrict__ agg, const double* __restrict__ xc,
+                                                        double omega, double* __restrict__ out, double* partial) {
+  const int W = WT > 0 ? WT : W_;
   __shared__ double sh[TPB / 64];
   double acc = 0.0;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const double yc = x[c] + xc[agg[c]];
     double ay = D[c] * yc;
+#pragma unroll
     for (int k = 0; k < W; ++k) {
       const int j = col[(long)k * n + c];
       if (j < n) ay += val[(long)k * n + c] * (x[j] + xc[agg[j]]);
@@ -115,24 +122,30 @@ __global__ void k_dot_partial(int n, const double* __restrict__ a, const double*
   }
 }
 
-// coarsest level: `sweeps` weighted-Jacobi sweeps from zero in one workgroup (vectors in LDS)
+// coarsest level: `sweeps` weighted-Jacobi sweeps from zero in one workgroup; operator and vectors
+// staged in LDS (n * W <= LDS_ENT), so the sweeps run at LDS latency
+constexpr int LDS_ENT = 6144;
 __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __restrict__ col,
                                                    const double* __restrict__ val, const double* __restrict__ D,
                                                    const double* __restrict__ b, double omega, int sweeps,
                                                    double* __restrict__ x) {
   __shared__ double xa[COARSEST], xb[COARSEST];
-  for (int c = threadIdx.x; c < n; c += CTPB) xa[c] = omega * b[c] / D[c];
+  __shared__ double sv[LDS_ENT];
+  __shared__ int sc[LDS_ENT];
+  __shared__ double sd[COARSEST], sb[COARSEST];
+  for (int e = threadIdx.x; e < n * W; e += CTPB) { sv[e] = val[e]; sc[e] = col[e]; }
+  for (int c = threadIdx.x; c < n; c += CTPB) { sd[c] = D[c]; sb[c] = b[c]; xa[c] = omega * b[c] / D[c]; }
   __syncthreads();
   double* cur = xa;
   double* nxt = xb;
   for (int s = 1; s < sweeps; ++s) {
     for (int c = threadIdx.x; c < n; c += CTPB) {
-      double y = D[c] * cur[c];
+      double y = sd[c] * cur[c];
       for (int k = 0; k < W; ++k) {
-        const int j = col[(long)k * n + c];
-        if (j < n) y += val[(long)k * n + c] * cur[j];
+        const int j = sc[k * n + c];
+        if (j < n) y += sv[k * n + c] * cur[j];
       }
-      nxt[c] = cur[c] + omega * (b[c] - y) / D[c];
+      nxt[c] = cur[c] + omega * (sb[c] - y) / sd[c];
     }
     __syncthreads();
     double* t = cur; cur = nxt; nxt = t;
@@ -296,7 +309,7 @@ void amg_setup(Ctx& x) {
   a.lv.clear();
   a.omega = env_d("DFMI_AMG_OMEGA", 0.6);
   a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 24);
-  a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", COARSEST)));
+  a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
   const int C = x.C;
   // level 0: the solver ELL (columns >= C are halo entries, dropped in the preconditioner)
   std::vector<int> col((size_t)x.ell.W * C);
@@ -347,7 +360,8 @@ void amg_setup(Ctx& x) {
   a.lv[0].W = x.ell.W;
   a.lv[0].x.alloc(C); a.lv[0].r.alloc(C); a.lv[0].xo.alloc(C);
   std::vector<int> fcol = col;
-  while (a.lv.back().n > a.coarsest) {
+  auto too_big = [&](const AmgLevel& l) { return l.n > a.coarsest || (size_t)l.n * l.W > 6144; };
+  while (too_big(a.lv.back())) {
     AmgLevel c;
     std::vector<int> ccol;
     Graph cg;
@@ -359,7 +373,7 @@ void amg_setup(Ctx& x) {
     g = std::move(cg);
     if (stalled) break;
   }
-  DFMI_CHECK(a.lv.back().n <= COARSEST, "AMG coarsening stalled above the coarsest-level capacity");
+  DFMI_CHECK(!too_big(a.lv.back()) || a.lv.back().n <= 8, "AMG coarsening stalled above the coarsest-level capacity");
   a.ready = true;
 }
 
@@ -395,8 +409,12 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, co
     AmgLevel& f = a.lv[l];
     {
       KScope _ks(x, "k_smooth_res");
-      hipLaunchKernelGGL(k_smooth_res, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l),
-                         DD(l), B(l), om, f.x.p, f.r.p);
+      if (f.W == 6)
+        hipLaunchKernelGGL(k_smooth_res<6>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
+                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
+      else
+        hipLaunchKernelGGL(k_smooth_res<0>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
+                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
     }
     {
       KScope _ks(x, "k_restrict");
@@ -421,8 +439,12 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, co
     double* out = l == 0 ? z : f.xo.p;
     KScope _ks(x, "k_prolong_smooth");
     const dim3 grid = l == 0 ? dim3(nblk) : dim3(blocks_for(f.n, TPB));
-    hipLaunchKernelGGL(k_prolong_smooth, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l),
-                       DD(l), B(l), f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
+    if (f.W == 6)
+      hipLaunchKernelGGL(k_prolong_smooth<6>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
+                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
+    else
+      hipLaunchKernelGGL(k_prolong_smooth<0>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
+                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
     if (l > 0) std::swap(f.x, f.xo);   // the corrected x of this level feeds the next finer prolongation
   }
   DFMI_HIP(hipGetLastError());
