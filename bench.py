@@ -216,6 +216,7 @@ def main():
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
                      "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
         "solver_iters": {e: s[0] for e, s in stats.items()},
+        "amg_levels": ctx.amg_info(),
         "finite": finite,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

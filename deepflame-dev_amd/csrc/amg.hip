@@ -172,7 +172,9 @@ int pair_match(const Graph& g, std::vector<int>& grp) {
     for (int e = g.start[v]; e < g.start[v + 1]; ++e) {
       const int u = g.adj[e];
       if (u == v || grp[u] >= 0) continue;
-      if (g.w[e] > bw || (g.w[e] == bw && u < best)) { bw = g.w[e]; best = u; }
+      // strengths within 1e-9 relative are ties (rounding must not break the geometric pattern)
+      if (g.w[e] > bw * (1 + 1e-9)) { bw = g.w[e]; best = u; }
+      else if (std::fabs(g.w[e] - bw) <= 1e-9 * bw && u < best) best = u;
     }
     grp[v] = ng;
     if (best >= 0) grp[best] = ng;

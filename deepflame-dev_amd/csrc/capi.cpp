@@ -532,6 +532,14 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
   });
 }
 
+int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width) {
+  return guard([&] {
+    const Amg& a = ctx->x.amg;
+    *n_levels = (int)a.lv.size();
+    for (int l = 0; l < (int)a.lv.size() && l < max_levels; ++l) { cells[l] = a.lv[l].n; width[l] = a.lv[l].W; }
+  });
+}
+
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
   return guard([&] {
     std::string e(eqn), n(name);

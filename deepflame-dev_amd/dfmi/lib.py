@@ -57,6 +57,7 @@ SIGNATURES = {
     "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
     "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
+    "dfmi_amg_info": [_P, C.c_int, _IP, _IP, _IP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
@@ -215,6 +216,11 @@ class Context:
 
     def set_preconditioner(self, eqn, name):
         self._call("dfmi_set_preconditioner", self.h, eqn.encode(), name.encode())
+
+    def amg_info(self):
+        n = C.c_int(); cells = np.zeros(32, np.int32); w = np.zeros(32, np.int32)
+        self._call("dfmi_amg_info", self.h, 32, C.byref(n), _ip(cells), _ip(w))
+        return [(int(cells[i]), int(w[i])) for i in range(n.value)]
 
     def solver_stats(self, eqn):
         it = C.c_int(); r0 = C.c_double(); rel = C.c_double()

@@ -124,6 +124,8 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
 /* preconditioner: "jacobi" (all) or "amg" (p; aggregation AMG V-cycle, the amgxpOptions
  * AGGREGATION solver's role) -- p defaults to "amg", U/Y/E to "jacobi" */
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
+/* AMG hierarchy after the first p solve: level count, cells and ELL width per level */
+int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width);
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
 
