@@ -17,8 +17,8 @@ struct AmgLevel {
 
 struct Amg {
   bool ready = false;
-  double omega = 0.6;
-  int coarse_sweeps = 24;
+  double omega = 0.85;
+  int coarse_sweeps = 8;
   int coarsest = 4096;
   std::vector<AmgLevel> lv;
 };

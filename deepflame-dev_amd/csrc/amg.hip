@@ -309,8 +309,8 @@ double env_d(const char* k, double d) { const char* v = std::getenv(k); return v
 void amg_setup(Ctx& x) {
   Amg& a = x.amg;
   a.lv.clear();
-  a.omega = env_d("DFMI_AMG_OMEGA", 0.6);
-  a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 24);
+  a.omega = env_d("DFMI_AMG_OMEGA", 0.85);
+  a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
   a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
   const int C = x.C;
   // level 0: the solver ELL (columns >= C are halo entries, dropped in the preconditioner)
