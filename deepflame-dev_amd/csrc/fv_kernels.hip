@@ -455,26 +455,51 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
-  double g[S][3];
+  // One pass over the cell's faces computes every species' Gauss gradient AND its diffAlphaD
+  // laplacian term (the two per-species face loops of the sequential code fused; each accumulator
+  // still sums in face order, so the result is bitwise the sequential one). Own-cell values live
+  // in registers; each face loads the neighbour's Y_s and hai_s once.
+  double g[S][3], lap[S], yc[S], ahc[S];
+  const double ac = alpha[c];
 #pragma unroll
-  for (int s = 0; s < S; ++s) { g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; }
+  for (int s = 0; s < S; ++s) {
+    g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0;
+    yc[s] = Y[s * C + c];
+    ahc[s] = ac * hai[s * C + c];
+  }
   each_face(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
     const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+    const double ms = m.magSf[f], dcf = m.dc[f];
+    const double an = alpha[o2];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const double yf = interp_f(w, Y[s * C + o], Y[s * C + n]);
+      const double yn = Y[s * C + o2];
+      const double ahn = an * hai[s * C + o2];
+      const double yf = own ? interp_f(w, yc[s], yn) : interp_f(w, yn, yc[s]);
       const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
-      if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; }
-      else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; }
+      const double gam = own ? interp_f(w, ahc[s], ahn) : interp_f(w, ahn, ahc[s]);
+      const double dy = own ? yn - yc[s] : yc[s] - yn;
+      const double v = gam * ms * (dcf * dy);
+      if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
+      else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
     }
   });
   each_slot(m, tyY, c, [&](int b, int t) {
+    const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) g[s][k] += m.bSf[k * B + b] * yf;
+      g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
+      double v;
+      if (bc_coupled(t)) {
+        const int pc = m.partner[b];
+        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+        v = interp_b(m.bw[b], ahc[s], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[s]));
+      } else {
+        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
+        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+      }
+      lap[s] += v;
     }
   });
   const double vol = m.V[c];
@@ -488,49 +513,28 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
 #pragma unroll
       for (int k = 0; k < 3; ++k) gout[(3L * s + k) * C + c] = g[s][k];
   }
-  double se[3], hd[3];
+  double se[3], hd[3], rd[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) rd[s] = rhoD[s * C + c];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double a = 0.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) a += rhoD[s * C + c] * g[s][k];
+    for (int s = 0; s < S; ++s) a += rd[s] * g[s][k];
     se[k] = a;
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double a = 0.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) a += hai[s * C + c] * (rhoD[s * C + c] * g[s][k] - Y[s * C + c] * se[k]);
+    for (int s = 0; s < S; ++s) a += hai[s * C + c] * (rd[s] * g[s][k] - yc[s] * se[k]);
     hd[k] = a;
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) { sumE[k * C + c] = se[k]; hD[k * C + c] = hd[k]; }
-  // diffAlphaD = sum_s laplacian(alpha*hai_s, Y_s)
   double dad = 0.0;
-  const double ac = alpha[c];
-  for (int s = 0; s < S; ++s) {
-    const double* ys = Y + s * C;
-    const double* hs = hai + s * C;
-    double lap = 0.0;
-    each_face(m, c, [&](int f, int o2, bool own) {
-      const int o = own ? c : o2, n = own ? o2 : c;
-      const double v = interp_f(m.w[f], alpha[o] * hs[o], alpha[n] * hs[n]) * m.magSf[f] * (m.dc[f] * (ys[n] - ys[o]));
-      if (own) lap += v; else lap -= v;
-    });
-    each_slot(m, tyY, c, [&](int b, int t) {
-      double v;
-      if (bc_coupled(t)) {
-        const int pc = m.partner[b];
-        const double an = pc >= 0 ? alpha[pc] * hs[pc] : balpha[b] * bhai[s * B + b];
-        v = interp_b(m.bw[b], ac * hs[c], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, ys, bY + s * B, b) - ys[c]));
-      } else {
-        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - ys[c]) : 0.0;
-        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
-      }
-      lap += v;
-    });
-    dad = dad + lap / vol;
-  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) dad = dad + lap[s] / vol;
   dAD[c] = dad;
   // boundary fields of the non-coupled slots (coupled slots interpolate cell values downstream)
   each_slot(m, tyY, c, [&](int b, int t) {
@@ -604,11 +608,10 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, d2 = 0.0;
-  double dL[S];
+  double dL[S], rc[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) dL[s] = 0.0;
+  for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
   each_face(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
     const double ph = phi[f], pu = phiUc[f];
     const double wu = ph >= 0 ? 1.0 : 0.0;
     const double L1 = -wu * ph, U1 = L1 + ph;
@@ -619,7 +622,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       if (s == inert) continue;
-      const double UL = dcf * (interp_f(w, rhoD[s * C + o], rhoD[s * C + n]) * ms);
+      const double rn = rhoD[s * C + o2];
+      const double UL = dcf * ((own ? interp_f(w, rc[s], rn) : interp_f(w, rn, rc[s])) * ms);
       dL[s] -= UL;
       if (own) { lower[s * F + f] = Ls - UL; upper[s * F + f] = Us - UL; }
     }
