@@ -45,6 +45,7 @@ void allocate_fields(Ctx& x) {
     alloc_field(x, std::string("boundary_") + n, B, 3, true);
   }
   alloc_field(x, "tauU", C, 9, false);
+  alloc_field(x, "chem_stats", C, 2, false);   // per cell: accepted / rejected integrator steps
   alloc_field(x, "boundary_tauU", B, 9, true);
   for (auto n : {"Y", "rhoD", "hai", "RR"}) {
     alloc_field(x, n, C, S, false);
@@ -166,6 +167,7 @@ void do_U(Ctx& x) {
 }
 void do_Y(Ctx& x) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
+  if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt);   // chemistry->solve(deltaT) before YEqn (YEqn.H)
   y_prep(x);
   y_assemble(x);
   Matrix& A = x.mY;
@@ -529,6 +531,32 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
     DFMI_CHECK(max_iter > 0 && tol >= 0 && abs_tol >= 0, "bad solver controls");
     SolverCfg& c = ctx->x.solver[e];
     c.max_iter = max_iter; c.tol = tol; c.abs_tol = abs_tol;
+  });
+}
+
+int dfmi_chem_set_mechanism(dfmi_ctx* ctx, int n_reactions, const int* idata, const int* irs, const double* ddata) {
+  return guard([&] {
+    DFMI_CHECK(ctx->x.have_sizes, "call dfmi_set_constant_values first");
+    chem_upload(ctx->x, n_reactions, idata, irs, ddata);
+  });
+}
+
+int dfmi_chem_set_options(dfmi_ctx* ctx, int mode, double rtol, double atol, double T_min) {
+  return guard([&] {
+    DFMI_CHECK(mode >= 0 && mode <= 2, "chemistry mode must be 0 (off), 1 (ODE) or 2 (DNN)");
+    DFMI_CHECK(rtol > 0 && atol > 0, "chemistry tolerances must be positive");
+    Chem& c = ctx->x.chem;
+    c.mode = mode; c.rtol = rtol; c.atol = atol; c.Tmin = T_min;
+  });
+}
+
+int dfmi_chem_solve(dfmi_ctx* ctx, double dt) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    DFMI_CHECK(dt > 0, "chemistry time step must be positive");
+    chem_solve(x, dt);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
   });
 }
 

@@ -1,0 +1,381 @@
+// chem.hip -- per-cell stiff chemistry on MI355X.
+//
+// Semantics of the reference chemistry step (dfChemistryModel::solveSingle,
+// src/dfChemistryModel/dfChemistryModel.C:737-780; GPU ABI precedent opencc_ode_all, YEqn.H:45-77):
+// every cell is a closed constant-volume reactor at FIXED temperature and density integrated over
+// the flow time step; the species source is RR_i = (Y_i(dt) - Y_i(0)) rho / dt. Kinetics follow
+// Cantera GasKinetics: Arrhenius rates, three-body efficiencies, Lindemann/Troe fall-off, reverse
+// rates from NASA7 equilibrium constants.
+//
+// Integrator: linearly-implicit Euler extrapolation (Deuflhard's SEULEX idea) with step sequence
+// 1, 2, 3 -> order 3, embedded error estimate T33 - T32, adaptive step size, analytic Jacobian of
+// the mass-action terms (fall-off [M]-dependence of k omitted: a W-method approximation the step
+// control absorbs). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
+// mass fractions) by default.
+//
+// Layout: one cell per lane, 64-lane workgroups. Per-lane rate constants (they depend only on T,
+// which is frozen) and the per-lane S x S iteration matrix live in LDS as [entry][lane]
+// (bank-conflict free); state vectors live in registers (compile-time S). The mechanism arrays are
+// wave-uniform (scalar loads).
+#include "dfmi_ctx.h"
+#include <cmath>
+
+namespace dfmi {
+namespace {
+
+constexpr int LANES = 64;
+constexpr double RU = 8314.46261815324;
+constexpr double P_ATM = 101325.0;
+
+struct ChemMech {
+  int R, ndd;
+  const int* idata;    // [R][8]: type, reversible, n_reac, n_prod, has_T2
+  const int* irs;      // [R][6]: reactant ids (3), product ids (3), -1 padded
+  const double* dd;    // [R][ndd]: A b Ta nu_r[3] nu_p[3] A0 b0 Ta0 troe[4] eff[S]
+  const double* nasa;  // [S][15]
+  const double* W;     // [S]
+};
+
+template <int S> struct Lane {
+  double* kf;   // LDS [R][LANES]
+  double* k0;
+  double* ikc;  // 1/Kc, 0 for irreversible
+  double* A;    // LDS [S*S][LANES]
+  int lane;
+  __device__ double& K(double* b, int r) const { return b[r * LANES + lane]; }
+  __device__ double& M(int i, int j) const { return A[(i * S + j) * LANES + lane]; }
+};
+
+template <int S>
+__device__ void rate_constants(const ChemMech& m, const Lane<S>& L, double T) {
+  const double lnT = log(T), rT = 1.0 / T;
+  double g[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {   // g_i / RT from NASA7
+    const double* row = m.nasa + i * 15;
+    const double* a = T > row[0] ? row + 1 : row + 8;
+    const double h = a[0] + a[1] * T / 2 + a[2] * T * T / 3 + a[3] * T * T * T / 4 + a[4] * T * T * T * T / 5 + a[5] / T;
+    const double s = a[0] * lnT + a[1] * T + a[2] * T * T / 2 + a[3] * T * T * T / 3 + a[4] * T * T * T * T / 4 + a[6];
+    g[i] = h - s;
+  }
+  for (int r = 0; r < m.R; ++r) {
+    const int* id = m.idata + r * 8;
+    const int* ix = m.irs + r * 6;
+    const double* d = m.dd + (long)r * m.ndd;
+    L.K(L.kf, r) = d[0] * exp(d[1] * lnT - d[2] * rT);
+    L.K(L.k0, r) = id[0] >= 2 ? d[9] * exp(d[10] * lnT - d[11] * rT) : 0.0;
+    double ik = 0.0;
+    if (id[1]) {
+      double dG = 0.0, dnu = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        const int ip = ix[3 + k], ir = ix[k];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {   // wave-uniform species ids; unrolled select keeps g in registers
+          if (ip == i) { dG += d[6 + k] * g[i]; }
+          if (ir == i) { dG -= d[3 + k] * g[i]; }
+        }
+        if (ip >= 0) dnu += d[6 + k];
+        if (ir >= 0) dnu -= d[3 + k];
+      }
+      // 1/Kc = exp(dG) (p_atm / RT)^-dnu
+      ik = exp(dG - dnu * log(P_ATM / (RU * T)));
+    }
+    L.K(L.ikc, r) = ik;
+  }
+}
+
+template <int S> __device__ __forceinline__ double sel(const double (&v)[S], int i) {
+  double o = 0.0;
+#pragma unroll
+  for (int k = 0; k < S; ++k) o = (k == i) ? v[k] : o;
+  return o;
+}
+template <int S> __device__ __forceinline__ void add_at(double (&v)[S], int i, double a) {
+#pragma unroll
+  for (int k = 0; k < S; ++k) if (k == i) v[k] += a;
+}
+
+// effective rate coefficient and the third-body factor of reaction r
+template <int S>
+__device__ __forceinline__ void rcoef(const ChemMech& m, const Lane<S>& L, int r, double T, const double (&C)[S],
+                                      double& k, double& Mf, double& Mc) {
+  const int* id = m.idata + r * 8;
+  const double* d = m.dd + (long)r * m.ndd;
+  k = L.K(L.kf, r);
+  Mf = 1.0;
+  Mc = 0.0;
+  if (id[0] == 0) return;
+  double M = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) M += d[17 + i] * C[i];
+  if (id[0] == 1) { Mf = M; Mc = 1.0; return; }
+  const double Pr = L.K(L.k0, r) * M / k;
+  double F = 1.0;
+  if (id[0] == 3) {
+    const double a = d[12], T3 = d[13], T1 = d[14], T2 = d[15];
+    const double Fc = (1 - a) * exp(-T / T3) + a * exp(-T / T1) + (id[4] ? exp(-T2 / T) : 0.0);
+    const double lFc = log10(fmax(Fc, 1e-300));
+    const double c = -0.4 - 0.67 * lFc, n = 0.75 - 1.27 * lFc;
+    const double lPr = log10(fmax(Pr, 1e-300));
+    const double f1 = (lPr + c) / (n - 0.14 * (lPr + c));
+    F = exp10(lFc / (1 + f1 * f1));
+  }
+  k = k * Pr / (1 + Pr) * F;
+}
+
+__device__ __forceinline__ double ipow(double c, double nu) {
+  return nu == 1.0 ? c : (nu == 2.0 ? c * c : (nu == 3.0 ? c * c * c : pow(c, nu)));
+}
+__device__ __forceinline__ double dipow(double c, double nu) {   // d/dc c^nu
+  return nu == 1.0 ? 1.0 : (nu == 2.0 ? 2.0 * c : (nu == 3.0 ? 3.0 * c * c : nu * pow(c, nu - 1.0)));
+}
+
+// w = dC/dt
+template <int S>
+__device__ void rhs(const ChemMech& m, const Lane<S>& L, double T, const double (&C)[S], double (&w)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) w[i] = 0.0;
+  for (int r = 0; r < m.R; ++r) {
+    const int* id = m.idata + r * 8;
+    const int* ix = m.irs + r * 6;
+    const double* d = m.dd + (long)r * m.ndd;
+    double k, Mf, Mc;
+    rcoef<S>(m, L, r, T, C, k, Mf, Mc);
+    double f = k, b = id[1] ? k * L.K(L.ikc, r) : 0.0;
+    for (int j = 0; j < 3; ++j) {
+      if (ix[j] >= 0) f *= ipow(sel<S>(C, ix[j]), d[3 + j]);
+      if (ix[3 + j] >= 0) b *= ipow(sel<S>(C, ix[3 + j]), d[6 + j]);
+    }
+    const double q = Mf * (f - b);
+    for (int j = 0; j < 3; ++j) {
+      if (ix[j] >= 0) add_at<S>(w, ix[j], -d[3 + j] * q);
+      if (ix[3 + j] >= 0) add_at<S>(w, ix[3 + j], d[6 + j] * q);
+    }
+  }
+}
+
+// A = I - h J  (J = d(dC/dt)/dC, mass-action part + third-body factor)
+template <int S>
+__device__ void build_matrix(const ChemMech& m, const Lane<S>& L, double T, const double (&C)[S], double h) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) L.M(i, j) = (i == j) ? 1.0 : 0.0;
+  for (int r = 0; r < m.R; ++r) {
+    const int* id = m.idata + r * 8;
+    const int* ix = m.irs + r * 6;
+    const double* d = m.dd + (long)r * m.ndd;
+    double k, Mf, Mc;
+    rcoef<S>(m, L, r, T, C, k, Mf, Mc);
+    const double kb = id[1] ? k * L.K(L.ikc, r) : 0.0;
+    double cr[3], cp[3];
+    for (int j = 0; j < 3; ++j) {
+      cr[j] = ix[j] >= 0 ? sel<S>(C, ix[j]) : 1.0;
+      cp[j] = ix[3 + j] >= 0 ? sel<S>(C, ix[3 + j]) : 1.0;
+    }
+    // dq/dC for each participating species (3 reactant slots, 3 product slots)
+    double dq[6];
+    int sp[6];
+    for (int a = 0; a < 3; ++a) {
+      double t = k;
+      for (int j = 0; j < 3; ++j) if (ix[j] >= 0) t *= (j == a) ? dipow(cr[j], d[3 + j]) : ipow(cr[j], d[3 + j]);
+      dq[a] = ix[a] >= 0 ? Mf * t : 0.0;
+      sp[a] = ix[a];
+      double u = kb;
+      for (int j = 0; j < 3; ++j) if (ix[3 + j] >= 0) u *= (j == a) ? dipow(cp[j], d[6 + j]) : ipow(cp[j], d[6 + j]);
+      dq[3 + a] = ix[3 + a] >= 0 ? -Mf * u : 0.0;
+      sp[3 + a] = ix[3 + a];
+    }
+    double q0 = 0.0;
+    if (Mc != 0.0) {
+      double f = k, b = kb;
+      for (int j = 0; j < 3; ++j) {
+        if (ix[j] >= 0) f *= ipow(cr[j], d[3 + j]);
+        if (ix[3 + j] >= 0) b *= ipow(cp[j], d[6 + j]);
+      }
+      q0 = f - b;
+    }
+    // rows touched: reactants (-nu_r) and products (+nu_p)
+    for (int a = 0; a < 6; ++a) {
+      const int row = ix[a];   // reactant slots 0..2, product slots 3..5
+      if (row < 0) continue;
+      const double nu = a < 3 ? -d[3 + a] : d[6 + (a - 3)];
+      for (int bb = 0; bb < 6; ++bb)
+        if (sp[bb] >= 0 && dq[bb] != 0.0) L.M(row, sp[bb]) -= h * nu * dq[bb];
+      if (Mc != 0.0)
+#pragma unroll
+        for (int j = 0; j < S; ++j) L.M(row, j) -= h * nu * d[17 + j] * q0;
+    }
+  }
+}
+
+// in-place LU without pivoting (A = I - hJ is an M-matrix-like perturbation of I); false if singular
+template <int S> __device__ bool lu(const Lane<S>& L) {
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const double p = L.M(k, k);
+    if (!(fabs(p) > 1e-300)) return false;
+    const double ip = 1.0 / p;
+#pragma unroll
+    for (int i = k + 1; i < S; ++i) {
+      const double f = L.M(i, k) * ip;
+      L.M(i, k) = f;
+#pragma unroll
+      for (int j = k + 1; j < S; ++j) L.M(i, j) -= f * L.M(k, j);
+    }
+  }
+  return true;
+}
+template <int S> __device__ void lu_solve(const Lane<S>& L, double (&b)[S]) {
+#pragma unroll
+  for (int i = 1; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) b[i] -= L.M(i, j) * b[j];
+#pragma unroll
+  for (int i = S - 1; i >= 0; --i) {
+#pragma unroll
+    for (int j = i + 1; j < S; ++j) b[i] -= L.M(i, j) * b[j];
+    b[i] = b[i] / L.M(i, i);
+  }
+}
+
+// n_sub linearly-implicit Euler substeps of size h/n_sub from y0 (f0 = rhs(y0) given)
+template <int S>
+__device__ bool lie(const ChemMech& m, const Lane<S>& L, double T, const double (&y0)[S], const double (&f0)[S],
+                    double h, int n_sub, double (&out)[S]) {
+  const double hs = h / n_sub;
+  build_matrix<S>(m, L, T, y0, hs);
+  if (!lu<S>(L)) return false;
+  double y[S], f[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) { y[i] = y0[i]; f[i] = f0[i]; }
+  for (int s = 0; s < n_sub; ++s) {
+    if (s > 0) rhs<S>(m, L, T, y, f);
+    double dlt[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) dlt[i] = hs * f[i];
+    lu_solve<S>(L, dlt);
+#pragma unroll
+    for (int i = 0; i < S; ++i) y[i] += dlt[i];
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = y[i];
+  return true;
+}
+
+template <int S>
+__global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double* __restrict__ Tf,
+                                                const double* __restrict__ rhof, const double* __restrict__ Yf,
+                                                double dt, double rtol, double atol, double Tmin, int max_steps,
+                                                double* __restrict__ RR, double* __restrict__ stats) {
+  extern __shared__ double lds[];
+  Lane<S> L;
+  L.lane = threadIdx.x;
+  L.kf = lds;
+  L.k0 = lds + (long)m.R * LANES;
+  L.ikc = lds + 2L * m.R * LANES;
+  L.A = lds + 3L * m.R * LANES;
+  const long c = (long)blockIdx.x * LANES + threadIdx.x;
+  if (c >= n) return;   // no block-level synchronisation below: early exit is safe
+  const double T = Tf[c], rho = rhof[c];
+  double Y0[S], y[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) { Y0[i] = Yf[(long)i * n + c]; y[i] = rho * Y0[i] / m.W[i]; }
+  int steps = 0, rejects = 0;
+  if (T >= Tmin) {
+    rate_constants<S>(m, L, T);
+    double sc[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) sc[i] = rho / m.W[i];   // Y -> C scale for the tolerances
+    double t = 0.0, h = dt;
+    while (t < dt) {
+      if (steps + rejects >= max_steps) { steps = -1; break; }
+      if (t + h > dt) h = dt - t;
+      double f0[S], r1[S], r2[S], t21[S], t22[S];
+      rhs<S>(m, L, T, y, f0);
+      bool ok = lie<S>(m, L, T, y, f0, h, 1, r1);
+      ok = ok && lie<S>(m, L, T, y, f0, h, 2, t21);
+      double err = 0.0;
+      if (ok) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) t22[i] = 2.0 * t21[i] - r1[i];
+        ok = lie<S>(m, L, T, y, f0, h, 3, r2);
+      }
+      if (ok) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const double t32 = 3.0 * r2[i] - 2.0 * t21[i];
+          const double t33 = t32 + (t32 - t22[i]) * 0.5;
+          const double e = fabs(t33 - t32) / (atol * sc[i] + rtol * fabs(t33));
+          err = fmax(err, e);
+          r2[i] = t33;
+        }
+        if (!(err == err)) ok = false;   // NaN
+      }
+      if (ok && err <= 1.0) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) y[i] = r2[i];
+        t += h;
+        ++steps;
+        const double fac = err > 0.0 ? 0.9 * pow(err, -1.0 / 3.0) : 5.0;
+        h = h * fmin(5.0, fmax(0.2, fac));
+      } else {
+        ++rejects;
+        const double fac = ok ? 0.9 * pow(err, -1.0 / 3.0) : 0.25;
+        h = h * fmin(0.5, fmax(0.1, fac));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double Yn = y[i] * m.W[i] / rho;
+    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho / dt : 0.0;
+  }
+  stats[c] = steps;
+  stats[n + c] = rejects;
+}
+
+}  // namespace
+
+void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd) {
+  Chem& h = x.chem;
+  DFMI_CHECK(x.S > 0 && R > 0 && R <= 256, "chemistry: bad reaction count");
+  h.R = R;
+  h.ndd = 17 + x.S;
+  h.idata.upload(idata, (size_t)R * 8, x.stream);
+  h.irs.upload(irs, (size_t)R * 6, x.stream);
+  h.dd.upload(dd, (size_t)R * h.ndd, x.stream);
+  for (int r = 0; r < R; ++r) {
+    for (int k = 0; k < 6; ++k) DFMI_CHECK(irs[r * 6 + k] < x.S, "chemistry: species index out of range");
+    DFMI_CHECK(idata[r * 8] >= 0 && idata[r * 8] <= 3, "chemistry: unknown reaction type");
+  }
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  h.ready = true;
+}
+
+void chem_solve(Ctx& x, double dt) {
+  Chem& h = x.chem;
+  DFMI_CHECK(h.ready, "chemistry mechanism not set (dfmi_chem_set_mechanism)");
+  DFMI_CHECK(x.thermo.S == x.S, "chemistry needs the thermo coefficients (NASA7, W)");
+  ChemMech m{h.R, h.ndd, h.idata.p, h.irs.p, h.dd.p, x.thermo.dnasa.p, x.thermo.dW.p};
+  const size_t lds = ((size_t)3 * h.R + (size_t)x.S * x.S) * LANES * sizeof(double);
+  DFMI_CHECK(lds <= 160 * 1024, "chemistry: mechanism too large for the LDS layout");
+  double* stats = x.f("chem_stats");
+  const dim3 g((unsigned)blocks_for(x.C, LANES));
+#define CALL(NS)                                                                                                    \
+  do {                                                                                                              \
+    KScope _ks(x, "k_chem");                                                                                        \
+    hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, m, x.f("T"), x.f("rho"), x.f("Y"), dt, \
+                       h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);                                      \
+  } while (0)
+  switch (x.S) {
+    case 4: CALL(4); break; case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break;
+    case 8: CALL(8); break; case 9: CALL(9); break; case 10: CALL(10); break; case 11: CALL(11); break;
+    case 12: CALL(12); break;
+    default: throw Error("chemistry: species count " + std::to_string(x.S) + " not instantiated (4..12)");
+  }
+#undef CALL
+  DFMI_HIP(hipGetLastError());
+}
+
+}  // namespace dfmi

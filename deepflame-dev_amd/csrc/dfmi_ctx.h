@@ -56,7 +56,18 @@ struct Thermo {
   DevBuf<double> dW, dnasa, dvisc, dcond, dbdiff, dvc1, dvc2;
 };
 
-struct Halo;   // RCCL processor-patch exchange (halo.cpp)
+struct Halo;   // RCCL processor-patch exchange (halo.hip)
+
+// per-cell chemistry (chem.hip): mechanism arrays (dfmi/kinetics.py layout) and integrator controls
+struct Chem {
+  bool ready = false;
+  int mode = 0;                 // 0 off, 1 stiff ODE integration, 2 DNN surrogate
+  int R = 0, ndd = 0;
+  DevBuf<int> idata, irs;
+  DevBuf<double> dd;
+  double rtol = 1e-6, atol = 1e-10, Tmin = 0.0;   // CVODE settings of the reference (CanteraTorchProperties)
+  int max_steps = 20000;
+};
 
 // HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)
 struct KernelTimer {
@@ -115,6 +126,7 @@ struct Ctx {
     DevBuf<int> src;             // coefficient: 2f = lower[f], 2f+1 = upper[f], -(b+1) = -boundaryCoeffs[b]
   } ell;
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
+  Chem chem;
   struct SolverWs {
     DevBuf<double> buf, scal, red_local, red_all;
     DevBuf<int> sysmap;
@@ -193,7 +205,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
 SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg);
-// halo.cpp
+// chem.hip
+void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd);
+void chem_solve(Ctx& x, double dt);
+// halo.hip
 // One exchange point: cell values of each item's components are sent across processor faces and land
 // in the receiver's neighbour slots (to_slots) or in the extended vector region [C, C+H) (solver vectors).
 struct HaloItem {

@@ -61,7 +61,9 @@ SIGNATURES = {
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
-    "dfmi_chem_set_mechanism": None,   # optional (declared if present)
+    "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
+    "dfmi_chem_set_options": [_P, C.c_int, C.c_double, C.c_double, C.c_double],
+    "dfmi_chem_solve": [_P, C.c_double],
 }
 
 
@@ -77,7 +79,7 @@ def _declare(lib):
 
 
 def exported_symbols() -> list:
-    return [n for n in SIGNATURES if n != "dfmi_chem_set_mechanism"] + ["dfmi_version"]
+    return list(SIGNATURES) + ["dfmi_version"]
 
 
 class DfmiError(RuntimeError):
@@ -216,6 +218,17 @@ class Context:
 
     def set_preconditioner(self, eqn, name):
         self._call("dfmi_set_preconditioner", self.h, eqn.encode(), name.encode())
+
+    def chem_set_mechanism(self, mech):
+        idata, irs, dd = mech.pack()
+        self._keep_chem = (idata, irs, dd)
+        self._call("dfmi_chem_set_mechanism", self.h, mech.R, _ip(idata), _ip(irs), _dp(dd))
+
+    def chem_set_options(self, mode, rtol=1e-6, atol=1e-10, T_min=0.0):
+        self._call("dfmi_chem_set_options", self.h, int(mode), float(rtol), float(atol), float(T_min))
+
+    def chem_solve(self, dt):
+        self._call("dfmi_chem_solve", self.h, float(dt))
 
     def amg_info(self):
         n = C.c_int(); cells = np.zeros(32, np.int32); w = np.zeros(32, np.int32)
