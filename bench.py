@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--ncorr", type=int, default=2)
     ap.add_argument("--dt", type=float, default=1e-6)
     ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
+    ap.add_argument("--chem", default="ode", choices=["ode", "off"],
+                    help="chemistry source: stiff ODE integration per cell (BASELINE config 3) or off")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -160,6 +162,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = {"uid": uid[0], "nranks": world, "rank": rank}
     case.setup_context(ctx, m, table, inert, args.dt, comm=comm)
+    if args.chem == "ode":
+        from dfmi.kinetics import parse_mechanism
+        ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, yml)))
+        ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)   # reference CVODE tolerances
     f = case.tgv_fields(m, ym["species"])
     case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
     del f
@@ -169,7 +175,7 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    ctx.kernel_timer(args.kernel)
+    ctx.kernel_timer(args.kernel + (",k_chem" if args.chem == "ode" else ""))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.time_step(args.ncorr)
@@ -177,7 +183,8 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    k_ms, k_n = ctx.kernel_time()
+    k_ms, k_n = ctx.kernel_time(args.kernel)
+    chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
     ctx.kernel_timer("")
     el = t1 - t0
     if world > 1:
@@ -217,6 +224,9 @@ def main():
                      "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "amg_levels": ctx.amg_info(),
+        "chemistry": ({"integrator": "linearly-implicit Euler extrapolation (order 3), rtol 1e-6 atol 1e-10",
+                       "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
+                       "k_chem_ms_per_step": chem_ms / max(chem_n, 1)} if args.chem == "ode" else None),
         "finite": finite,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -456,29 +456,47 @@ int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
   });
 }
 
-int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernel) {
+int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernels) {
   return guard([&] {
     Ctx& x = ctx->x;
     DFMI_HIP(hipStreamSynchronize(x.stream));
-    x.ktimer.target = kernel ? kernel : "";
-    x.ktimer.used = 0;
+    KernelTimer& k = x.ktimer;
+    k.targets.clear(); k.rec.clear(); k.used = 0;
+    std::string s(kernels ? kernels : ""), cur;
+    for (char ch : s + ",") {
+      if (ch == ',') { if (!cur.empty()) k.targets.push_back(cur); cur.clear(); }
+      else if (ch != ' ') cur += ch;
+    }
+  });
+}
+
+int dfmi_kernel_time_named(dfmi_ctx* ctx, const char* kernel, double* total_ms, int* launches) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    KernelTimer& k = x.ktimer;
+    int t = -1;
+    for (size_t i = 0; i < k.targets.size(); ++i) if (k.targets[i] == kernel) t = (int)i;
+    DFMI_CHECK(t >= 0, std::string("kernel '") + kernel + "' is not armed");
+    double tot = 0;
+    int n = 0;
+    for (size_t r = 0; r < k.rec.size() && 2 * r + 1 < k.used; ++r) {
+      if (k.rec[r] != t) continue;
+      float ms = 0;
+      DFMI_HIP(hipEventElapsedTime(&ms, k.pool[2 * r], k.pool[2 * r + 1]));
+      tot += ms;
+      ++n;
+    }
+    *total_ms = tot;
+    *launches = n;
   });
 }
 
 int dfmi_kernel_time(dfmi_ctx* ctx, double* total_ms, int* launches) {
   return guard([&] {
-    Ctx& x = ctx->x;
-    DFMI_HIP(hipStreamSynchronize(x.stream));
-    double tot = 0;
-    KernelTimer& k = x.ktimer;
-    for (size_t i = 0; i + 1 < k.used; i += 2) {
-      float ms = 0;
-      DFMI_HIP(hipEventElapsedTime(&ms, k.pool[i], k.pool[i + 1]));
-      tot += ms;
-    }
-    *total_ms = tot;
-    *launches = (int)(k.used / 2);
-    k.used = 0;
+    DFMI_CHECK(!ctx->x.ktimer.targets.empty(), "no kernel armed");
+    const std::string first = ctx->x.ktimer.targets[0];
+    if (dfmi_kernel_time_named(ctx, first.c_str(), total_ms, launches)) throw Error(g_err);
   });
 }
 

@@ -71,8 +71,9 @@ struct Chem {
 
 // HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)
 struct KernelTimer {
-  std::string target;
-  std::vector<hipEvent_t> pool;   // pairs (start, end)
+  std::vector<std::string> targets;   // armed kernel names
+  std::vector<hipEvent_t> pool;       // pairs (start, end)
+  std::vector<int> rec;               // target index of each recorded pair
   size_t used = 0;
   ~KernelTimer() { for (auto e : pool) (void)hipEventDestroy(e); }
   hipEvent_t next() {
@@ -165,16 +166,19 @@ struct Ctx {
 // Records a start/end event pair around a launch when `name` is the armed kernel.
 struct KScope {
   Ctx& x;
-  bool on;
-  static bool match(const std::string& t, const char* name) {   // template arguments ignored
+  int idx;
+  static int match(const std::vector<std::string>& ts, const char* name) {   // template arguments ignored
+    if (ts.empty()) return -1;
     size_t n = 0;
     while (name[n] && name[n] != '<') ++n;
-    return !t.empty() && t.size() == n && t.compare(0, n, name, n) == 0;
+    for (size_t i = 0; i < ts.size(); ++i)
+      if (ts[i].size() == n && ts[i].compare(0, n, name, n) == 0) return (int)i;
+    return -1;
   }
-  KScope(Ctx& c, const char* name) : x(c), on(match(c.ktimer.target, name)) {
-    if (on) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream));
+  KScope(Ctx& c, const char* name) : x(c), idx(match(c.ktimer.targets, name)) {
+    if (idx >= 0) { x.ktimer.rec.push_back(idx); DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream)); }
   }
-  ~KScope() noexcept(false) { if (on) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream)); }
+  ~KScope() noexcept(false) { if (idx >= 0) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream)); }
 };
 
 // ---- launchers (fv_kernels.hip)

@@ -61,6 +61,7 @@ SIGNATURES = {
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
+    "dfmi_kernel_time_named": [_P, C.c_char_p, _DP, _IP],
     "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
     "dfmi_chem_set_options": [_P, C.c_int, C.c_double, C.c_double, C.c_double],
     "dfmi_chem_solve": [_P, C.c_double],
@@ -247,10 +248,13 @@ class Context:
         """Arm HIP-event timing of every launch of `kernel` on this context's stream."""
         self._call("dfmi_kernel_timer", self.h, kernel.encode())
 
-    def kernel_time(self):
-        """(total_ms, launches) of the armed kernel since the last call."""
+    def kernel_time(self, name=None):
+        """(total_ms, launches) of an armed kernel since arming (default: the first armed)."""
         ms = C.c_double(); n = C.c_int()
-        self._call("dfmi_kernel_time", self.h, C.byref(ms), C.byref(n))
+        if name is None:
+            self._call("dfmi_kernel_time", self.h, C.byref(ms), C.byref(n))
+        else:
+            self._call("dfmi_kernel_time_named", self.h, name.encode(), C.byref(ms), C.byref(n))
         return ms.value, n.value
 
     def sync(self):

@@ -147,10 +147,11 @@ int dfmi_chem_solve(dfmi_ctx* ctx, double dt);
 /* ---- kernel timing (the reference's TICK_START_EVENT / TICK_END_EVENT cudaEvent pairs,
  * src_gpu/dfMatrixOpBase.H:46-60): arm HIP-event timing of every launch of one kernel
  * (name as in the source, e.g. "k_y_assemble"; "" disarms), recorded on the context stream */
-int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernel);
-/* synchronise and return the summed duration and count of the armed kernel's launches since
- * the last call (then reset) */
+int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernels);   /* comma-separated names; re-arming resets */
+/* synchronise and return the summed duration and count of the first armed kernel's launches */
 int dfmi_kernel_time(dfmi_ctx* ctx, double* total_ms, int* launches);
+/* the same for one named armed kernel */
+int dfmi_kernel_time_named(dfmi_ctx* ctx, const char* kernel, double* total_ms, int* launches);
 
 #ifdef __cplusplus
 }
