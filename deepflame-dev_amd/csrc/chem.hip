@@ -7,10 +7,10 @@
 // Cantera GasKinetics: Arrhenius rates, three-body efficiencies, Lindemann/Troe fall-off, reverse
 // rates from NASA7 equilibrium constants.
 //
-// Integrator: linearly-implicit Euler extrapolation (Deuflhard's SEULEX idea) with step sequence
-// 1, 2, 3 -> order 3, embedded error estimate T33 - T32, adaptive step size, analytic Jacobian of
-// the mass-action terms (fall-off [M]-dependence of k omitted: a W-method approximation the step
-// control absorbs). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
+// Integrator: ROS3 Rosenbrock (L-stable, order 3, embedded order-2 error estimate, one Jacobian and
+// one LU per step) with adaptive step size; alternative (DFMI_CHEM_METHOD=extrap): linearly-implicit
+// Euler extrapolation with step sequence 1, 2, 3. Analytic Jacobian of the mass-action terms (the
+// fall-off [M]-dependence of k is omitted, an approximation the step control absorbs). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
 // mass fractions) by default.
 //
 // Layout: one cell per lane, 64-lane workgroups. Per-lane rate constants (they depend only on T,
@@ -19,6 +19,7 @@
 // wave-uniform (scalar loads).
 #include "dfmi_ctx.h"
 #include <cmath>
+#include <cstdlib>
 
 namespace dfmi {
 namespace {
@@ -263,11 +264,48 @@ __device__ bool lie(const ChemMech& m, const Lane<S>& L, double T, const double 
   return true;
 }
 
+// One ROS3 step (Sandu et al. 1997, L-stable, order 3 with embedded order 2; the coefficients
+// of KPP's Rosenbrock ROS-3): (I - h g J) K_i = h g [f(y + sum a_ij K_j) + sum (c_ij / h) K_j];
+// y_new = y + sum m_i K_i, error = sum e_i K_i. One Jacobian and one LU per step; stage 3 reuses
+// f of stage 2 (a31 = a21 = 1, a32 = 0).
+template <int S>
+__device__ bool ros3(const ChemMech& m, const Lane<S>& L, double T, const double (&y)[S], const double (&f0)[S],
+                     double h, double (&ynew)[S], double (&err)[S]) {
+  constexpr double g = 0.43586652150845899941601945119356;
+  constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
+                   c32 = 0.92076794298330791242156818474003e1;
+  constexpr double m1 = 1.0, m2 = 0.61697947043828245592553615689730e1, m3 = -0.42772256543218573326238373806514;
+  constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
+  const double hg = h * g;
+  build_matrix<S>(m, L, T, y, hg);
+  if (!lu<S>(L)) return false;
+  double k1[S], k2[S], k3[S], y2[S], f2[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) k1[i] = hg * f0[i];
+  lu_solve<S>(L, k1);
+#pragma unroll
+  for (int i = 0; i < S; ++i) y2[i] = y[i] + k1[i];
+  rhs<S>(m, L, T, y2, f2);
+  const double rh = 1.0 / h;
+#pragma unroll
+  for (int i = 0; i < S; ++i) k2[i] = hg * (f2[i] + c21 * rh * k1[i]);
+  lu_solve<S>(L, k2);
+#pragma unroll
+  for (int i = 0; i < S; ++i) k3[i] = hg * (f2[i] + rh * (c31 * k1[i] + c32 * k2[i]));
+  lu_solve<S>(L, k3);
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    ynew[i] = y[i] + m1 * k1[i] + m2 * k2[i] + m3 * k3[i];
+    err[i] = e1 * k1[i] + e2 * k2[i] + e3 * k3[i];
+  }
+  return true;
+}
+
 template <int S>
 __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double* __restrict__ Tf,
                                                 const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                 double dt, double rtol, double atol, double Tmin, int max_steps,
-                                                double* __restrict__ RR, double* __restrict__ stats) {
+                                                int method, double* __restrict__ RR, double* __restrict__ stats) {
   extern __shared__ double lds[];
   Lane<S> L;
   L.lane = threadIdx.x;
@@ -293,24 +331,34 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double
       if (t + h > dt) h = dt - t;
       double f0[S], r1[S], r2[S], t21[S], t22[S];
       rhs<S>(m, L, T, y, f0);
-      bool ok = lie<S>(m, L, T, y, f0, h, 1, r1);
-      ok = ok && lie<S>(m, L, T, y, f0, h, 2, t21);
+      bool ok;
       double err = 0.0;
-      if (ok) {
+      if (method == 0) {   // ROS3
+        ok = ros3<S>(m, L, T, y, f0, h, r2, r1);
+        if (ok) {
 #pragma unroll
-        for (int i = 0; i < S; ++i) t22[i] = 2.0 * t21[i] - r1[i];
-        ok = lie<S>(m, L, T, y, f0, h, 3, r2);
-      }
-      if (ok) {
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          const double t32 = 3.0 * r2[i] - 2.0 * t21[i];
-          const double t33 = t32 + (t32 - t22[i]) * 0.5;
-          const double e = fabs(t33 - t32) / (atol * sc[i] + rtol * fabs(t33));
-          err = fmax(err, e);
-          r2[i] = t33;
+          for (int i = 0; i < S; ++i) err = fmax(err, fabs(r1[i]) / (atol * sc[i] + rtol * fmax(fabs(y[i]), fabs(r2[i]))));
+          if (!(err == err)) ok = false;
         }
-        if (!(err == err)) ok = false;   // NaN
+      } else {             // linearly-implicit Euler extrapolation, sequence 1, 2, 3
+        ok = lie<S>(m, L, T, y, f0, h, 1, r1);
+        ok = ok && lie<S>(m, L, T, y, f0, h, 2, t21);
+        if (ok) {
+#pragma unroll
+          for (int i = 0; i < S; ++i) t22[i] = 2.0 * t21[i] - r1[i];
+          ok = lie<S>(m, L, T, y, f0, h, 3, r2);
+        }
+        if (ok) {
+#pragma unroll
+          for (int i = 0; i < S; ++i) {
+            const double t32 = 3.0 * r2[i] - 2.0 * t21[i];
+            const double t33 = t32 + (t32 - t22[i]) * 0.5;
+            const double e = fabs(t33 - t32) / (atol * sc[i] + rtol * fabs(t33));
+            err = fmax(err, e);
+            r2[i] = t33;
+          }
+          if (!(err == err)) ok = false;   // NaN
+        }
       }
       if (ok && err <= 1.0) {
 #pragma unroll
@@ -361,12 +409,13 @@ void chem_solve(Ctx& x, double dt) {
   const size_t lds = ((size_t)3 * h.R + (size_t)x.S * x.S) * LANES * sizeof(double);
   DFMI_CHECK(lds <= 160 * 1024, "chemistry: mechanism too large for the LDS layout");
   double* stats = x.f("chem_stats");
+  if (const char* e = std::getenv("DFMI_CHEM_METHOD")) h.method = std::string(e) == "extrap" ? 1 : 0;
   const dim3 g((unsigned)blocks_for(x.C, LANES));
 #define CALL(NS)                                                                                                    \
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \
     hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, m, x.f("T"), x.f("rho"), x.f("Y"), dt, \
-                       h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);                                      \
+                       h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats);                            \
   } while (0)
   switch (x.S) {
     case 4: CALL(4); break; case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break;

@@ -67,6 +67,7 @@ struct Chem {
   DevBuf<double> dd;
   double rtol = 1e-6, atol = 1e-10, Tmin = 0.0;   // CVODE settings of the reference (CanteraTorchProperties)
   int max_steps = 20000;
+  int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
 };
 
 // HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)

@@ -45,10 +45,12 @@ def _states(ym, n, seed=0):
     return T, rho, Y
 
 
+@pytest.mark.parametrize("method", ["ros3", "extrap"])
 @pytest.mark.parametrize("mech", [("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
                                   ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt")])
-def test_chem_rr_matches_oracle(mech):
+def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     from chem_oracle import Kinetics
+    monkeypatch.setenv("DFMI_CHEM_METHOD", method)
     ctx, m, ym, mc = _setup(*mech)
     C = m.n_cells
     T, rho, Y = _states(ym, C)
