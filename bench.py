@@ -224,7 +224,7 @@ def main():
                      "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "amg_levels": ctx.amg_info(),
-        "chemistry": ({"integrator": "linearly-implicit Euler extrapolation (order 3), rtol 1e-6 atol 1e-10",
+        "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
                        "k_chem_ms_per_step": chem_ms / max(chem_n, 1)} if args.chem == "ode" else None),
         "finite": finite,
