@@ -66,7 +66,7 @@ struct Chem {
   DevBuf<int> idata, irs;
   DevBuf<double> dd;
   double rtol = 1e-6, atol = 1e-10, Tmin = 0.0;   // CVODE settings of the reference (CanteraTorchProperties)
-  int max_steps = 20000;
+  int max_steps = 100000;
   int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
 };
 

@@ -1,7 +1,7 @@
 """GPU stiff-chemistry integrator (A10) vs the CPU oracle (SciPy BDF, tight tolerances).
 
 RR = (Y(dt) - Y) rho / dt is a difference of nearly equal numbers, so integrator tolerances show up
-amplified: with tight GPU tolerances (rtol 1e-10) RR agrees to 1e-6 of its per-species scale; with
+amplified: with tight GPU tolerances (rtol 1e-8) RR agrees to 1e-5 of its per-species scale; with
 the reference's CVODE tolerances (rtol 1e-6, atol 1e-10) to 2e-3."""
 import os
 
@@ -61,12 +61,13 @@ def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     ref = kin.reaction_rates(T[idx], None, rho[idx], Y[:, idx], dt)
     # per-species scale, floored for species that do not react (N2: rounding-level RR)
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
-    ctx.chem_set_options(1, rtol=1e-10, atol=1e-16)
+    ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
     ctx.chem_solve(dt)
+    assert ctx.get_field("chem_stats", (2, C))[0].min() >= 1      # no cell hit the step limit
     rr = ctx.get_field("RR", (mc.S, C))[:, idx]
     assert np.all(np.isfinite(rr))
-    assert np.abs(rr - ref).max(axis=None, initial=0) / scale.max() < 1e-6
-    assert (np.abs(rr - ref) / scale).max() < 1e-5
+    assert np.abs(rr - ref).max(axis=None, initial=0) / scale.max() < 1e-5
+    assert (np.abs(rr - ref) / scale).max() < 1e-4
     # mass conservation: sum_i RR_i = 0
     assert np.abs(rr.sum(axis=0)).max() < 1e-9 * np.abs(rr).max()
     ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
