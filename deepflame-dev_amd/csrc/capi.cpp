@@ -168,6 +168,7 @@ void do_U(Ctx& x) {
 void do_Y(Ctx& x) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
   if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt);   // chemistry->solve(deltaT) before YEqn (YEqn.H)
+  else if (x.chem.mode == 2) dnn_solve(x);              // chemistrySolver_GPU.Inference (YEqn_GPU.H)
   y_prep(x);
   y_assemble(x);
   Matrix& A = x.mY;
@@ -565,6 +566,25 @@ int dfmi_chem_set_options(dfmi_ctx* ctx, int mode, double rtol, double atol, dou
     DFMI_CHECK(rtol > 0 && atol > 0, "chemistry tolerances must be positive");
     Chem& c = ctx->x.chem;
     c.mode = mode; c.rtol = rtol; c.atol = atol; c.Tmin = T_min;
+  });
+}
+
+int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* dims, const float* params,
+                       const double* x_mu, const double* x_std, const double* y_mu, const double* y_std,
+                       double T_react, double dt_infer) {
+  return guard([&] {
+    DFMI_CHECK(ctx->x.have_sizes && ctx->x.inert >= 0, "set sizes and the inert index first");
+    dnn_upload(ctx->x, n_modules, n_layers, dims, params, x_mu, x_std, y_mu, y_std, T_react, dt_infer);
+  });
+}
+
+int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    dnn_solve(x);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    if (n_reacting) *n_reacting = x.dnn.last_reacting;
   });
 }
 

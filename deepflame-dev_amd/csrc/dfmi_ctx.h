@@ -58,6 +58,21 @@ struct Thermo {
 
 struct Halo;   // RCCL processor-patch exchange (halo.hip)
 
+// DF-ODENet surrogate (dnn.hip): S-1 MLPs, fp16 weights per layer [module][out][Kpad], fp32 biases
+struct Dnn {
+  bool ready = false;
+  int nmod = 0;
+  std::vector<int> dims, Kp;
+  std::vector<DevBuf<_Float16>> W;
+  std::vector<DevBuf<float>> b;
+  DevBuf<double> xmu, xstd, ymu, ystd;
+  double T_react = 610.0, dt = 1e-6;      // unReactT_ (dfChemistrySolver.cu:90), RR divisor (:191)
+  int chunk = 65536;                      // reacting cells per inference batch
+  int last_reacting = 0;
+  DevBuf<int> bc, idx;
+  DevBuf<_Float16> x0, h0, h1;
+};
+
 // per-cell chemistry (chem.hip): mechanism arrays (dfmi/kinetics.py layout) and integrator controls
 struct Chem {
   bool ready = false;
@@ -129,6 +144,7 @@ struct Ctx {
   } ell;
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
   Chem chem;
+  Dnn dnn;
   struct SolverWs {
     DevBuf<double> buf, scal, red_local, red_all;
     DevBuf<int> sysmap;
@@ -210,6 +226,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
 SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg);
+// dnn.hip
+void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* params, const double* xmu,
+                const double* xstd, const double* ymu, const double* ystd, double T_react, double dt_infer);
+void dnn_solve(Ctx& x);
 // chem.hip
 void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd);
 void chem_solve(Ctx& x, double dt);

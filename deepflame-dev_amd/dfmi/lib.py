@@ -65,6 +65,9 @@ SIGNATURES = {
     "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
     "dfmi_chem_set_options": [_P, C.c_int, C.c_double, C.c_double, C.c_double],
     "dfmi_chem_solve": [_P, C.c_double],
+    "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
+                           C.c_double],
+    "dfmi_dnn_infer": [_P, _IP],
 }
 
 
@@ -230,6 +233,21 @@ class Context:
 
     def chem_solve(self, dt):
         self._call("dfmi_chem_solve", self.h, float(dt))
+
+    def dnn_set_model(self, dims, params, x_mu, x_std, y_mu, y_std, T_react=610.0, dt_infer=1e-6):
+        """params: list over modules of [(W [out,in], b [out]) per layer] (numpy float32)."""
+        d = _i32(dims)
+        flat = np.concatenate([np.concatenate([np.ravel(W), np.ravel(b)]) for mod in params for (W, b) in mod])
+        flat = np.ascontiguousarray(flat, dtype=np.float32)
+        self._keep_dnn = flat
+        arr = [_f64(a) for a in (x_mu, x_std, y_mu, y_std)]
+        self._call("dfmi_dnn_set_model", self.h, len(params), len(dims) - 1, _ip(d),
+                   flat.ctypes.data_as(C.POINTER(C.c_float)), *[_dp(a) for a in arr], float(T_react), float(dt_infer))
+
+    def dnn_infer(self):
+        n = C.c_int()
+        self._call("dfmi_dnn_infer", self.h, C.byref(n))
+        return n.value
 
     def amg_info(self):
         n = C.c_int(); cells = np.zeros(32, np.int32); w = np.zeros(32, np.int32)

@@ -144,6 +144,20 @@ int dfmi_chem_set_options(dfmi_ctx* ctx, int mode, double rtol, double atol, dou
  * "chem_stats" [2][C] = accepted / rejected steps (-1: step limit hit) */
 int dfmi_chem_solve(dfmi_ctx* ctx, double dt);
 
+/* ---- DF-ODENet surrogate (dfChemistrySolver::setConstantValue/Inference,
+ * dfChemistrySolver.cu:78-206; model test/Tu500K-Phi1/inference.py:12-25) ---------------------- */
+/* n_modules = S - 1 nets (species 0..S-2; the inert species must be last), each n_layers Linear
+ * layers dims[0] = S+2 -> ... -> dims[n_layers] = 1 with GELU between; params (fp32) per module, per
+ * layer: weight [out][in] (torch Linear layout) then bias [out]. Normalisation Xmu/Xstd [S+2],
+ * Ymu/Ystd [S-1] (the reference hard-codes the H2 values, :95-105). Cells with T >= T_react
+ * (reference 610 K) react; RR = (y_new - Y) rho (p/101325) / dt_infer (reference 1e-6). Inference
+ * runs in fp16 (MFMA) with fp32 accumulation, as the reference's .to(kHalf) modules. */
+int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* dims, const float* params,
+                       const double* x_mu, const double* x_std, const double* y_mu, const double* y_std,
+                       double T_react, double dt_infer);
+/* run the surrogate on the current T, p, rho, Y -> field "RR" (0 for non-reacting cells) */
+int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting);
+
 /* ---- kernel timing (the reference's TICK_START_EVENT / TICK_END_EVENT cudaEvent pairs,
  * src_gpu/dfMatrixOpBase.H:46-60): arm HIP-event timing of every launch of one kernel
  * (name as in the source, e.g. "k_y_assemble"; "" disarms), recorded on the context stream */

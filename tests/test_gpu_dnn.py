@@ -1,0 +1,101 @@
+"""DF-ODENet surrogate (A9) on MI355X vs a plain PyTorch fp32 restatement of the reference's
+inference (dfChemistrySolver.cu:4-75 pre/post-processing; inference.py:12-25 NN_MLP).
+The model weights of the reference are not in the repository: nets are seeded
+N(0, 1/fan_in). Inference runs in fp16 with fp32 accumulation, like the reference's .to(kHalf)
+modules, so RR is compared at 2e-2 of each species' scale (fp16 has an 11-bit mantissa)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+# normalisation constants the reference hard-codes for its H2 9-species nets (dfChemistrySolver.cu:95-105)
+XMU = [1.2996375154e+03, 1.4349643303e+05, -4.3678815323e+00, -5.8949183472e+00, -3.8840763486e+00,
+       -5.5436246211e+00, -6.0178199636e+00, -2.1469850084e+00, -6.9828365432e+00, -7.7747568654e+00,
+       -1.8571483828e-01]
+XSTD = [3.9612732767e+02, 1.8822821412e+04, 1.1226048640e+00, 6.8397462420e-01, 1.8879462146e+00,
+        1.2433158499e+00, 1.3169176600e+00, 4.3600457243e-01, 8.1820904505e-01, 8.0471805333e-01,
+        6.1020187522e-02]
+YMU = [-0.0101101322, -0.0138129078, -0.0146349442, -0.0088870325, -0.0075195178, 0.0020506931, -0.0103104668,
+       -0.0192603020]
+YSTD = [0.0297933161, 0.0802139099, 0.0230954310, 0.1541940427, 0.1316836678, 0.0042975580, 0.1476416977,
+        0.0860471308]
+DIMS = [11, 1600, 800, 400, 1]
+
+
+def _weights(seed=0):
+    rng = np.random.default_rng(seed)
+    mods = []
+    for m in range(8):
+        layers = []
+        for l in range(4):
+            fin, fout = DIMS[l], DIMS[l + 1]
+            W = (rng.standard_normal((fout, fin)) / np.sqrt(fin)).astype(np.float32)
+            b = (0.1 * rng.standard_normal(fout)).astype(np.float32)
+            layers.append((W, b))
+        mods.append(layers)
+    return mods
+
+
+def _torch_reference(mods, T, p, rho, Y, dt=1e-6, Tr=610.0):
+    import torch
+    S, C = Y.shape
+    RR = np.zeros((S, C))
+    react = T >= Tr
+    Yr = Y[:, react]
+    bct = (Yr ** 0.1 - 1) * 10
+    x = np.concatenate([T[react][None, :], np.full((1, react.sum()), 101325.0), bct], axis=0).T
+    x = (x - np.array(XMU)) / np.array(XSTD)
+    xt = torch.tensor(x, dtype=torch.float32)
+    yn = np.zeros((S - 1, react.sum()))
+    for m, layers in enumerate(mods):
+        h = xt
+        for l, (W, b) in enumerate(layers):
+            h = h @ torch.tensor(W).T + torch.tensor(b)
+            if l < len(layers) - 1:
+                h = torch.nn.functional.gelu(h)
+        out = h[:, 0].double().numpy()
+        yn[m] = ((out * YSTD[m] + YMU[m] + bct[m]) * 0.1 + 1) ** 10
+    tot = yn.sum(axis=0) + Yr[S - 1]
+    yn = yn / tot
+    RR[:S - 1, react] = (yn - Yr[:S - 1]) * rho[react] * (p[react] / 101325.0) / dt
+    return RR
+
+
+def test_dnn_matches_torch_fp32():
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, "Burke2012_s9r23.yaml"))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    m = hex_box(16, 16, 8)
+    ctx = Context(0)
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6)
+    mods = _weights()
+    ctx.dnn_set_model(DIMS, mods, XMU, XSTD, YMU, YSTD)
+    rng = np.random.default_rng(1)
+    C = m.n_cells
+    yu, yb = case.h2_air_compositions(ym["species"])
+    prog = rng.random(C)
+    Y = (1 - prog) * yu[:, None] + prog * yb[:, None] + 1e-4 * rng.random((9, C))
+    Y /= Y.sum(axis=0)
+    T = 300.0 + 2200.0 * rng.random(C)
+    p = 101325.0 * (1 + 0.05 * rng.standard_normal(C))
+    Wm = 1.0 / (Y / t.W[:, None]).sum(axis=0)
+    rho = p * Wm / (8314.46261815324 * T)
+    for n, v in (("T", T), ("p", p), ("rho", rho), ("Y", Y)):
+        ctx.set_field(n, v)
+    nr = ctx.dnn_infer()
+    assert nr == int((T >= 610.0).sum())
+    RR = ctx.get_field("RR", (9, C))
+    ref = _torch_reference(mods, T, p, rho, Y)
+    assert np.all(RR[:, T < 610.0] == 0.0)
+    scale = np.abs(ref).max(axis=1, keepdims=True)[:8]
+    err = np.abs(RR[:8] - ref[:8]) / scale
+    assert np.all(np.isfinite(RR))
+    assert np.median(err) < 2e-3, np.median(err)
+    assert err.max() < 2e-2, err.max()
