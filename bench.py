@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--ncorr", type=int, default=2)
     ap.add_argument("--dt", type=float, default=1e-6)
     ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
-    ap.add_argument("--chem", default="ode", choices=["ode", "off"],
-                    help="chemistry source: stiff ODE integration per cell (BASELINE config 3) or off")
+    ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
+                    help="chemistry source: stiff ODE integration per cell (BASELINE config 3), the DF-ODENet "
+                         "surrogate (MFMA fp16, config 4's path on the H2 nets) or off")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -166,6 +167,10 @@ def main():
         from dfmi.kinetics import parse_mechanism
         ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, yml)))
         ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)   # reference CVODE tolerances
+    elif args.chem == "dnn":
+        from dfmi import dnn_model
+        dnn_model.configure(ctx)
+        ctx.chem_set_options(2)
     f = case.tgv_fields(m, ym["species"])
     case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
     del f
@@ -175,7 +180,10 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    ctx.kernel_timer(args.kernel + (",k_chem" if args.chem == "ode" else ""))
+    extra = {"ode": ",k_chem", "dnn": ",k_mlp_gemm", "off": ""}[args.chem]
+    ctx.kernel_timer(args.kernel + extra)
+    if args.chem == "dnn":
+        ctx.dnn_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.time_step(args.ncorr)
@@ -185,6 +193,8 @@ def main():
         dist.barrier()
     k_ms, k_n = ctx.kernel_time(args.kernel)
     chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
+    gemm_ms, gemm_n = ctx.kernel_time("k_mlp_gemm") if args.chem == "dnn" else (0.0, 0)
+    n_react, gemm_flops = ctx.dnn_stats() if args.chem == "dnn" else (0, 0.0)
     ctx.kernel_timer("")
     el = t1 - t0
     if world > 1:
@@ -227,6 +237,12 @@ def main():
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
                        "k_chem_ms_per_step": chem_ms / max(chem_n, 1)} if args.chem == "ode" else None),
+        "dnn": ({"reacting_cells": n_react, "gemm_launches": gemm_n, "gemm_ms_total": gemm_ms,
+                 "mfma_roofline": {"bound": "mfma", "achieved": gemm_flops / (gemm_ms / 1e3) / 1e12,
+                                   "peak": 2500.0, "unit": "TFLOP/s",
+                                   "frac": gemm_flops / (gemm_ms / 1e3) / 1e12 / 2500.0},
+                 "inferences_per_s_gemm_time": n_react * args.steps / (gemm_ms / 1e3)}
+                if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

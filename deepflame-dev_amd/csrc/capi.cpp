@@ -588,6 +588,15 @@ int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting) {
   });
 }
 
+int dfmi_dnn_stats(dfmi_ctx* ctx, int* n_reacting, double* gemm_flops) {
+  return guard([&] {
+    Dnn& d = ctx->x.dnn;
+    if (n_reacting) *n_reacting = d.last_reacting;
+    if (gemm_flops) *gemm_flops = d.gemm_flops;
+    d.gemm_flops = 0;
+  });
+}
+
 int dfmi_chem_solve(dfmi_ctx* ctx, double dt) {
   return guard([&] {
     Ctx& x = ctx->x;

@@ -69,6 +69,7 @@ struct Dnn {
   double T_react = 610.0, dt = 1e-6;      // unReactT_ (dfChemistrySolver.cu:90), RR divisor (:191)
   int chunk = 65536;                      // reacting cells per inference batch
   int last_reacting = 0;
+  double gemm_flops = 0;                  // algorithmic GEMM flops issued since the last query
   DevBuf<int> bc, idx;
   DevBuf<_Float16> x0, h0, h1;
 };

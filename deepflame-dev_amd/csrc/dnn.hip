@@ -284,6 +284,7 @@ void dnn_solve(Ctx& x) {
     for (int l = 0; l + 1 < L; ++l) {
       const int N = d.dims[l + 1], K = d.Kp[l];
       _Float16* out = bufs[l & 1];
+      d.gemm_flops += 2.0 * n * N * d.dims[l] * d.nmod;
       const dim3 g(blocks_for(N, BN), blocks_for(n, BM), d.nmod);
       KScope _ks(x, "k_mlp_gemm");
       hipLaunchKernelGGL(k_mlp_gemm<true>, g, dim3(GT), 0, x.stream, n, N, K, in, sIn, d.W[l].p, (long)N * K,

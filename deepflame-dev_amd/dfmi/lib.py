@@ -68,6 +68,7 @@ SIGNATURES = {
     "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
                            C.c_double],
     "dfmi_dnn_infer": [_P, _IP],
+    "dfmi_dnn_stats": [_P, _IP, _DP],
 }
 
 
@@ -248,6 +249,11 @@ class Context:
         n = C.c_int()
         self._call("dfmi_dnn_infer", self.h, C.byref(n))
         return n.value
+
+    def dnn_stats(self):
+        n = C.c_int(); f = C.c_double()
+        self._call("dfmi_dnn_stats", self.h, C.byref(n), C.byref(f))
+        return n.value, f.value
 
     def amg_info(self):
         n = C.c_int(); cells = np.zeros(32, np.int32); w = np.zeros(32, np.int32)

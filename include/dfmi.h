@@ -157,6 +157,8 @@ int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* di
                        double T_react, double dt_infer);
 /* run the surrogate on the current T, p, rho, Y -> field "RR" (0 for non-reacting cells) */
 int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting);
+/* reacting cells of the last inference; algorithmic hidden-layer GEMM flops since the last call */
+int dfmi_dnn_stats(dfmi_ctx* ctx, int* n_reacting, double* gemm_flops);
 
 /* ---- kernel timing (the reference's TICK_START_EVENT / TICK_END_EVENT cudaEvent pairs,
  * src_gpu/dfMatrixOpBase.H:46-60): arm HIP-event timing of every launch of one kernel
