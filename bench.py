@@ -74,7 +74,11 @@ def parse():
 
 
 def cpu_baseline(args, table, ym, inert):
-    """The oracle (TEST INFRASTRUCTURE, the checker) timed on a bounded sample on the host."""
+    """The oracle (TEST INFRASTRUCTURE, the checker) timed on a bounded sample on the host, 1 core:
+    the flow part on a cpu_n^3 box (sequential C++ restatement + exact sparse solves), plus -- when the
+    GPU step integrates chemistry -- the oracle's per-cell chemistry (SciPy BDF, the reference's
+    CVODE tolerances) timed on cells sampled from the same initial state; cell-updates/s =
+    1 / (flow seconds per cell + chemistry seconds per cell)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -94,9 +98,24 @@ def cpu_baseline(args, table, ym, inert):
         if time.perf_counter() - t0 > 10.0 or steps >= 5:
             break
     el = time.perf_counter() - t0
-    return {"value": m.n_cells * steps / el, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/df_oracle.cpp (sequential C++ restatement) + scipy spsolve, {n}^3 = {m.n_cells} "
-                      f"cells periodic TGV, {table.S} species, {steps} outer iterations in {el:.1f} s"}
+    flow_s_per_cell = el / (m.n_cells * steps)
+    sample = (f"flow: oracle/df_oracle.cpp (sequential C++ restatement) + scipy spsolve, {n}^3 = {m.n_cells} cells "
+              f"periodic TGV, {table.S} species, {steps} outer iterations in {el:.1f} s")
+    chem_s_per_cell = 0.0
+    if args.chem == "ode":
+        from chem_oracle import Kinetics
+        from dfmi.kinetics import parse_mechanism
+        yml = MECHS[args.mech][0]
+        kin = Kinetics(parse_mechanism(os.path.join(ROOT, "tests", "golden", yml)), ym["nasa"], ym["W"])
+        rng = np.random.default_rng(0)
+        idx = rng.choice(m.n_cells, 24, replace=False)
+        t1 = time.perf_counter()
+        kin.reaction_rates(st["T"][idx], None, st["rho"][idx], st["Y"][:, idx], args.dt, rtol=1e-6, atol=1e-10)
+        chem_s_per_cell = (time.perf_counter() - t1) / idx.size
+        sample += (f"; chemistry: oracle/chem_oracle.py SciPy BDF (rtol 1e-6, atol 1e-10) on {idx.size} sampled cells, "
+                   f"{chem_s_per_cell * 1e3:.2f} ms/cell")
+    return {"value": 1.0 / (flow_s_per_cell + chem_s_per_cell), "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": sample}
 
 
 def host_state(m, table, f):
