@@ -597,6 +597,10 @@ int dfmi_dnn_stats(dfmi_ctx* ctx, int* n_reacting, double* gemm_flops) {
   });
 }
 
+int dfmi_chem_info(dfmi_ctx* ctx, int* generated) {
+  return guard([&] { *generated = ctx->x.chem.generated; });
+}
+
 int dfmi_chem_solve(dfmi_ctx* ctx, double dt) {
   return guard([&] {
     Ctx& x = ctx->x;

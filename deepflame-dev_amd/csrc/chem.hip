@@ -383,6 +383,101 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double
   stats[n + c] = rejects;
 }
 
+// ---- generated fast path: the mechanism compiled in (dfmi/chem_codegen.py), state in registers
+#include "chem_gen_burke9.inc"
+#include "chem_gen_es80.inc"
+
+template <class G>
+__global__ void __launch_bounds__(LANES) k_chem_gen(long n, const double* __restrict__ Tf,
+                                                    const double* __restrict__ rhof, const double* __restrict__ Yf,
+                                                    double dt, double rtol, double atol, double Tmin, int max_steps,
+                                                    double* __restrict__ RR, double* __restrict__ stats) {
+  constexpr int S = G::S;
+  constexpr double g = 0.43586652150845899941601945119356;
+  constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
+                   c32 = 0.92076794298330791242156818474003e1;
+  constexpr double m2 = 0.61697947043828245592553615689730e1, m3 = -0.42772256543218573326238373806514;
+  constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
+  const long c = (long)blockIdx.x * LANES + threadIdx.x;
+  if (c >= n) return;
+  const double T = Tf[c], rho = rhof[c];
+  double Y0[S], y[S], sc[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    Y0[i] = Yf[(long)i * n + c];
+    y[i] = rho * Y0[i] / G::W[i];
+    sc[i] = atol * rho / G::W[i];
+  }
+  int steps = 0, rejects = 0;
+  if (T >= Tmin) {
+    double k[G::NK];
+    G::consts(T, k);
+    double t = 0.0, h = dt;
+    while (t < dt) {
+      if (steps + rejects >= max_steps) { steps = -1; break; }
+      if (t + h > dt) h = dt - t;
+      const double hg = h * g, rh = 1.0 / h;
+      double f0[S], A[S * S];
+      G::wdot(T, k, y, f0);
+#pragma unroll
+      for (int e = 0; e < S * S; ++e) A[e] = 0.0;
+      G::jac(T, k, y, A);
+#pragma unroll
+      for (int e = 0; e < S * S; ++e) A[e] = (e % (S + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
+      bool ok = G::factor(A);
+      double err = 0.0, yn[S];
+      if (ok) {
+        double k1[S], k2[S], k3[S], y2[S], f2[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) k1[i] = hg * f0[i];
+        G::solve(A, k1);
+#pragma unroll
+        for (int i = 0; i < S; ++i) y2[i] = y[i] + k1[i];
+        G::wdot(T, k, y2, f2);
+#pragma unroll
+        for (int i = 0; i < S; ++i) k2[i] = hg * (f2[i] + c21 * rh * k1[i]);
+        G::solve(A, k2);
+#pragma unroll
+        for (int i = 0; i < S; ++i) k3[i] = hg * (f2[i] + rh * (c31 * k1[i] + c32 * k2[i]));
+        G::solve(A, k3);
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          yn[i] = y[i] + k1[i] + m2 * k2[i] + m3 * k3[i];
+          const double e = e1 * k1[i] + e2 * k2[i] + e3 * k3[i];
+          err = fmax(err, fabs(e) / (sc[i] + rtol * fmax(fabs(y[i]), fabs(yn[i]))));
+        }
+        if (!(err == err)) ok = false;
+      }
+      if (ok && err <= 1.0) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) y[i] = yn[i];
+        t += h;
+        ++steps;
+        const double fac = err > 0.0 ? 0.9 * pow(err, -1.0 / 3.0) : 5.0;
+        h = h * fmin(5.0, fmax(0.2, fac));
+      } else {
+        ++rejects;
+        const double fac = ok ? 0.9 * pow(err, -1.0 / 3.0) : 0.25;
+        h = h * fmin(0.5, fmax(0.1, fac));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double Yn = y[i] * G::W[i] / rho;
+    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho / dt : 0.0;
+  }
+  stats[c] = steps;
+  stats[n + c] = rejects;
+}
+
+// FNV-1a over the packed mechanism, NASA7 rows and molecular weights (dfmi/chem_codegen.py:fingerprint)
+unsigned long long fnv(unsigned long long h, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ull; }
+  return h;
+}
+
 }  // namespace
 
 void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd) {
@@ -390,6 +485,9 @@ void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* 
   DFMI_CHECK(x.S > 0 && R > 0 && R <= 256, "chemistry: bad reaction count");
   h.R = R;
   h.ndd = 17 + x.S;
+  h.h_idata.assign(idata, idata + (size_t)R * 8);
+  h.h_irs.assign(irs, irs + (size_t)R * 6);
+  h.h_dd.assign(dd, dd + (size_t)R * (17 + x.S));
   h.idata.upload(idata, (size_t)R * 8, x.stream);
   h.irs.upload(irs, (size_t)R * 6, x.stream);
   h.dd.upload(dd, (size_t)R * h.ndd, x.stream);
@@ -411,6 +509,31 @@ void chem_solve(Ctx& x, double dt) {
   double* stats = x.f("chem_stats");
   if (const char* e = std::getenv("DFMI_CHEM_METHOD")) h.method = std::string(e) == "extrap" ? 1 : 0;
   const dim3 g((unsigned)blocks_for(x.C, LANES));
+  // compiled-in mechanism? (bitwise the same arrays, NASA7 and weights)
+  unsigned long long fp = 0xcbf29ce484222325ull;
+  const int S32 = x.S;
+  fp = fnv(fp, &S32, 4);
+  fp = fnv(fp, h.h_idata.data(), h.h_idata.size() * 4);
+  fp = fnv(fp, h.h_irs.data(), h.h_irs.size() * 4);
+  fp = fnv(fp, h.h_dd.data(), h.h_dd.size() * 8);
+  fp = fnv(fp, x.thermo.nasa.data(), x.thermo.nasa.size() * 8);
+  fp = fnv(fp, x.thermo.W.data(), x.thermo.W.size() * 8);
+  h.generated = 0;
+  if (!std::getenv("DFMI_CHEM_GENERIC") && h.method == 0) {
+    if (fp == ChemGen_burke9::FINGERPRINT) h.generated = 1;
+    else if (fp == ChemGen_es80::FINGERPRINT) h.generated = 2;
+  }
+  if (h.generated) {
+    KScope _ks(x, "k_chem");
+    if (h.generated == 1)
+      hipLaunchKernelGGL(k_chem_gen<ChemGen_burke9>, g, dim3(LANES), 0, x.stream, (long)x.C, x.f("T"), x.f("rho"),
+                         x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+    else
+      hipLaunchKernelGGL(k_chem_gen<ChemGen_es80>, g, dim3(LANES), 0, x.stream, (long)x.C, x.f("T"), x.f("rho"),
+                         x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+    DFMI_HIP(hipGetLastError());
+    return;
+  }
 #define CALL(NS)                                                                                                    \
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \

@@ -84,6 +84,9 @@ struct Chem {
   double rtol = 1e-6, atol = 1e-10, Tmin = 0.0;   // CVODE settings of the reference (CanteraTorchProperties)
   int max_steps = 100000;
   int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
+  int generated = 0;            // last solve used a compiled-in mechanism (chem_gen_*.inc): 1 burke9, 2 es80
+  std::vector<int> h_idata, h_irs;
+  std::vector<double> h_dd;
 };
 
 // HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)

@@ -41,18 +41,26 @@ __global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Flo
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  // global -> LDS: each thread moves 2 x 16 B of A and of W per K tile
-  auto load_tile = [&](int buf, int k0) {
+  // global -> registers -> LDS, register double-buffered: the next K tile's global loads are issued
+  // before this tile's MFMAs and stored to the other LDS buffer after them
+  half8 ra[2], rw[2];
+  auto gload = [&](int k0) {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int idx = tid + it * GT;          // 0..511
       const int r = idx >> 2, c = (idx & 3) * 8;
-      half8 va = {}, vw = {};
       const int gm = m0 + r, gn = n0 + r;
-      if (gm < M) va = *reinterpret_cast<const half8*>(A + (long)gm * K + k0 + c);
-      if (gn < N) vw = *reinterpret_cast<const half8*>(W + (long)gn * K + k0 + c);
-      *reinterpret_cast<half8*>(&As[buf][r * LDK + c]) = va;
-      *reinterpret_cast<half8*>(&Ws[buf][r * LDK + c]) = vw;
+      ra[it] = gm < M ? *reinterpret_cast<const half8*>(A + (long)gm * K + k0 + c) : half8{};
+      rw[it] = gn < N ? *reinterpret_cast<const half8*>(W + (long)gn * K + k0 + c) : half8{};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * GT;
+      const int r = idx >> 2, c = (idx & 3) * 8;
+      *reinterpret_cast<half8*>(&As[buf][r * LDK + c]) = ra[it];
+      *reinterpret_cast<half8*>(&Ws[buf][r * LDK + c]) = rw[it];
     }
   };
   f32x16 acc[2][2];
@@ -63,12 +71,13 @@ __global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Flo
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
   const int nk = K / BK;
-  load_tile(0, 0);
+  gload(0);
+  lstore(0);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(cur ^ 1, (kt + 1) * BK);
+    if (kt + 1 < nk) gload((kt + 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 16) {
       half8 af[2], bf[2];
@@ -81,6 +90,7 @@ __global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Flo
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+    if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
   // epilogue: C/D map col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)

@@ -65,6 +65,7 @@ SIGNATURES = {
     "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
     "dfmi_chem_set_options": [_P, C.c_int, C.c_double, C.c_double, C.c_double],
     "dfmi_chem_solve": [_P, C.c_double],
+    "dfmi_chem_info": [_P, _IP],
     "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
                            C.c_double],
     "dfmi_dnn_infer": [_P, _IP],
@@ -234,6 +235,11 @@ class Context:
 
     def chem_solve(self, dt):
         self._call("dfmi_chem_solve", self.h, float(dt))
+
+    def chem_info(self):
+        g = C.c_int()
+        self._call("dfmi_chem_info", self.h, C.byref(g))
+        return g.value
 
     def dnn_set_model(self, dims, params, x_mu, x_std, y_mu, y_std, T_react=610.0, dt_infer=1e-6):
         """params: list over modules of [(W [out,in], b [out]) per layer] (numpy float32)."""

@@ -143,6 +143,9 @@ int dfmi_chem_set_options(dfmi_ctx* ctx, int mode, double rtol, double atol, dou
 /* integrate every cell over dt at fixed T, rho -> field "RR" = (Y(dt) - Y) rho / dt; field
  * "chem_stats" [2][C] = accepted / rejected steps (-1: step limit hit) */
 int dfmi_chem_solve(dfmi_ctx* ctx, double dt);
+/* which integrator the last solve used: 0 data-driven generic kernel, > 0 a mechanism compiled in
+ * by dfmi/chem_codegen.py (1 Burke2012_s9r23, 2 ES80_H2-7-16) */
+int dfmi_chem_info(dfmi_ctx* ctx, int* generated);
 
 /* ---- DF-ODENet surrogate (dfChemistrySolver::setConstantValue/Inference,
  * dfChemistrySolver.cu:78-206; model test/Tu500K-Phi1/inference.py:12-25) ---------------------- */

@@ -45,12 +45,14 @@ def _states(ym, n, seed=0):
     return T, rho, Y
 
 
-@pytest.mark.parametrize("method", ["ros3", "extrap"])
+@pytest.mark.parametrize("method", ["ros3", "ros3-generic", "extrap"])
 @pytest.mark.parametrize("mech", [("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
                                   ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt")])
 def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     from chem_oracle import Kinetics
-    monkeypatch.setenv("DFMI_CHEM_METHOD", method)
+    monkeypatch.setenv("DFMI_CHEM_METHOD", method.split("-")[0])
+    if method.endswith("generic"):
+        monkeypatch.setenv("DFMI_CHEM_GENERIC", "1")
     ctx, m, ym, mc = _setup(*mech)
     C = m.n_cells
     T, rho, Y = _states(ym, C)
@@ -64,6 +66,8 @@ def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
     ctx.chem_solve(dt)
     assert ctx.get_field("chem_stats", (2, C))[0].min() >= 1      # no cell hit the step limit
+    if method == "ros3" and mech[0].startswith("Burke"):
+        assert ctx.chem_info() == 1                               # the compiled-in mechanism ran
     rr = ctx.get_field("RR", (mc.S, C))[:, idx]
     assert np.all(np.isfinite(rr))
     assert np.abs(rr - ref).max(axis=None, initial=0) / scale.max() < 1e-5
