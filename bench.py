@@ -229,6 +229,15 @@ def main():
     kbytes = algorithmic_bytes(args.kernel, m.n_cells, m.n_faces, m.n_boundary_slots, table.S)
     k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
     achieved = kbytes / k_avg_s / 1e9 if k_n else None
+    # HBM bytes per launch from the PMC passes committed under profiles/ (scripts/pmc_traffic.sh +
+    # scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) KB, gfx950 correction), same workload
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc) and n == 128 and world == 1:
+        tab = json.load(open(pmc))
+        for key, v in tab.items():
+            if key.split("::")[-1].split("<")[0] == args.kernel:
+                traffic = v["hbm_bytes_median"]
     out = {
         "metric": "cell-updates/s (dfLowMachFoam outer iter)",
         "value": value,
@@ -249,7 +258,8 @@ def main():
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
         "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
                      "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "amg_levels": ctx.amg_info(),
