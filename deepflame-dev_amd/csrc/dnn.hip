@@ -23,17 +23,22 @@ namespace {
 using half8 = __attribute__((ext_vector_type(8))) _Float16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDK = BK + 8;   // LDS row stride in halves (80 B) against bank conflicts
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int LDK = BK + 8;   // LDS row stride in halves (144 B) against bank conflicts
 constexpr int GT = 256;
+constexpr int LD_IT = BM * BK / 8 / GT;   // 16-byte global loads per thread per operand per K tile
 
 __device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
 
-// C[z][M][N] = act(A[z][M][K] . W[z][N][K]^T + b[z][N]), fp16 in/out, fp32 accumulate
+// C[z][M][N] = act(A[z][M][K] . W[z][N][K]^T + b[z][N]), fp16 in/out, fp32 accumulate.
+// Block 128x128, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles), K tile 64,
+// LDS double buffer fed through registers: the next tile's global loads are in flight during this
+// tile's 16 MFMAs per wave.
 template <bool GELU>
-__global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, long sA,
-                                                 const _Float16* __restrict__ W, long sW, const float* __restrict__ bias,
-                                                 long sb, _Float16* __restrict__ Cout, long sC) {
+__global__ void __launch_bounds__(GT, 2) k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, long sA,
+                                                    const _Float16* __restrict__ W, long sW,
+                                                    const float* __restrict__ bias, long sb,
+                                                    _Float16* __restrict__ Cout, long sC) {
   __shared__ _Float16 As[2][BM * LDK];
   __shared__ _Float16 Ws[2][BN * LDK];
   const int z = blockIdx.z;
@@ -41,24 +46,22 @@ __global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Flo
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  // global -> registers -> LDS, register double-buffered: the next K tile's global loads are issued
-  // before this tile's MFMAs and stored to the other LDS buffer after them
-  half8 ra[2], rw[2];
+  half8 ra[LD_IT], rw[LD_IT];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = tid + it * GT;          // 0..511
-      const int r = idx >> 2, c = (idx & 3) * 8;
+    for (int it = 0; it < LD_IT; ++it) {
+      const int idx = tid + it * GT;
+      const int r = idx / (BK / 8), c = (idx % (BK / 8)) * 8;
       const int gm = m0 + r, gn = n0 + r;
-      ra[it] = gm < M ? *reinterpret_cast<const half8*>(A + (long)gm * K + k0 + c) : half8{};
-      rw[it] = gn < N ? *reinterpret_cast<const half8*>(W + (long)gn * K + k0 + c) : half8{};
+      ra[it] = (gm < M && k0 + c < K) ? *reinterpret_cast<const half8*>(A + (long)gm * K + k0 + c) : half8{};
+      rw[it] = (gn < N && k0 + c < K) ? *reinterpret_cast<const half8*>(W + (long)gn * K + k0 + c) : half8{};
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < LD_IT; ++it) {
       const int idx = tid + it * GT;
-      const int r = idx >> 2, c = (idx & 3) * 8;
+      const int r = idx / (BK / 8), c = (idx % (BK / 8)) * 8;
       *reinterpret_cast<half8*>(&As[buf][r * LDK + c]) = ra[it];
       *reinterpret_cast<half8*>(&Ws[buf][r * LDK + c]) = rw[it];
     }
@@ -70,7 +73,7 @@ __global__ void __launch_bounds__(GT) k_mlp_gemm(int M, int N, int K, const _Flo
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  const int nk = K / BK;
+  const int nk = (K + BK - 1) / BK;
   gload(0);
   lstore(0);
   __syncthreads();
