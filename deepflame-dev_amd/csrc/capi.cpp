@@ -170,12 +170,15 @@ void do_Y(Ctx& x) {
   if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt);   // chemistry->solve(deltaT) before YEqn (YEqn.H)
   else if (x.chem.mode == 2) dnn_solve(x);              // chemistrySolver_GPU.Inference (YEqn_GPU.H)
   y_prep(x);
-  y_assemble(x);
   Matrix& A = x.mY;
   std::vector<int> map;
   for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
+  // production path: the assembly writes the solver's ELL rows directly (no LDU round trip)
+  double *val, *dS, *rhs;
+  bicg_layout(x, (int)map.size(), &val, &dS, &rhs);
+  y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
   solve_bicgstab(x, "Y", (int)map.size(), map.data(), A.lower, x.F, A.upper, x.F, A.diag, x.C, A.source, x.C, A.ic,
-                 A.bc, x.B, "Y", x.f("Y"), x.C, x.solver["Y"]);
+                 A.bc, x.B, "Y", x.f("Y"), x.C, x.solver["Y"], true);
   y_post_solve(x);
 }
 void do_E(Ctx& x) {

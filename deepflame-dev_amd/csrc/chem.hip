@@ -384,8 +384,11 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double
 }
 
 // ---- generated fast path: the mechanism compiled in (dfmi/chem_codegen.py), state in registers
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-variable"
 #include "chem_gen_burke9.inc"
 #include "chem_gen_es80.inc"
+#pragma clang diagnostic pop
 
 template <class G>
 __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const double* __restrict__ Tf,

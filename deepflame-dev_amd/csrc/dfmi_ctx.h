@@ -212,6 +212,7 @@ void p_assemble(Ctx& x);
 void p_post_solve(Ctx& x);
 void y_prep(Ctx& x);
 void y_assemble(Ctx& x);
+void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs);
 void y_post_solve(Ctx& x);
 void e_assemble(Ctx& x);
 void e_post_solve(Ctx& x);
@@ -226,7 +227,8 @@ void thermo_correct(Ctx& x, bool from_T);
 SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
                           const double* upper, long ustride, const double* diag, long dstride, const double* source,
                           long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
-                          double* xsol, long xstride, const SolverCfg& cfg);
+                          double* xsol, long xstride, const SolverCfg& cfg, bool prebuilt = false);
+void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs);
 SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg);

@@ -652,6 +652,83 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
   });
 }
 
+// The same YEqn assembly, emitted directly in the solver's ELL layout (production path): per
+// system (non-inert species) the row values [W][C] in the gather order (neighbour faces, owned
+// faces, coupled slots), dS = diag + sum internalCoeffs and rhs = source + non-coupled
+// boundaryCoeffs in slot order -- bitwise what k_ell_build makes from the LDU arrays, without writing
+// and re-reading lower/upper/internalCoeffs/boundaryCoeffs.
+template <int S>
+__global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
+    double* __restrict__ dS, double* __restrict__ rhs) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, B = m.B;
+  double d1 = 0.0, d2 = 0.0;
+  double dL[S], rc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
+  int k = 0;
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const double ph = phi[f], pu = phiUc[f];
+    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double L1 = -wu * ph, U1 = L1 + ph;
+    const double L2 = -wu * pu, U2 = L2 + pu;
+    if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+    const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
+    const double Ls = L1 + L2, Us = U1 + U2;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == inert) continue;
+      const int ss = s < inert ? s : s - 1;
+      const double rn = rhoD[s * C + o2];
+      const double UL = dcf * ((own ? interp_f(w, rc[s], rn) : interp_f(w, rn, rc[s])) * ms);
+      dL[s] -= UL;
+      val[((long)ss * W + k) * C + c] = own ? Us - UL : Ls - UL;
+    }
+    ++k;
+  });
+  const double vol = m.V[c];
+  const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+  const double ro = m.rdt * rho_old[c];
+  double dg[S], sr[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    dg[s] = dd - dL[s];
+    sr[s] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
+  }
+  each_slot(m, tyY, c, [&](int b, int t) {
+    const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+    const bool cp = bc_coupled(t);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == inert) continue;
+      const int ss = s < inert ? s : s - 1;
+      const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
+      const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+      const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+      const double pG = gam * m.bmagSf[b];
+      const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+      const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+      dg[s] += icv;
+      if (cp) val[((long)ss * W + k) * C + c] = -bcv;
+      else sr[s] += bcv;
+    }
+    if (cp) ++k;
+  });
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s == inert) continue;
+    const int ss = s < inert ? s : s - 1;
+    for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + c] = 0.0;
+    dS[ss * Ce + c] = dg[s];
+    rhs[ss * Ce + c] = sr[s];
+  }
+}
+
 template <int S>
 __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -853,6 +930,15 @@ void y_assemble(Ctx& x) {
 #define CALL(NS) LAUNCH(k_y_assemble<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
                         x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p)
+  DFMI_SWITCH_S(x.S, CALL)
+#undef CALL
+}
+
+void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs) {
+  MeshView m = x.view();
+#define CALL(NS) LAUNCH(k_y_assemble_ell<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
+                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
+                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs)
   DFMI_SWITCH_S(x.S, CALL)
 #undef CALL
 }

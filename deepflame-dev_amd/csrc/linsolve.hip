@@ -458,18 +458,33 @@ void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce) {
 
 }  // namespace
 
-SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
-                          const double* upper, long ustride, const double* diag, long dstride, const double* source,
-                          long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
-                          double* xsol, long xstride, const SolverCfg& cfg) {
+// BiCGStab workspace: 11 vectors of nsys * (C + H), then the ELL values [nsys][W][C], then partials.
+// Assembly kernels that emit the ELL form directly (y_assemble_ell) write into it before the solve.
+void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   if (!x.ell.ready) build_ell(x);
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
+  const size_t need = 11 * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 6 + 64;
+  if (x.ws.buf.n < need) x.ws.buf.alloc(need);
+  const long N = nsys * Ce;
+  *dS = x.ws.buf.p;
+  *rhs = x.ws.buf.p + N;
+  *val = x.ws.buf.p + 11 * N;
+}
+
+SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
+                          const double* upper, long ustride, const double* diag, long dstride, const double* source,
+                          long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
+                          double* xsol, long xstride, const SolverCfg& cfg, bool prebuilt) {
+  {
+    double *v_, *d_, *r_;
+    bicg_layout(x, nsys, &v_, &d_, &r_);
+  }
+  const long C = x.C, Ce = (long)x.C + x.H;
+  const int W = x.ell.W;
+  const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   auto& WS = x.ws;
-  const size_t nvec = 11;
-  const size_t need = nvec * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 6 + 64;
-  if (WS.buf.n < need) WS.buf.alloc(need);
   if (WS.scal.n < (size_t)nsys * NSCAL) WS.scal.alloc((size_t)nsys * NSCAL);
   const int* smap = nullptr;
   if (sys_map_host) {
@@ -490,7 +505,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   const int8_t* ty = x.st(type_field);
   dim3 g(nblk, nsys), bl(TPB);
   Launch L{x, nblk, nsys};
-  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, smap, W, x.ell.src.p, Ce, val, b.dS, b.rhs); }
+  if (!prebuilt) {
+    KScope _ks(x, "k_ell_build");
+    hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, smap, W, x.ell.src.p, Ce, val, b.dS, b.rhs);
+  }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, smap, b.xw); }
   DFMI_HIP(hipGetLastError());
   halo_vecs(x, {b.xw}, nsys, Ce);
