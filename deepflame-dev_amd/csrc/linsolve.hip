@@ -176,21 +176,14 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const 
   block_partials<2>(acc, partial, s);
 }
 
-// ---- fused iteration (3 kernels): the direction and intermediate vectors are recomputed on the fly
-// for the neighbours an SpMV gathers instead of being stored by separate vector passes.
-struct BF { const double *dS, *r, *r0, *pold, *vold; double *pnew, *vnew, *t; };
-
-// prologue: res, rho from (r.r, r0.r); convergence; beta. p = r + beta (p_old - omega v_old) (own cell
-// stored, neighbours recomputed); v = A (p / dS); partial r0.v
-template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_pv(long C, long Ce, int W_, const int* __restrict__ col,
-                                                const double* __restrict__ val, int it, int max_iter, double tol,
-                                                double abs_tol, Red red, double* scal, BF b, double* partial) {
+// prologue: res, rho from (r.r, r0.r); convergence; p = r + beta (p - omega v); phat = p / dS
+__global__ void __launch_bounds__(TPB) k_bcg_p(long C, long Ce, int it, int max_iter, double tol, double abs_tol,
+                                               Red red, double* scal, BV b) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
-  double rv[2];
-  red_sum<2>(red, s, rv);
-  const double res = sqrt(rv[0]), rho = rv[1];
+  double v[2];
+  red_sum<2>(red, s, v);
+  const double res = sqrt(v[0]), rho = v[1];
   const double res0 = it == 0 ? res : st[4];
   const double omega = st[3];
   const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || omega == 0.0));
@@ -202,67 +195,58 @@ __global__ void __launch_bounds__(TPB) k_bcg_pv(long C, long Ce, int W_, const i
   }
   if (stop) return;
   const double beta = it == 0 ? 0.0 : (rho / st[1]) * (st[2] / omega);
-  const int W = WT > 0 ? WT : W_;
-  const double* vs = val + (long)s * W * C;
-  const double* r = b.r + s * Ce;
-  const double* po = b.pold + s * Ce;
-  const double* vo = b.vold + s * Ce;
-  const double* dS = b.dS + s * Ce;
-  auto pdir = [&](long j) { return it == 0 ? r[j] : r[j] + beta * (po[j] - omega * vo[j]); };
-  double acc[1] = {0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const double pc = pdir(c);
-    b.pnew[s * Ce + c] = pc;
-    double y = dS[c] * (pc / dS[c]);
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col[k * C + c];
-      y += vs[k * C + c] * (pdir(j) / dS[j]);
-    }
-    b.vnew[s * Ce + c] = y;
-    acc[0] += b.r0[s * Ce + c] * y;
+    const long i = s * Ce + c;
+    const double pv = it == 0 ? b.r[i] : b.r[i] + beta * (b.p[i] - omega * b.v[i]);
+    b.p[i] = pv;
+    b.phat[i] = pv / b.dS[i];
   }
-  block_partials<1>(acc, partial, s);
 }
 
-// prologue: alpha = rho / (r0.v). s = r - alpha v (recomputed for the neighbours); t = A (s / dS);
-// partials (t.s, t.t)
-template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_st(long C, long Ce, int W_, const int* __restrict__ col,
-                                                const double* __restrict__ val, Red red, double* scal, BF b,
-                                                double* partial) {
+// out = A in; partial dots (NV = 1: r0.out; NV = 2: out.sv, out.out)
+template <int WT, int NV>
+__global__ void __launch_bounds__(TPB) k_bcg_spmv(long C, long Ce, int W, const int* __restrict__ col,
+                                                  const double* __restrict__ val, const double* scal,
+                                                  const double* __restrict__ dS, const double* __restrict__ in,
+                                                  double* __restrict__ out, const double* __restrict__ dotv,
+                                                  double* partial) {
+  const int s = blockIdx.y;
+  if (scal[s * NSCAL + 6] == 0.0) return;   // uniform per block
+  const double* vs = val + (long)s * W * C;
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double y = ell_mv<WT>(W, C, col, vs, dS[i], in + s * Ce, c);
+    out[i] = y;
+    if (NV == 1) acc[0] += dotv[i] * y;
+    else { acc[0] += y * dotv[i]; acc[NV - 1] += y * y; }
+  }
+  block_partials<NV>(acc, partial, s);
+}
+
+// prologue: alpha = rho / (r0.v); s = r - alpha v; shat = s / dS
+__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
-  double pv[1];
-  red_sum<1>(red, s, pv);
+  double v[1];
+  red_sum<1>(red, s, v);
   const double rho = st[0];
-  const double alpha = pv[0] != 0.0 ? rho / pv[0] : 0.0;
+  const double alpha = v[0] != 0.0 ? rho / v[0] : 0.0;
   if (leader()) { st[2] = alpha; st[1] = rho; }
-  const int W = WT > 0 ? WT : W_;
-  const double* vs = val + (long)s * W * C;
-  const double* r = b.r + s * Ce;
-  const double* v = b.vnew + s * Ce;
-  const double* dS = b.dS + s * Ce;
-  double acc[2] = {0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const double sc = r[c] - alpha * v[c];
-    double y = dS[c] * (sc / dS[c]);
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col[k * C + c];
-      y += vs[k * C + c] * ((r[j] - alpha * v[j]) / dS[j]);
-    }
-    b.t[s * Ce + c] = y;
-    acc[0] += y * sc;
-    acc[1] += y * y;
+    const long i = s * Ce + c;
+    const double ss = b.r[i] - alpha * b.v[i];
+    b.sv[i] = ss;
+    b.shat[i] = ss / b.dS[i];
   }
-  block_partials<2>(acc, partial, s);
 }
 
-// prologue: omega = (t.s)/(t.t). x += alpha p/dS + omega s/dS; r = s - omega t; partials (r.r, r0.r)
-__global__ void __launch_bounds__(TPB) k_bcg_xr(long C, long Ce, Red red, Sys q, const int* __restrict__ sys_map,
-                                                double* scal, BF b, double* __restrict__ rw, double* partial) {
+// prologue: omega = (t.s)/(t.t); x += alpha phat + omega shat; r = s - omega t; partials (r.r, r0.r)
+__global__ void __launch_bounds__(TPB) k_bcg_x(long C, long Ce, Red red, Sys q, const int* __restrict__ sys_map,
+                                               double* scal, BV b, double* partial) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
@@ -275,12 +259,10 @@ __global__ void __launch_bounds__(TPB) k_bcg_xr(long C, long Ce, Red red, Sys q,
   double* xv = q.x + ms * q.xstride;
   double acc[2] = {0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const long i = (long)s * Ce + c;
-    const double d = b.dS[i];
-    const double sc = b.r[i] - alpha * b.vnew[i];
-    xv[c] = xv[c] + alpha * (b.pnew[i] / d) + omega * (sc / d);
-    const double rr = sc - omega * b.t[i];
-    rw[i] = rr;
+    const long i = s * Ce + c;
+    xv[c] = xv[c] + alpha * b.phat[i] + omega * b.shat[i];
+    const double rr = b.sv[i] - omega * b.t[i];
+    b.r[i] = rr;
     acc[0] += rr * rr;
     acc[1] += b.r0[i] * rr;
   }
@@ -520,29 +502,25 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   Red red = L.after(p1, 2);
   WS.hscal.resize((size_t)nsys * NSCAL);
   const int check = 2;
-  halo_vecs(x, {b.dS}, nsys, Ce);
-  // buffers: p and v alternate between two arrays (the fused kernels read the old ones for neighbours)
-  double* pbuf[2] = {b.p, b.phat};
-  double* vbuf[2] = {b.v, b.shat};
   for (int it = 0;; ++it) {
-    BF f{b.dS, b.r, b.r0, pbuf[it & 1], vbuf[it & 1], pbuf[(it + 1) & 1], vbuf[(it + 1) & 1], b.t};
-    halo_vecs(x, {b.r, pbuf[it & 1], vbuf[it & 1]}, nsys, Ce);
-    dispatch_W(W, [&](auto wt) {
-      constexpr int WT = decltype(wt)::value;
-      KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL(k_bcg_pv<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
-                         cfg.abs_tol, red, WS.scal.p, f, p2);
-    });
+    { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, C, Ce, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red, WS.scal.p, b); }
     if (it >= cfg.max_iter) break;
-    red = L.after(p2, 1);
-    halo_vecs(x, {f.vnew}, nsys, Ce);
+    halo_vecs(x, {b.phat}, nsys, Ce);
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL(k_bcg_st<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, red, WS.scal.p, f, p3);
+      hipLaunchKernelGGL((k_bcg_spmv<WT, 1>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.phat, b.v, b.r0, p2);
+    });
+    red = L.after(p2, 1);
+    { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
+    halo_vecs(x, {b.shat}, nsys, Ce);
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_spmv");
+      hipLaunchKernelGGL((k_bcg_spmv<WT, 2>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.shat, b.t, b.sv, p3);
     });
     red = L.after(p3, 2);
-    { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_xr, g, bl, 0, x.stream, C, Ce, red, q, smap, WS.scal.p, f, b.r, p1); }
+    { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, C, Ce, red, q, smap, WS.scal.p, b, p1); }
     DFMI_HIP(hipGetLastError());
     red = L.after(p1, 2);
     if ((it + 1) % check == 0) {
