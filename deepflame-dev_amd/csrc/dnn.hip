@@ -23,15 +23,15 @@ namespace {
 using half8 = __attribute__((ext_vector_type(8))) _Float16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int LDK = BK + 8;   // LDS row stride in halves (144 B) against bank conflicts
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDK = BK + 8;   // LDS row stride in halves (80 B) against bank conflicts
 constexpr int GT = 256;
 constexpr int LD_IT = BM * BK / 8 / GT;   // 16-byte global loads per thread per operand per K tile
 
 __device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
 
 // C[z][M][N] = act(A[z][M][K] . W[z][N][K]^T + b[z][N]), fp16 in/out, fp32 accumulate.
-// Block 128x128, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles), K tile 64,
+// Block 128x128, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles), K tile 32,
 // LDS double buffer fed through registers: the next tile's global loads are in flight during this
 // tile's 16 MFMAs per wave.
 template <bool GELU>
