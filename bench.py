@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
     ap.add_argument("--mech", default="burke9", choices=sorted(MECHS))
     ap.add_argument("--ncorr", type=int, default=2)
+    ap.add_argument("--init", default="reference", choices=["reference", "tgv"],
+                    help="initial state: the reference's own 64^3 TGV 0/ fields tiled (BASELINE config 3), or the "
+                         "analytic TGV")
     ap.add_argument("--dt", type=float, default=1e-6)
     ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
     ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
@@ -87,7 +90,7 @@ def cpu_baseline(args, table, ym, inert):
     n = args.cpu_n
     m = hex_box(n, n, n)
     pt = case.default_patch_types(m)
-    f = case.tgv_fields(m, ym["species"])
+    f = reference_fields(m, ym["species"]) if args.init == "reference" else case.tgv_fields(m, ym["species"])
     st = host_state(m, table, f)
     o = O.Oracle(m, table, st, pt, inert, 1.0 / args.dt)
     t0 = time.perf_counter()
@@ -116,6 +119,22 @@ def cpu_baseline(args, table, ym, inert):
                    f"{chem_s_per_cell * 1e3:.2f} ms/cell")
     return {"value": 1.0 / (flow_s_per_cell + chem_s_per_cell), "unit": "cell-updates/s", "cores": 1, "kind": "port",
             "sample": sample}
+
+
+def reference_fields(m, species):
+    """The reference example's initial state (examples/dfLowMachFoam/notorch/threeD_reactingTGV/H2/
+    cvodeIntegrator/0, 64^3, committed under tests/golden/tgv64) tiled periodically over this
+    rank's block of the global box (BASELINE config 3: 64^3 fields tiled 2x2x2 into 128^3)."""
+    import numpy as np
+    from dfmi.foam_io import read_case_fields
+    src = read_case_fields(os.path.join(ROOT, "tests", "golden", "tgv64"), species)
+    ii, jj, kk = m.local_index
+    lnx, lny, lnz = m.block_dims
+    rx, ry, rz = m.block
+    gi, gj, gk = rx * lnx + ii, ry * lny + jj, rz * lnz + kk
+    idx = (gi % 64) + 64 * ((gj % 64) + 64 * (gk % 64))
+    return {"T": src["T"][idx], "p": src["p"][idx], "U": np.ascontiguousarray(src["U"][:, idx]),
+            "Y": np.ascontiguousarray(src["Y"][:, idx])}
 
 
 def host_state(m, table, f):
@@ -190,7 +209,10 @@ def main():
         from dfmi import dnn_model
         dnn_model.configure(ctx)
         ctx.chem_set_options(2)
-    f = case.tgv_fields(m, ym["species"])
+    if args.init == "reference":
+        f = reference_fields(m, ym["species"])
+    else:
+        f = case.tgv_fields(m, ym["species"])
     case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
     del f
 
@@ -250,7 +272,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (reacting Taylor-Green vortex initial state, hex box generated in-process)",
+        "data": ("reference initial fields (examples/dfLowMachFoam/notorch/threeD_reactingTGV/H2/cvodeIntegrator/0, "
+                 "64^3, committed as tests/golden/tgv64) tiled over a hex box generated in-process"
+                 if args.init == "reference" else "synthetic analytic TGV on a hex box generated in-process"),
         "config": {"workload": f"dfLowMachFoam 3D periodic box {n * decomp[0]}x{n * decomp[1]}x{n * decomp[2]} = "
                                f"{cells_total} hex cells ({m.n_cells} per GPU), H2/air {table.S} species "
                                f"({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
