@@ -9,9 +9,8 @@
 // (block-Jacobi across processor faces); the outer PCG SpMV carries the halo.
 // Per solve: Galerkin coarse operators P^T A P (piecewise-constant P) are summed on the device from
 // precomputed contribution lists in a fixed order -- deterministic, no atomics.
-// V-cycle: one weighted-Jacobi pre-sweep from zero fused with the residual and the restriction (one
-// pass per level, nothing stored but the coarse right-hand side), coarse correction, prolongation
-// fused with one post-sweep (the pre-smoothed x recomputed from b and D); the coarsest level (<= 4096 cells) is
+// V-cycle: one weighted-Jacobi pre-sweep from zero (fused into the residual pass), restriction,
+// coarse correction, prolongation fused with one post-sweep; the coarsest level (<= 4096 cells) is
 // smoothed by a fixed number of Jacobi sweeps inside one workgroup (LDS-resident vectors). All pieces
 // are linear and the pre/post sweeps are adjoint, so the preconditioner is symmetric (valid for CG).
 #include "dfmi_ctx.h"
@@ -47,54 +46,52 @@ __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, co
   }
 }
 
-// Pre-smoothing and restriction fused, one thread per coarse cell I: for every member i of I
-// (ascending), x_i = omega b_i / D_i (one Jacobi sweep from zero), r_i = b_i - (A x)_i with the
-// neighbours' x recomputed from b and D, and b_coarse[I] = sum_i r_i in member order (deterministic).
-// Neither x nor r is stored: the prolongation recomputes x from b and D. Columns >= n (other ranks)
-// are dropped (the preconditioner is rank-local).
+// x = omega b / D (first sweep from zero); r = b - A x   (columns >= n: other ranks, dropped)
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_smooth_restrict(int n, int W_, const int* __restrict__ col,
-                                                         const double* __restrict__ val, const double* __restrict__ D,
-                                                         const double* __restrict__ b, double omega, int nc,
-                                                         const int* __restrict__ mstart,
-                                                         const int* __restrict__ members, double* __restrict__ bc) {
+__global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __restrict__ col,
+                                                    const double* __restrict__ val, const double* __restrict__ D,
+                                                    const double* __restrict__ b, double omega,
+                                                    double* __restrict__ x, double* __restrict__ r) {
   const int W = WT > 0 ? WT : W_;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const double xc = omega * b[c] / D[c];
+  double y = D[c] * xc;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const int j = col[(long)k * n + c];
+    if (j < n) y += val[(long)k * n + c] * (omega * b[j] / D[j]);
+  }
+  x[c] = xc;
+  r[c] = b[c] - y;
+}
+
+__global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
+                           const double* __restrict__ r, double* __restrict__ bc) {
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
   if (I >= nc) return;
   double a = 0.0;
-  const int e1 = mstart[I + 1];
-  for (int e = mstart[I]; e < e1; ++e) {
-    const int c = members[e];
-    const double xc = omega * b[c] / D[c];
-    double y = D[c] * xc;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col[(long)k * n + c];
-      if (j < n) y += val[(long)k * n + c] * (omega * b[j] / D[j]);
-    }
-    a += b[c] - y;
-  }
+  for (int e = mstart[I]; e < mstart[I + 1]; ++e) a += r[members[e]];
   bc[I] = a;
 }
 
-// y = omega b / D + P xc (the pre-smoothed x recomputed); out = y + omega (b - A y) / D; optional
-// block partials of b.out (level 0: r.z)
+// y = x + P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z)
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int* __restrict__ col,
                                                         const double* __restrict__ val, const double* __restrict__ D,
-                                                        const double* __restrict__ b, const int* __restrict__ agg,
-                                                        const double* __restrict__ xc, double omega,
-                                                        double* __restrict__ out, double* partial) {
+                                                        const double* __restrict__ b, const double* __restrict__ x,
+                                                        const int* __restrict__ agg, const double* __restrict__ xc,
+                                                        double omega, double* __restrict__ out, double* partial) {
   const int W = WT > 0 ? WT : W_;
   __shared__ double sh[TPB / 64];
   double acc = 0.0;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
-    const double yc = omega * b[c] / D[c] + xc[agg[c]];
+    const double yc = x[c] + xc[agg[c]];
     double ay = D[c] * yc;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
       const int j = col[(long)k * n + c];
-      if (j < n) ay += val[(long)k * n + c] * (omega * b[j] / D[j] + xc[agg[j]]);
+      if (j < n) ay += val[(long)k * n + c] * (x[j] + xc[agg[j]]);
     }
     const double o = yc + omega * (b[c] - ay) / D[c];
     out[c] = o;
@@ -409,17 +406,23 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, co
   auto DD = [&](int l) { return l == 0 ? D0 : (const double*)a.lv[l].D.p; };
   auto COL = [&](int l) { return l == 0 ? col0 : (const int*)a.lv[l].col.p; };
   auto B = [&](int l) { return l == 0 ? r : (const double*)a.lv[l].b.p; };
-  // down: pre-smooth + restrict, one fused pass per level
+  // down
   for (int l = 0; l + 1 < L; ++l) {
     AmgLevel& f = a.lv[l];
-    AmgLevel& cl = a.lv[l + 1];
-    KScope _ks(x, "k_smooth_restrict");
-    if (f.W == 6)
-      hipLaunchKernelGGL(k_smooth_restrict<6>, dim3(blocks_for(cl.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
-                         VAL(l), DD(l), B(l), om, cl.n, f.mstart.p, f.members.p, cl.b.p);
-    else
-      hipLaunchKernelGGL(k_smooth_restrict<0>, dim3(blocks_for(cl.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
-                         VAL(l), DD(l), B(l), om, cl.n, f.mstart.p, f.members.p, cl.b.p);
+    {
+      KScope _ks(x, "k_smooth_res");
+      if (f.W == 6)
+        hipLaunchKernelGGL(k_smooth_res<6>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
+                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
+      else
+        hipLaunchKernelGGL(k_smooth_res<0>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
+                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
+    }
+    {
+      KScope _ks(x, "k_restrict");
+      hipLaunchKernelGGL(k_restrict, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
+                         f.mstart.p, f.members.p, f.r.p, a.lv[l + 1].b.p);
+    }
   }
   // coarsest
   {
@@ -432,18 +435,19 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, co
     KScope _ks(x, "k_dot_partial");
     hipLaunchKernelGGL(k_dot_partial, dim3(nblk), dim3(TPB), 0, x.stream, x.C, r, (const double*)z, partial);
   }
-  // up: prolongate + post-smooth; the corrected solution of level l is the coarse input of level l-1
+  // up
   for (int l = L - 2; l >= 0; --l) {
     AmgLevel& f = a.lv[l];
-    double* out = l == 0 ? z : f.x.p;
+    double* out = l == 0 ? z : f.xo.p;
     KScope _ks(x, "k_prolong_smooth");
     const dim3 grid = l == 0 ? dim3(nblk) : dim3(blocks_for(f.n, TPB));
     if (f.W == 6)
       hipLaunchKernelGGL(k_prolong_smooth<6>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
-                         f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
+                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
     else
       hipLaunchKernelGGL(k_prolong_smooth<0>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
-                         f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
+                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
+    if (l > 0) std::swap(f.x, f.xo);   // the corrected x of this level feeds the next finer prolongation
   }
   DFMI_HIP(hipGetLastError());
 }
