@@ -165,6 +165,21 @@ def host_state(m, table, f):
     return s
 
 
+def chem_step_stats(ctx, C):
+    """Integrator steps per cell of the last chemistry solve and how evenly 64-lane waves are loaded:
+    a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
+    cell order and in the descending-cost order the binned launch approximates."""
+    import numpy as np
+    st = ctx.get_field("chem_stats", (2, C))
+    cost = np.maximum(st[0], 0) + st[1]
+    pad = (-C) % 64
+    nat = np.concatenate([cost, np.zeros(pad)]).reshape(-1, 64).max(axis=1).mean()
+    srt = np.concatenate([np.sort(cost)[::-1], np.zeros(pad)]).reshape(-1, 64).max(axis=1).mean()
+    return {"steps_mean": float(st[0].mean()), "rejects_mean": float(st[1].mean()), "steps_max": float(cost.max()),
+            "wave_eff_natural": float(cost.mean() / nat) if nat else None,
+            "wave_eff_sorted": float(cost.mean() / srt) if srt else None}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -221,7 +236,7 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    extra = {"ode": ",k_chem", "dnn": ",k_mlp_gemm", "off": ""}[args.chem]
+    extra = {"ode": ",k_chem,k_bin", "dnn": ",k_mlp_gemm", "off": ""}[args.chem]
     ctx.kernel_timer(args.kernel + extra)
     if args.chem == "dnn":
         ctx.dnn_stats()
@@ -234,6 +249,7 @@ def main():
         dist.barrier()
     k_ms, k_n = ctx.kernel_time(args.kernel)
     chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
+    bin_ms, _ = ctx.kernel_time("k_bin") if args.chem == "ode" else (0.0, 0)
     gemm_ms, gemm_n = ctx.kernel_time("k_mlp_gemm") if args.chem == "dnn" else (0.0, 0)
     n_react, gemm_flops = ctx.dnn_stats() if args.chem == "dnn" else (0, 0.0)
     ctx.kernel_timer("")
@@ -289,7 +305,9 @@ def main():
         "amg_levels": ctx.amg_info(),
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
-                       "k_chem_ms_per_step": chem_ms / max(chem_n, 1)} if args.chem == "ode" else None),
+                       "k_chem_ms_per_step": chem_ms / max(chem_n, 1),
+                       "k_bin_ms_per_step": bin_ms / max(chem_n, 1),
+                       **chem_step_stats(ctx, m.n_cells)} if args.chem == "ode" else None),
         "dnn": ({"reacting_cells": n_react, "gemm_launches": gemm_n, "gemm_ms_total": gemm_ms,
                  "mfma_roofline": {"bound": "mfma", "achieved": gemm_flops / (gemm_ms / 1e3) / 1e12,
                                    "peak": 2500.0, "unit": "TFLOP/s",

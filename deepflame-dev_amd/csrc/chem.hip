@@ -13,6 +13,10 @@
 // fall-off [M]-dependence of k is omitted, an approximation the step control absorbs). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
 // mass fractions) by default.
 //
+// Scheduling: cells are launched in descending order of the integrator steps they needed in the
+// previous solve (counting sort, k_bin_*): a wave costs its slowest lane, and on the reference TGV
+// state natural order loads waves at 23% (mean / per-wave max); binned, k_chem drops 7.3 -> 1.9 ms.
+//
 // Layout: one cell per lane, 64-lane workgroups. Per-lane rate constants (they depend only on T,
 // which is frozen) and the per-lane S x S iteration matrix live in LDS as [entry][lane]
 // (bank-conflict free); state vectors live in registers (compile-time S). The mechanism arrays are
@@ -301,8 +305,78 @@ __device__ bool ros3(const ChemMech& m, const Lane<S>& L, double T, const double
   return true;
 }
 
+// ---- cost binning: a wave runs as long as its slowest lane, so cells are handed to the integrator
+// ordered by the integrator steps (accepted + rejected) they took in the previous solve, most
+// expensive first. Counting sort over NBIN buckets, stable inside a bucket (ascending cell index, so
+// the gathers of T, rho, Y stay mostly coalesced). Every cell's integration is independent of its
+// position, so the order changes timing only, never results.
+constexpr int NBIN = 32, BCB = 256, BCELLS = 4096;   // 4096 cells per binning block, 16 passes of 256
+__device__ inline int cost_bin(double st, double rj) {
+  const int c = (int)(st + rj);
+  return NBIN - 1 - (c < 0 ? NBIN - 1 : (c > NBIN - 1 ? NBIN - 1 : c));   // bucket 0 = most expensive
+}
+// per-block bucket counts, bucket-major [NBIN][nb]
+__global__ void __launch_bounds__(BCB) k_bin_count(long n, const double* __restrict__ stats, int nb, int* __restrict__ cnt) {
+  __shared__ int h[NBIN];
+  if (threadIdx.x < NBIN) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = 0; i < BCELLS / BCB; ++i) {
+    const long c = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
+    if (c < n) atomicAdd(&h[cost_bin(stats[c], stats[n + c])], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < NBIN) cnt[(long)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+// exclusive scan of the bucket-major counts in place (one workgroup, contiguous chunk per thread)
+__global__ void __launch_bounds__(1024) k_bin_scan(int total, int* __restrict__ cnt) {
+  __shared__ int part[1024];
+  const int per = (total + 1023) / 1024, b0 = threadIdx.x * per, b1 = min(b0 + per, total);
+  int a = 0;
+  for (int i = b0; i < b1; ++i) a += cnt[i];
+  part[threadIdx.x] = a;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {   // Hillis-Steele inclusive scan of the 1024 partials
+    const int v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  a = part[threadIdx.x] - a;
+  for (int i = b0; i < b1; ++i) { const int v = cnt[i]; cnt[i] = a; a += v; }
+}
+__global__ void __launch_bounds__(BCB) k_bin_scatter(long n, const double* __restrict__ stats, int nb,
+                                                     const int* __restrict__ off, int* __restrict__ perm) {
+  __shared__ int wc[BCB / 64][NBIN];
+  __shared__ int base[NBIN];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x < NBIN) base[threadIdx.x] = off[(long)threadIdx.x * nb + blockIdx.x];
+  for (int i = 0; i < BCELLS / BCB; ++i) {
+    const long c = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
+    const int k = c < n ? cost_bin(stats[c], stats[n + c]) : -1;
+    int rank = 0;
+    for (int b = 0; b < NBIN; ++b) {
+      const unsigned long long m = __ballot(k == b);
+      if (k == b) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[w][b] = __popcll(m);
+    }
+    __syncthreads();
+    if (k >= 0) {
+      int pos = base[k] + rank;
+      for (int v = 0; v < w; ++v) pos += wc[v][k];
+      perm[pos] = (int)c;
+    }
+    __syncthreads();
+    if (threadIdx.x < NBIN) {
+      int a = 0;
+      for (int v = 0; v < BCB / 64; ++v) a += wc[v][threadIdx.x];
+      base[threadIdx.x] += a;
+    }
+  }
+}
+
 template <int S>
-__global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double* __restrict__ Tf,
+__global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ perm, ChemMech m,
+                                                const double* __restrict__ Tf,
                                                 const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                 double dt, double rtol, double atol, double Tmin, int max_steps,
                                                 int method, double* __restrict__ RR, double* __restrict__ stats) {
@@ -313,8 +387,9 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double
   L.k0 = lds + (long)m.R * LANES;
   L.ikc = lds + 2L * m.R * LANES;
   L.A = lds + 3L * m.R * LANES;
-  const long c = (long)blockIdx.x * LANES + threadIdx.x;
-  if (c >= n) return;   // no block-level synchronisation below: early exit is safe
+  const long t = (long)blockIdx.x * LANES + threadIdx.x;
+  if (t >= n) return;   // no block-level synchronisation below: early exit is safe
+  const long c = perm ? perm[t] : t;
   const double T = Tf[c], rho = rhof[c];
   double Y0[S], y[S];
 #pragma unroll
@@ -391,7 +466,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, ChemMech m, const double
 #pragma clang diagnostic pop
 
 template <class G>
-__global__ void __launch_bounds__(LANES) k_chem_gen(long n, const double* __restrict__ Tf,
+__global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restrict__ perm, const double* __restrict__ Tf,
                                                     const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                     double dt, double rtol, double atol, double Tmin, int max_steps,
                                                     double* __restrict__ RR, double* __restrict__ stats) {
@@ -401,8 +476,9 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const double* __rest
                    c32 = 0.92076794298330791242156818474003e1;
   constexpr double m2 = 0.61697947043828245592553615689730e1, m3 = -0.42772256543218573326238373806514;
   constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
-  const long c = (long)blockIdx.x * LANES + threadIdx.x;
-  if (c >= n) return;
+  const long t = (long)blockIdx.x * LANES + threadIdx.x;
+  if (t >= n) return;
+  const long c = perm ? perm[t] : t;
   const double T = Tf[c], rho = rhof[c];
   double Y0[S], y[S], sc[S];
 #pragma unroll
@@ -526,21 +602,34 @@ void chem_solve(Ctx& x, double dt) {
     if (fp == ChemGen_burke9::FINGERPRINT) h.generated = 1;
     else if (fp == ChemGen_es80::FINGERPRINT) h.generated = 2;
   }
+  if (const char* e = std::getenv("DFMI_CHEM_BIN")) h.bin = std::atoi(e) != 0;
+  const int* perm = nullptr;
+  if (h.bin) {
+    KScope _ks(x, "k_bin");
+    const int nb = blocks_for(x.C, BCELLS);
+    if (h.perm.n < (size_t)x.C) h.perm.alloc(x.C);
+    if (h.bcnt.n < (size_t)nb * NBIN) h.bcnt.alloc((size_t)nb * NBIN);
+    hipLaunchKernelGGL(k_bin_count, dim3(nb), dim3(BCB), 0, x.stream, (long)x.C, (const double*)stats, nb, h.bcnt.p);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, x.stream, nb * NBIN, h.bcnt.p);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nb), dim3(BCB), 0, x.stream, (long)x.C, (const double*)stats, nb,
+                       (const int*)h.bcnt.p, h.perm.p);
+    perm = h.perm.p;
+  }
   if (h.generated) {
     KScope _ks(x, "k_chem");
     if (h.generated == 1)
-      hipLaunchKernelGGL(k_chem_gen<ChemGen_burke9>, g, dim3(LANES), 0, x.stream, (long)x.C, x.f("T"), x.f("rho"),
-                         x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+      hipLaunchKernelGGL(k_chem_gen<ChemGen_burke9>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
+                         x.f("rho"), x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
     else
-      hipLaunchKernelGGL(k_chem_gen<ChemGen_es80>, g, dim3(LANES), 0, x.stream, (long)x.C, x.f("T"), x.f("rho"),
-                         x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+      hipLaunchKernelGGL(k_chem_gen<ChemGen_es80>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
+                         x.f("rho"), x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
     DFMI_HIP(hipGetLastError());
     return;
   }
 #define CALL(NS)                                                                                                    \
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \
-    hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, m, x.f("T"), x.f("rho"), x.f("Y"), dt, \
+    hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, perm, m, x.f("T"), x.f("rho"), x.f("Y"), dt, \
                        h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats);                            \
   } while (0)
   switch (x.S) {

@@ -85,6 +85,8 @@ struct Chem {
   int max_steps = 100000;
   int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
   int generated = 0;            // last solve used a compiled-in mechanism (chem_gen_*.inc): 1 burke9, 2 es80
+  bool bin = true;              // order cells by the previous solve's step count (DFMI_CHEM_BIN=0: natural order)
+  DevBuf<int> perm, bcnt;       // cost-binned cell order; per-block bucket counts / offsets
   std::vector<int> h_idata, h_irs;
   std::vector<double> h_dd;
 };
