@@ -9,15 +9,23 @@ struct Ctx;
 struct AmgLevel {
   int n = 0, W = 0;
   DevBuf<int> col;                      // [W][n] (levels >= 1; level 0 uses the solver ELL)
-  DevBuf<double> val, D;                // per-solve coarse operator (levels >= 1)
   DevBuf<int> agg, mstart, members;     // fine -> coarse map, coarse -> fine member lists (to level+1)
   DevBuf<int> gstart, gsrc;             // Galerkin contribution lists building level+1
-  DevBuf<double> b, x, r, xo;           // work vectors
+  // per-solve operator (levels >= 1; level 0 in fp32 mode: a rounded copy of the solver ELL) and
+  // work vectors, in the preconditioner's precision (one of the two sets is allocated)
+  DevBuf<double> val, D, b, x, r, xo;
+  DevBuf<float> fval, fD, fb, fx, fr, fxo;
 };
 
+// Precision of the V-cycle. fp32 (default) keeps every level's operator and work vectors in single
+// precision (AmgX's mixed mode: preconditioner in float, Krylov iteration in double); the outer PCG
+// residuals, dot products and solution stay fp64, so the attainable accuracy is unchanged and only
+// the preconditioner's HBM traffic halves. DFMI_AMG_PREC=f64 keeps the whole hierarchy in double.
 struct Amg {
   bool ready = false;
+  bool fp32 = true;
   double omega = 0.85;
+  double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
   int coarsest = 4096;
   std::vector<AmgLevel> lv;

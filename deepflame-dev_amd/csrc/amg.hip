@@ -10,15 +10,22 @@
 // Per solve: Galerkin coarse operators P^T A P (piecewise-constant P) are summed on the device from
 // precomputed contribution lists in a fixed order -- deterministic, no atomics.
 // V-cycle: one weighted-Jacobi pre-sweep from zero (fused into the residual pass), restriction,
-// coarse correction, prolongation fused with one post-sweep; the coarsest level (<= 4096 cells) is
+// coarse correction scaled by an over-correction factor (1.35: piecewise-constant interpolation
+// under-corrects smooth errors; 28 instead of 32 PCG iterations per 2M-cell step), prolongation fused
+// with one post-sweep; the coarsest level (<= 4096 cells) is
 // smoothed by a fixed number of Jacobi sweeps inside one workgroup (LDS-resident vectors). All pieces
 // are linear and the pre/post sweeps are adjoint, so the preconditioner is symmetric (valid for CG).
+// Precision: by default the whole V-cycle runs in fp32 (operators rounded once per solve, work
+// vectors in float; AmgX's mixed-precision mode) -- it only preconditions, the PCG residuals, dot
+// products and solution stay fp64 -- which halves the preconditioner's bytes per iteration.
 #include "dfmi_ctx.h"
 #include "amg.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <numeric>
+#include <string>
+#include <type_traits>
 
 namespace dfmi {
 namespace {
@@ -28,10 +35,14 @@ constexpr int COARSEST = 1024;   // k_coarsest capacity (cells); also n * W <= L
 constexpr int CTPB = 1024;
 
 // ---------------------------------------------------------------- kernels
-// coarse values: out[s * nc + I] = sum of the fine sources listed for (slot s, cell I)
+// Value type T is the V-cycle precision (double, or float in the default mixed mode); TB the type
+// of a level's right-hand side (level 0: the PCG residual, always double); TO the type written out.
+
+// coarse values: out[s * nc + I] = sum (in double) of the fine sources listed for (slot s, cell I)
+template <class TF, class TC>
 __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, const int* __restrict__ gsrc,
-                           const double* __restrict__ fval, const double* __restrict__ fD, double* __restrict__ cval,
-                           double* __restrict__ cD) {
+                           const TF* __restrict__ fval, const TF* __restrict__ fD, TC* __restrict__ cval,
+                           TC* __restrict__ cD) {
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
   if (I >= nc) return;
   for (int s = 0; s < slots; ++s) {
@@ -39,63 +50,72 @@ __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, co
     double a = 0.0;
     for (long e = e0; e < e1; ++e) {
       const int src = gsrc[e];
-      a += src >= 0 ? fval[src] : fD[-src - 1];
+      a += src >= 0 ? (double)fval[src] : (double)fD[-src - 1];
     }
-    if (s < slots - 1) cval[(long)s * nc + I] = a;
-    else cD[I] = a;
+    if (s < slots - 1) cval[(long)s * nc + I] = (TC)a;
+    else cD[I] = (TC)a;
   }
+}
+
+// level-0 operator rounded to the V-cycle precision (once per solve)
+__global__ void k_round_f32(long n, const double* __restrict__ a, float* __restrict__ b) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = (float)a[i];
 }
 
 // x = omega b / D (first sweep from zero); r = b - A x   (columns >= n: other ranks, dropped)
-template <int WT>
+template <int WT, class T, class TB>
 __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __restrict__ col,
-                                                    const double* __restrict__ val, const double* __restrict__ D,
-                                                    const double* __restrict__ b, double omega,
-                                                    double* __restrict__ x, double* __restrict__ r) {
+                                                    const T* __restrict__ val, const T* __restrict__ D,
+                                                    const TB* __restrict__ b, T omega,
+                                                    T* __restrict__ x, T* __restrict__ r) {
   const int W = WT > 0 ? WT : W_;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
-  const double xc = omega * b[c] / D[c];
-  double y = D[c] * xc;
+  const T bc = (T)b[c];
+  const T xc = omega * bc / D[c];
+  T y = D[c] * xc;
 #pragma unroll
   for (int k = 0; k < W; ++k) {
     const int j = col[(long)k * n + c];
-    if (j < n) y += val[(long)k * n + c] * (omega * b[j] / D[j]);
+    if (j < n) y += val[(long)k * n + c] * (omega * (T)b[j] / D[j]);
   }
   x[c] = xc;
-  r[c] = b[c] - y;
+  r[c] = bc - y;
 }
 
+template <class T>
 __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
-                           const double* __restrict__ r, double* __restrict__ bc) {
+                           const T* __restrict__ r, T* __restrict__ bc) {
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
   if (I >= nc) return;
-  double a = 0.0;
+  T a = 0;
   for (int e = mstart[I]; e < mstart[I + 1]; ++e) a += r[members[e]];
   bc[I] = a;
 }
 
-// y = x + P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z)
-template <int WT>
+// y = x + s P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z,
+// formed in double from the values actually stored)
+template <int WT, class T, class TB, class TO>
 __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int* __restrict__ col,
-                                                        const double* __restrict__ val, const double* __restrict__ D,
-                                                        const double* __restrict__ b, const double* __restrict__ x,
-                                                        const int* __restrict__ agg, const double* __restrict__ xc,
-                                                        double omega, double* __restrict__ out, double* partial) {
+                                                        const T* __restrict__ val, const T* __restrict__ D,
+                                                        const TB* __restrict__ b, const T* __restrict__ x,
+                                                        const int* __restrict__ agg, const T* __restrict__ xc,
+                                                        T omega, T sc, TO* __restrict__ out, double* partial) {
   const int W = WT > 0 ? WT : W_;
   __shared__ double sh[TPB / 64];
   double acc = 0.0;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
-    const double yc = x[c] + xc[agg[c]];
-    double ay = D[c] * yc;
+    const T yc = x[c] + sc * xc[agg[c]];
+    T ay = D[c] * yc;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
       const int j = col[(long)k * n + c];
-      if (j < n) ay += val[(long)k * n + c] * (x[j] + xc[agg[j]]);
+      if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
     }
-    const double o = yc + omega * (b[c] - ay) / D[c];
+    const TB bc = b[c];
+    const TO o = (TO)(yc + omega * ((T)bc - ay) / D[c]);
     out[c] = o;
-    acc += b[c] * o;
+    acc += (double)bc * (double)o;
   }
   if (!partial) return;
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -125,22 +145,23 @@ __global__ void k_dot_partial(int n, const double* __restrict__ a, const double*
 // coarsest level: `sweeps` weighted-Jacobi sweeps from zero in one workgroup; operator and vectors
 // staged in LDS (n * W <= LDS_ENT), so the sweeps run at LDS latency
 constexpr int LDS_ENT = 6144;
+template <class T, class TB, class TO>
 __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __restrict__ col,
-                                                   const double* __restrict__ val, const double* __restrict__ D,
-                                                   const double* __restrict__ b, double omega, int sweeps,
-                                                   double* __restrict__ x) {
-  __shared__ double xa[COARSEST], xb[COARSEST];
-  __shared__ double sv[LDS_ENT];
+                                                   const T* __restrict__ val, const T* __restrict__ D,
+                                                   const TB* __restrict__ b, T omega, int sweeps,
+                                                   TO* __restrict__ x) {
+  __shared__ T xa[COARSEST], xb[COARSEST];
+  __shared__ T sv[LDS_ENT];
   __shared__ int sc[LDS_ENT];
-  __shared__ double sd[COARSEST], sb[COARSEST];
+  __shared__ T sd[COARSEST], sb[COARSEST];
   for (int e = threadIdx.x; e < n * W; e += CTPB) { sv[e] = val[e]; sc[e] = col[e]; }
-  for (int c = threadIdx.x; c < n; c += CTPB) { sd[c] = D[c]; sb[c] = b[c]; xa[c] = omega * b[c] / D[c]; }
+  for (int c = threadIdx.x; c < n; c += CTPB) { sd[c] = D[c]; sb[c] = (T)b[c]; xa[c] = omega * (T)b[c] / D[c]; }
   __syncthreads();
-  double* cur = xa;
-  double* nxt = xb;
+  T* cur = xa;
+  T* nxt = xb;
   for (int s = 1; s < sweeps; ++s) {
     for (int c = threadIdx.x; c < n; c += CTPB) {
-      double y = sd[c] * cur[c];
+      T y = sd[c] * cur[c];
       for (int k = 0; k < W; ++k) {
         const int j = sc[k * n + c];
         if (j < n) y += sv[k * n + c] * cur[j];
@@ -148,9 +169,9 @@ __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __re
       nxt[c] = cur[c] + omega * (sb[c] - y) / sd[c];
     }
     __syncthreads();
-    double* t = cur; cur = nxt; nxt = t;
+    T* t = cur; cur = nxt; nxt = t;
   }
-  for (int c = threadIdx.x; c < n; c += CTPB) x[c] = cur[c];
+  for (int c = threadIdx.x; c < n; c += CTPB) x[c] = (TO)cur[c];
 }
 
 // ---------------------------------------------------------------- host: hierarchy
@@ -297,9 +318,6 @@ void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLe
   c.n = nc;
   c.W = Wc;
   c.col.upload(ccol, st);
-  c.val.alloc((size_t)Wc * nc);
-  c.D.alloc(nc);
-  c.b.alloc(nc); c.x.alloc(nc); c.r.alloc(nc); c.xo.alloc(nc);
 }
 
 double env_d(const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; }
@@ -312,6 +330,11 @@ void amg_setup(Ctx& x) {
   a.omega = env_d("DFMI_AMG_OMEGA", 0.85);
   a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
   a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
+  a.overcorr = env_d("DFMI_AMG_OVERCORR", 1.35);
+  {
+    const char* pe = std::getenv("DFMI_AMG_PREC");
+    a.fp32 = !(pe && std::string(pe) == "f64");
+  }
   const int C = x.C;
   // level 0: the solver ELL (columns >= C are halo entries, dropped in the preconditioner)
   std::vector<int> col((size_t)x.ell.W * C);
@@ -360,7 +383,6 @@ void amg_setup(Ctx& x) {
   a.lv.emplace_back();
   a.lv[0].n = C;
   a.lv[0].W = x.ell.W;
-  a.lv[0].x.alloc(C); a.lv[0].r.alloc(C); a.lv[0].xo.alloc(C);
   std::vector<int> fcol = col;
   auto too_big = [&](const AmgLevel& l) { return l.n > a.coarsest || (size_t)l.n * l.W > 6144; };
   while (too_big(a.lv.back())) {
@@ -376,80 +398,136 @@ void amg_setup(Ctx& x) {
     if (stalled) break;
   }
   DFMI_CHECK(!too_big(a.lv.back()) || a.lv.back().n <= 8, "AMG coarsening stalled above the coarsest-level capacity");
+  if (a.lv.size() == 1) a.fp32 = false;   // a single level writes z directly: keep it in double
+  for (size_t l = 0; l < a.lv.size(); ++l) {
+    AmgLevel& v = a.lv[l];
+    const size_t nv = v.n, ne = (size_t)v.W * v.n;
+    if (a.fp32) {
+      v.fval.alloc(ne); v.fD.alloc(nv);
+      if (l > 0) v.fb.alloc(nv);
+      v.fx.alloc(nv); v.fr.alloc(nv); v.fxo.alloc(nv);
+    } else {
+      if (l > 0) { v.val.alloc(ne); v.D.alloc(nv); v.b.alloc(nv); }
+      v.x.alloc(nv); v.r.alloc(nv); v.xo.alloc(nv);
+    }
+  }
   a.ready = true;
 }
 
 // Per solve: coarse operators from the level-0 values (val0 [W][C], D0 = diag + internalCoeffs).
 void amg_galerkin(Ctx& x, const double* val0, const double* D0) {
   Amg& a = x.amg;
-  const double* fv = val0;
-  const double* fD = D0;
+  if (a.fp32) {   // the level-0 smoother reads a single-precision copy of the solver's ELL operator
+    AmgLevel& l0 = a.lv[0];
+    KScope _ks(x, "k_round_f32");
+    hipLaunchKernelGGL(k_round_f32, dim3(2048), dim3(TPB), 0, x.stream, (long)l0.W * l0.n, val0, l0.fval.p);
+    hipLaunchKernelGGL(k_round_f32, dim3(512), dim3(TPB), 0, x.stream, (long)l0.n, D0, l0.fD.p);
+    DFMI_HIP(hipGetLastError());
+  }
   for (size_t l = 0; l + 1 < a.lv.size(); ++l) {
     AmgLevel& f = a.lv[l];
     AmgLevel& c = a.lv[l + 1];
     KScope _ks(x, "k_galerkin");
-    hipLaunchKernelGGL(k_galerkin, dim3(blocks_for(c.n, TPB)), dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p,
-                       f.gsrc.p, fv, fD, c.val.p, c.D.p);
+    const dim3 g(blocks_for(c.n, TPB));
+    if (!a.fp32)
+      hipLaunchKernelGGL((k_galerkin<double, double>), g, dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p, f.gsrc.p,
+                         l == 0 ? val0 : (const double*)f.val.p, l == 0 ? D0 : (const double*)f.D.p, c.val.p, c.D.p);
+    else if (l == 0)   // coarse sums from the fp64 fine values, rounded once
+      hipLaunchKernelGGL((k_galerkin<double, float>), g, dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p, f.gsrc.p,
+                         val0, D0, c.fval.p, c.fD.p);
+    else
+      hipLaunchKernelGGL((k_galerkin<float, float>), g, dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p, f.gsrc.p,
+                         (const float*)f.fval.p, (const float*)f.fD.p, c.fval.p, c.fD.p);
     DFMI_HIP(hipGetLastError());
-    fv = c.val.p;
-    fD = c.D.p;
   }
 }
 
-// z = M^-1 r; block partials of r.z (one per block of the level-0 grid) into `partial`
-void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-               double* partial, int nblk) {
+namespace {
+
+template <class K0, class K6, class... A>
+void launch_w(int W, dim3 g, hipStream_t st, K0 k0, K6 k6, A... a) {
+  if (W == 6) hipLaunchKernelGGL(k6, g, dim3(TPB), 0, st, a...);
+  else hipLaunchKernelGGL(k0, g, dim3(TPB), 0, st, a...);
+}
+
+// z = M^-1 r in precision T; block partials of r.z (one per block of the level-0 grid) into `partial`
+template <class T>
+void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
+             double* partial, int nblk) {
+  constexpr bool F = std::is_same<T, float>::value;
   Amg& a = x.amg;
   const int L = (int)a.lv.size();
-  const double om = a.omega;
-  auto VAL = [&](int l) { return l == 0 ? val0 : (const double*)a.lv[l].val.p; };
-  auto DD = [&](int l) { return l == 0 ? D0 : (const double*)a.lv[l].D.p; };
+  const T om = (T)a.omega, sc = (T)a.overcorr;
+  auto VAL = [&](int l) -> const T* {
+    if constexpr (F) return a.lv[l].fval.p; else return l == 0 ? val0 : (const double*)a.lv[l].val.p;
+  };
+  auto DD = [&](int l) -> const T* {
+    if constexpr (F) return a.lv[l].fD.p; else return l == 0 ? D0 : (const double*)a.lv[l].D.p;
+  };
   auto COL = [&](int l) { return l == 0 ? col0 : (const int*)a.lv[l].col.p; };
-  auto B = [&](int l) { return l == 0 ? r : (const double*)a.lv[l].b.p; };
-  // down
+  auto BV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fb.p; else return a.lv[l].b.p; };
+  auto XV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fx.p; else return a.lv[l].x.p; };
+  auto RV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fr.p; else return a.lv[l].r.p; };
+  auto XO = [&](int l) -> T* { if constexpr (F) return a.lv[l].fxo.p; else return a.lv[l].xo.p; };
+  // down: smooth from zero + residual, restrict
   for (int l = 0; l + 1 < L; ++l) {
     AmgLevel& f = a.lv[l];
+    const dim3 g(blocks_for(f.n, TPB));
     {
       KScope _ks(x, "k_smooth_res");
-      if (f.W == 6)
-        hipLaunchKernelGGL(k_smooth_res<6>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
-                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
+      if (l == 0)
+        launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
+                 DD(0), r, om, XV(0), RV(0));
       else
-        hipLaunchKernelGGL(k_smooth_res<0>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, f.W, COL(l),
-                           VAL(l), DD(l), B(l), om, f.x.p, f.r.p);
+        launch_w(f.W, g, x.stream, k_smooth_res<0, T, T>, k_smooth_res<6, T, T>, f.n, f.W, COL(l), VAL(l), DD(l),
+                 (const T*)BV(l), om, XV(l), RV(l));
     }
     {
       KScope _ks(x, "k_restrict");
-      hipLaunchKernelGGL(k_restrict, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
-                         f.mstart.p, f.members.p, f.r.p, a.lv[l + 1].b.p);
+      hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
+                         f.mstart.p, f.members.p, (const T*)RV(l), BV(l + 1));
     }
   }
   // coarsest
   {
     AmgLevel& c = a.lv[L - 1];
     KScope _ks(x, "k_coarsest");
-    hipLaunchKernelGGL(k_coarsest, dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, COL(L - 1), VAL(L - 1), DD(L - 1),
-                       B(L - 1), om, a.coarse_sweeps, L == 1 ? z : c.x.p);
+    if (L > 1)
+      hipLaunchKernelGGL((k_coarsest<T, T, T>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, COL(L - 1), VAL(L - 1),
+                         DD(L - 1), (const T*)BV(L - 1), om, a.coarse_sweeps, XV(L - 1));
+    else if constexpr (!F)   // single level (double only): solve straight into z
+      hipLaunchKernelGGL((k_coarsest<double, double, double>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, col0, val0,
+                         D0, r, om, a.coarse_sweeps, z);
   }
   if (L == 1) {
     KScope _ks(x, "k_dot_partial");
     hipLaunchKernelGGL(k_dot_partial, dim3(nblk), dim3(TPB), 0, x.stream, x.C, r, (const double*)z, partial);
   }
-  // up
+  // up: prolongate the coarse correction + one smoothing sweep
   for (int l = L - 2; l >= 0; --l) {
     AmgLevel& f = a.lv[l];
-    double* out = l == 0 ? z : f.xo.p;
     KScope _ks(x, "k_prolong_smooth");
-    const dim3 grid = l == 0 ? dim3(nblk) : dim3(blocks_for(f.n, TPB));
-    if (f.W == 6)
-      hipLaunchKernelGGL(k_prolong_smooth<6>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
-                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
-    else
-      hipLaunchKernelGGL(k_prolong_smooth<0>, grid, dim3(TPB), 0, x.stream, f.n, f.W, COL(l), VAL(l), DD(l), B(l),
-                         f.x.p, f.agg.p, a.lv[l + 1].x.p, om, out, l == 0 ? partial : nullptr);
-    if (l > 0) std::swap(f.x, f.xo);   // the corrected x of this level feeds the next finer prolongation
+    if (l == 0) {
+      launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
+               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, (const T*)XV(1), om, sc, z,
+               partial);
+    } else {
+      launch_w(f.W, dim3(blocks_for(f.n, TPB)), x.stream, k_prolong_smooth<0, T, T, T>, k_prolong_smooth<6, T, T, T>,
+               f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), (const T*)XV(l), (const int*)f.agg.p,
+               (const T*)XV(l + 1), om, sc, XO(l), (double*)nullptr);
+      // the corrected x of this level feeds the next finer prolongation
+      if constexpr (F) std::swap(f.fx, f.fxo); else std::swap(f.x, f.xo);
+    }
   }
   DFMI_HIP(hipGetLastError());
+}
+
+}  // namespace
+
+void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
+               double* partial, int nblk) {
+  if (x.amg.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk);
+  else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk);
 }
 
 }  // namespace dfmi

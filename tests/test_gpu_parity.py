@@ -207,11 +207,14 @@ def test_full_outer_iteration(periodic):
     ctx.set_solver("p", 1000, 1e-5)
 
 
+@pytest.mark.parametrize("prec", ["f32", "f64"])
 @pytest.mark.parametrize("coarsest", ["16", "4096"])
-def test_amg_pcg_full_step(coarsest, monkeypatch):
+def test_amg_pcg_full_step(coarsest, prec, monkeypatch):
     """AMG-preconditioned p solves (multi-level hierarchy forced on a small mesh) reach the oracle's
-    exact solution; AMG needs fewer iterations than Jacobi."""
+    exact solution with the V-cycle in fp32 (default) or fp64 -- the preconditioner's precision
+    changes the iteration count, not the attainable accuracy; AMG needs fewer iterations than Jacobi."""
     monkeypatch.setenv("DFMI_AMG_COARSEST", coarsest)
+    monkeypatch.setenv("DFMI_AMG_PREC", prec)
     ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
     for e in ("U", "Y", "E"):
         ctx.set_solver(e, 300, 1e-15, 1e-300)
