@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+PMC_FILE = "r01_pmc_traffic.json"
 
 MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species table made by dfmi.transport_fit
     "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
@@ -34,25 +35,32 @@ MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species 
 }
 
 
-def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int) -> float:
-    """Bytes a kernel must move at minimum (each input read once, each output written once;
-    fp64 values, int32 indices). DESIGN.md 'Kernels' lists the per-unit figures."""
+def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None) -> float:
+    """Bytes one unit of a kernel's work must move at minimum (each input read once, each output
+    written once; fp64 values, int32 indices). Units: k_y_assemble_ell one launch (all S-1 solved
+    species); k_cg_spmv one active PCG iteration; k_bcg_spmv one SpMV of one active system.
+    Bc = coupled boundary slots (cyclic / processor: one matrix entry each). DESIGN.md 5 lists them."""
     Sa = S - 1                                     # solved species (inert excluded)
-    if kernel == "k_y_assemble":
-        # cells: Y, rhoD, RR in (Sa each), rho, rho_old, V in, diag/source out (Sa each)
-        # faces: phi, phiUc, w, deltaCoeffs, magSf, owner, neighbour in; lower/upper out (Sa each)
-        return C * (8 * 5 * Sa + 24) + F * (5 * 8 + 8 + 16 * Sa) + B * (8 * 8 + 16 * Sa)
+    Bc = B if Bc is None else Bc
+    if kernel == "k_y_assemble_ell" or kernel == "k_y_assemble":
+        # SURVEY.md 8(d): fused Y-species assembly (ddt + div phi + div phiUc + lap rhoD + RR),
+        # 64 F + 64 C bytes per solved species
+        return Sa * (64.0 * F + 64.0 * C)
     if kernel == "k_cg_spmv":
         # fused PCG step p = z + beta p_old; q = A p: cells z, p_old, dS in, p, q out (40 B);
         # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
         # ELL gather stores the same 2 x 12 B per face from the two cells' sides); coupled slots 12 B
-        return C * 40 + F * 24 + B * 12
+        return C * 40.0 + F * 24.0 + Bc * 12.0
     if kernel == "k_bcg_spmv":
-        return C * 24 + F * 24 + B * 16
+        # out = A in (+ dot with r0 or s): cells dS, in, out, dot partner (32 B); matrix as above
+        return C * 32.0 + F * 24.0 + Bc * 12.0
     if kernel == "k_thermo_cells":
         # T, he, p in; Y in (S); T, psi, rho, mu, alpha out; rhoD, hai out (S each)
-        return C * 8 * (3 + S + 5 + 2 * S)
+        return C * 8.0 * (3 + S + 5 + 2 * S)
     raise KeyError(kernel)
+
+
+ROOF_KERNELS = ("k_bcg_spmv", "k_cg_spmv", "k_y_assemble_ell")
 
 
 def parse():
@@ -67,7 +75,8 @@ def parse():
                     help="initial state: the reference's own 64^3 TGV 0/ fields tiled (BASELINE config 3), or the "
                          "analytic TGV")
     ap.add_argument("--dt", type=float, default=1e-6)
-    ap.add_argument("--kernel", default="k_cg_spmv", help="kernel whose roofline is reported")
+    ap.add_argument("--kernel", default="auto",
+                    help="kernel of the primary roofline entry (auto: the HBM-bound kernel with the most time)")
     ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
                     help="chemistry source: stiff ODE integration per cell (BASELINE config 3), the DF-ODENet "
                          "surrogate (MFMA fp16, config 4's path on the H2 nets) or off")
@@ -236,8 +245,10 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    extra = {"ode": ",k_chem,k_bin", "dnn": ",k_mlp_gemm", "off": ""}[args.chem]
-    ctx.kernel_timer(args.kernel + extra)
+    extra = {"ode": ["k_chem", "k_bin"], "dnn": ["k_mlp_gemm"], "off": []}[args.chem]
+    ctx.kernel_timer(",".join(ROOF_KERNELS + tuple(extra)))
+    for e in ("U", "Y", "E", "p"):
+        ctx.solver_work(e, reset=True)
     if args.chem == "dnn":
         ctx.dnn_stats()
     t0 = time.perf_counter()
@@ -247,7 +258,8 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    k_ms, k_n = ctx.kernel_time(args.kernel)
+    ktime = {k: ctx.kernel_time(k) for k in ROOF_KERNELS}
+    work = {e: ctx.solver_work(e) for e in ("U", "Y", "E", "p")}
     chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
     bin_ms, _ = ctx.kernel_time("k_bin") if args.chem == "ode" else (0.0, 0)
     gemm_ms, gemm_n = ctx.kernel_time("k_mlp_gemm") if args.chem == "dnn" else (0.0, 0)
@@ -264,18 +276,31 @@ def main():
 
     cells_total = m.n_cells * world
     value = cells_total * args.steps / el
-    kbytes = algorithmic_bytes(args.kernel, m.n_cells, m.n_faces, m.n_boundary_slots, table.S)
-    k_avg_s = (k_ms / 1e3 / k_n) if k_n else float("nan")
-    achieved = kbytes / k_avg_s / 1e9 if k_n else None
     # HBM bytes per launch from the PMC passes committed under profiles/ (scripts/pmc_traffic.sh +
     # scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) KB, gfx950 correction), same workload
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if os.path.exists(pmc) and n == 128 and world == 1:
-        tab = json.load(open(pmc))
-        for key, v in tab.items():
-            if key.split("::")[-1].split("<")[0] == args.kernel:
-                traffic = v["hbm_bytes_median"]
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)
+    if os.path.exists(pmc_path) and n == 128 and world == 1:
+        for key, v in json.load(open(pmc_path)).items():
+            pmc[key.split("::")[-1].split("<")[0]] = v
+    Bc = m.n_coupled_slots
+    units = {"k_bcg_spmv": 2.0 * (work["U"] + work["Y"] + work["E"]), "k_cg_spmv": work["p"],
+             "k_y_assemble_ell": float(ktime["k_y_assemble_ell"][1])}
+    roofs = {}
+    for k in ROOF_KERNELS:
+        ms, nl = ktime[k]
+        if not nl or ms <= 0:
+            continue
+        per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc)
+        total_bytes = per_unit * units[k]
+        achieved = total_bytes / (ms / 1e3) / 1e9
+        tr = pmc.get(k)
+        roofs[k] = {"kernel": k, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": tr["hbm_bytes_mean"] if tr else None,
+                    "algorithmic_bytes": total_bytes / nl, "launches": nl, "work_units": units[k],
+                    "bytes_per_unit": per_unit, "avg_us": ms * 1e3 / nl, "total_ms": ms}
+    primary = args.kernel if args.kernel != "auto" else max(roofs, key=lambda k: roofs[k]["total_ms"])
     out = {
         "metric": "cell-updates/s (dfLowMachFoam outer iter)",
         "value": value,
@@ -297,10 +322,13 @@ def main():
                    "cells_per_gpu": m.n_cells, "species": table.S,
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
-        "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                     "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
-                     "algorithmic_bytes": kbytes, "launches": k_n, "avg_us": k_avg_s * 1e6},
+        "roofline": dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "
+                         "WRITE_SIZE passes, mean per dispatch, gfx950 read correction)",
+                         note="achieved = algorithmic bytes of the work done (active systems/iterations) / "
+                              "summed HIP-event kernel time over the timed steps; algorithmic_bytes and traffic "
+                              "are per launch"),
+        "rooflines": {k: {kk: v[kk] for kk in ("achieved", "frac", "traffic", "algorithmic_bytes", "avg_us",
+                                               "launches")} for k, v in roofs.items()},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "amg_levels": ctx.amg_info(),
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",

@@ -33,8 +33,9 @@ struct Amg {
 
 void amg_setup(Ctx& x);
 void amg_galerkin(Ctx& x, const double* val0, const double* D0);
-// z = M^-1 r with block partials of r.z written to partial[0 .. nblk) (grid of `nblk` blocks)
+// z = M^-1 r with block partials of r.z written to partial[0 .. nblk) (grid of `nblk` blocks); every
+// kernel returns at once when *active == 0 (a converged solve; nullptr: always run)
 void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-               double* partial, int nblk);
+               double* partial, int nblk, const double* active = nullptr);
 
 }  // namespace dfmi

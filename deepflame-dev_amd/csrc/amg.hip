@@ -67,10 +67,10 @@ template <int WT, class T, class TB>
 __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __restrict__ col,
                                                     const T* __restrict__ val, const T* __restrict__ D,
                                                     const TB* __restrict__ b, T omega,
-                                                    T* __restrict__ x, T* __restrict__ r) {
+                                                    T* __restrict__ x, T* __restrict__ r, const double* act) {
   const int W = WT > 0 ? WT : W_;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
+  if (c >= n || (act && *act == 0.0)) return;
   const T bc = (T)b[c];
   const T xc = omega * bc / D[c];
   T y = D[c] * xc;
@@ -85,9 +85,9 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __
 
 template <class T>
 __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
-                           const T* __restrict__ r, T* __restrict__ bc) {
+                           const T* __restrict__ r, T* __restrict__ bc, const double* act) {
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I >= nc) return;
+  if (I >= nc || (act && *act == 0.0)) return;
   T a = 0;
   for (int e = mstart[I]; e < mstart[I + 1]; ++e) a += r[members[e]];
   bc[I] = a;
@@ -100,8 +100,10 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int
                                                         const T* __restrict__ val, const T* __restrict__ D,
                                                         const TB* __restrict__ b, const T* __restrict__ x,
                                                         const int* __restrict__ agg, const T* __restrict__ xc,
-                                                        T omega, T sc, TO* __restrict__ out, double* partial) {
+                                                        T omega, T sc, TO* __restrict__ out, double* partial,
+                                                        const double* act) {
   const int W = WT > 0 ? WT : W_;
+  if (act && *act == 0.0) return;   // uniform: no barrier below is reached by part of the block
   __shared__ double sh[TPB / 64];
   double acc = 0.0;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
@@ -149,7 +151,8 @@ template <class T, class TB, class TO>
 __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __restrict__ col,
                                                    const T* __restrict__ val, const T* __restrict__ D,
                                                    const TB* __restrict__ b, T omega, int sweeps,
-                                                   TO* __restrict__ x) {
+                                                   TO* __restrict__ x, const double* act) {
+  if (act && *act == 0.0) return;
   __shared__ T xa[COARSEST], xb[COARSEST];
   __shared__ T sv[LDS_ENT];
   __shared__ int sc[LDS_ENT];
@@ -453,7 +456,7 @@ void launch_w(int W, dim3 g, hipStream_t st, K0 k0, K6 k6, A... a) {
 // z = M^-1 r in precision T; block partials of r.z (one per block of the level-0 grid) into `partial`
 template <class T>
 void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-             double* partial, int nblk) {
+             double* partial, int nblk, const double* act) {
   constexpr bool F = std::is_same<T, float>::value;
   Amg& a = x.amg;
   const int L = (int)a.lv.size();
@@ -477,15 +480,15 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
       KScope _ks(x, "k_smooth_res");
       if (l == 0)
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
-                 DD(0), r, om, XV(0), RV(0));
+                 DD(0), r, om, XV(0), RV(0), act);
       else
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, T>, k_smooth_res<6, T, T>, f.n, f.W, COL(l), VAL(l), DD(l),
-                 (const T*)BV(l), om, XV(l), RV(l));
+                 (const T*)BV(l), om, XV(l), RV(l), act);
     }
     {
       KScope _ks(x, "k_restrict");
       hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
-                         f.mstart.p, f.members.p, (const T*)RV(l), BV(l + 1));
+                         f.mstart.p, f.members.p, (const T*)RV(l), BV(l + 1), act);
     }
   }
   // coarsest
@@ -494,10 +497,10 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
     KScope _ks(x, "k_coarsest");
     if (L > 1)
       hipLaunchKernelGGL((k_coarsest<T, T, T>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, COL(L - 1), VAL(L - 1),
-                         DD(L - 1), (const T*)BV(L - 1), om, a.coarse_sweeps, XV(L - 1));
+                         DD(L - 1), (const T*)BV(L - 1), om, a.coarse_sweeps, XV(L - 1), act);
     else if constexpr (!F)   // single level (double only): solve straight into z
       hipLaunchKernelGGL((k_coarsest<double, double, double>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, col0, val0,
-                         D0, r, om, a.coarse_sweeps, z);
+                         D0, r, om, a.coarse_sweeps, z, act);
   }
   if (L == 1) {
     KScope _ks(x, "k_dot_partial");
@@ -510,11 +513,11 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
     if (l == 0) {
       launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
                f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, (const T*)XV(1), om, sc, z,
-               partial);
+               partial, act);
     } else {
       launch_w(f.W, dim3(blocks_for(f.n, TPB)), x.stream, k_prolong_smooth<0, T, T, T>, k_prolong_smooth<6, T, T, T>,
                f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), (const T*)XV(l), (const int*)f.agg.p,
-               (const T*)XV(l + 1), om, sc, XO(l), (double*)nullptr);
+               (const T*)XV(l + 1), om, sc, XO(l), (double*)nullptr, act);
       // the corrected x of this level feeds the next finer prolongation
       if constexpr (F) std::swap(f.fx, f.fxo); else std::swap(f.x, f.xo);
     }
@@ -525,9 +528,9 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
 }  // namespace
 
 void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-               double* partial, int nblk) {
-  if (x.amg.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk);
-  else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk);
+               double* partial, int nblk, const double* active) {
+  if (x.amg.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active);
+  else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active);
 }
 
 }  // namespace dfmi

@@ -633,11 +633,17 @@ int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
 
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel) {
   return guard([&] {
-    auto it = ctx->x.last_stats.find(eqn);
-    DFMI_CHECK(it != ctx->x.last_stats.end(), std::string("no solve recorded for ") + eqn);
-    if (iters) *iters = it->second.iters;
-    if (res0) *res0 = it->second.res0;
-    if (rel) *rel = it->second.res;
+    const SolveStats st = solve_stats(ctx->x, eqn);
+    if (iters) *iters = st.iters;
+    if (res0) *res0 = st.res0;
+    if (rel) *rel = st.res;
+  });
+}
+
+int dfmi_solver_work(dfmi_ctx* ctx, const char* eqn, double* iters, int reset) {
+  return guard([&] {
+    const double v = solver_work(ctx->x, eqn, reset != 0);
+    if (iters) *iters = v;
   });
 }
 

@@ -57,6 +57,23 @@ template <class T> struct DevBuf {
   operator T*() const { return p; }
 };
 
+// Owning pinned host allocation (device-visible; async copies into it need no staging).
+template <class T> struct PinnedBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() { release(); }
+  void release() { if (p) { (void)hipHostFree(p); p = nullptr; n = 0; } }
+  void ensure(size_t count) {
+    if (count <= n) return;
+    release();
+    DFMI_HIP(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+    n = count;
+  }
+};
+
 inline int blocks_for(long n, int tpb) { return (int)((n + tpb - 1) / tpb); }
 
 }  // namespace dfmi

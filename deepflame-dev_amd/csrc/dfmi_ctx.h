@@ -131,7 +131,6 @@ struct Ctx {
   // matrices
   Matrix mU, mY, mE, mP;
   std::map<std::string, SolverCfg> solver;
-  std::map<std::string, SolveStats> last_stats;
   Thermo thermo;
   // scratch
   DevBuf<double> scratch;
@@ -154,8 +153,14 @@ struct Ctx {
   struct SolverWs {
     DevBuf<double> buf, scal, red_local, red_all;
     DevBuf<int> sysmap;
-    std::vector<double> hscal;
+    PinnedBuf<double> poll;          // two convergence snapshots (linsolve.hip: Poller)
+    hipEvent_t ev[2] = {nullptr, nullptr};
   } ws;
+  // final solver state of the last solve of each equation, copied asynchronously at the end of the
+  // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
+  struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
+  std::map<std::string, StatSnap> stat_snap;
+  DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
   ~Ctx();
   int n_corr = 2;
@@ -231,6 +236,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
                           long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
                           double* xsol, long xstride, const SolverCfg& cfg, bool prebuilt = false);
 void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs);
+// iterations / initial and final relative residual of the last solve of `eqn` (synchronises)
+SolveStats solve_stats(Ctx& x, const std::string& eqn);
+// system-iterations of the solves of `eqn` since the last reset (synchronises)
+double solver_work(Ctx& x, const std::string& eqn, bool reset);
 SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
                      const double* source, const double* ic, const double* bc, const char* type_field, double* xsol,
                      double* bxsol, const SolverCfg& cfg);

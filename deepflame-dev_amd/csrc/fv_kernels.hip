@@ -75,6 +75,17 @@ __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const do
   }
 }
 
+// ------------------------------------------------------------------ old <- new (preTimeStep)
+// every pair in one launch (grid.y = pair) instead of one copy launch per field
+constexpr int MAXCOPY = 12;
+struct CopyList { const double* src[MAXCOPY]; double* dst[MAXCOPY]; long n[MAXCOPY]; };
+__global__ void k_copy_multi(CopyList L) {
+  const int j = blockIdx.y;
+  const double* __restrict__ a = L.src[j];
+  double* __restrict__ b = L.dst[j];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < L.n[j]; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
 // ------------------------------------------------------------------ rhoEqn (dfRhoEqn.cu:41-92)
 __global__ void k_rho(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ rho_old,
                       const double* __restrict__ phi, const double* __restrict__ bphi, double* __restrict__ rho,
@@ -827,10 +838,17 @@ void copy_old(Ctx& x) {   // dfMatrixDataBase::preTimeStep (dfMatrixDataBase.cu:
   const char* pairs[][2] = {{"rho_old", "rho"}, {"boundary_rho_old", "boundary_rho"}, {"phi_old", "phi"},
                             {"boundary_phi_old", "boundary_phi"}, {"U_old", "U"}, {"boundary_U_old", "boundary_U"},
                             {"K_old", "K"}, {"p_old", "p"}, {"boundary_p_old", "boundary_p"}};
+  CopyList L{};
+  int k = 0;
   for (auto& pr : pairs) {
     Field& dst = x.fields.at(pr[0]);
-    DFMI_HIP(hipMemcpyAsync(dst.buf.p, x.f(pr[1]), dst.buf.n * sizeof(double), hipMemcpyDeviceToDevice, x.stream));
+    if (dst.buf.n == 0) continue;
+    L.src[k] = x.f(pr[1]); L.dst[k] = dst.buf.p; L.n[k] = (long)dst.buf.n; ++k;
   }
+  static_assert(sizeof(pairs) / sizeof(pairs[0]) <= MAXCOPY, "CopyList capacity");
+  KScope _ks(x, "k_copy_multi");
+  if (k) hipLaunchKernelGGL(k_copy_multi, dim3(1024, k), dim3(TPB), 0, x.stream, L);
+  DFMI_HIP(hipGetLastError());
 }
 
 void rho_process(Ctx& x, bool write_matrix) {

@@ -131,7 +131,11 @@ struct Halo {
 };
 
 void halo_destroy(Halo* h) { delete h; }
-Ctx::~Ctx() { halo_destroy(halo); halo = nullptr; }
+Ctx::~Ctx() {
+  halo_destroy(halo);
+  halo = nullptr;
+  for (auto& e : ws.ev) if (e) (void)hipEventDestroy(e);
+}
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }
 

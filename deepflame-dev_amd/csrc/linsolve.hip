@@ -181,6 +181,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_p(long C, long Ce, int it, int max_
                                                Red red, double* scal, BV b) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
+  if (it > 0 && st[6] == 0.0) return;   // stopped earlier (uniform per block)
   double v[2];
   red_sum<2>(red, s, v);
   const double res = sqrt(v[0]), rho = v[1];
@@ -295,6 +296,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
                                                  double abs_tol, Red red_rz, Red red_rr, double* scal, CV v,
                                                  const double* __restrict__ pold, double* __restrict__ pnew,
                                                  double* partial) {
+  if (it > 0 && scal[6] == 0.0) return;   // stopped earlier
   double a[1], b[1];
   red_sum<1>(red_rz, 0, a);
   red_sum<1>(red_rr, 0, b);
@@ -438,6 +440,64 @@ void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce) {
   halo_update(x, it.data(), (int)it.size());
 }
 
+// Convergence polling without draining the stream: every `check` iterations the solver state is
+// copied into pinned host memory behind an event, and the host reads the snapshot of the PREVIOUS
+// check -- the GPU is already running the next batch by then (systems that converged turn every
+// kernel into an early return), so the queue never empties inside a solve. The decision is a pure
+// function of the globally reduced scalars, identical on every rank.
+struct Poller {
+  Ctx& x;
+  const double* scal;
+  int nsys, slot = 0, pending = -1;
+  Poller(Ctx& c, const double* s, int n) : x(c), scal(s), nsys(n) {
+    x.ws.poll.ensure((size_t)2 * n * NSCAL);
+    for (auto& e : x.ws.ev)
+      if (!e) DFMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // snapshot now; true when the previous snapshot shows every system stopped
+  bool snapshot_and_test() {
+    double* dst = x.ws.poll.p + (size_t)slot * nsys * NSCAL;
+    DFMI_HIP(hipMemcpyAsync(dst, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+    DFMI_HIP(hipEventRecord(x.ws.ev[slot], x.stream));
+    bool done = false;
+    if (pending >= 0) {
+      DFMI_HIP(hipEventSynchronize(x.ws.ev[pending]));
+      const double* h = x.ws.poll.p + (size_t)pending * nsys * NSCAL;
+      done = true;
+      for (int s = 0; s < nsys; ++s) done = done && h[s * NSCAL + 6] == 0.0;
+    }
+    pending = slot;
+    slot ^= 1;
+    return done;
+  }
+};
+
+int work_slot(const std::string& eqn) {
+  if (eqn == "U") return 0;
+  if (eqn == "Y") return 1;
+  if (eqn == "E") return 2;
+  if (eqn == "p") return 3;
+  throw Error("dfmi: unknown equation '" + eqn + "'");
+}
+
+__global__ void k_accum_iters(const double* scal, int nsys, double* acc) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0;
+  for (int s = 0; s < nsys; ++s) a += scal[s * NSCAL + 7];
+  *acc += a;
+}
+
+// final state of the solve, copied for dfmi_solver_stats without waiting; iterations summed into
+// the equation's work counter on the device
+void record_stats(Ctx& x, const char* eqn, const double* scal, int nsys) {
+  if (x.work.n == 0) { x.work.alloc(4); x.work.zero(x.stream); }
+  hipLaunchKernelGGL(k_accum_iters, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.work.p + work_slot(eqn));
+  auto& sn = x.stat_snap[eqn];
+  sn.h.ensure((size_t)nsys * NSCAL);
+  sn.nsys = nsys;
+  DFMI_HIP(hipMemcpyAsync(sn.h.p, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+}
+
 }  // namespace
 
 // BiCGStab workspace: 11 vectors of nsys * (C + H), then the ELL values [nsys][W][C], then partials.
@@ -453,6 +513,33 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   *dS = x.ws.buf.p;
   *rhs = x.ws.buf.p + N;
   *val = x.ws.buf.p + 11 * N;
+}
+
+double solver_work(Ctx& x, const std::string& eqn, bool reset) {
+  const int k = work_slot(eqn);
+  if (x.work.n == 0) return 0.0;
+  double v = 0.0;
+  DFMI_HIP(hipMemcpyAsync(&v, x.work.p + k, sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  if (reset) {
+    DFMI_HIP(hipMemsetAsync(x.work.p + k, 0, sizeof(double), x.stream));
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  }
+  return v;
+}
+
+SolveStats solve_stats(Ctx& x, const std::string& eqn) {
+  auto it = x.stat_snap.find(eqn);
+  DFMI_CHECK(it != x.stat_snap.end(), "no solve recorded for " + eqn);
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  SolveStats st;
+  for (int s = 0; s < it->second.nsys; ++s) {   // worst system
+    const double* h = it->second.h.p + s * NSCAL;
+    st.iters = std::max(st.iters, (int)h[7]);
+    st.res0 = std::max(st.res0, h[4]);
+    st.res = std::max(st.res, h[4] > 0 ? h[5] / h[4] : 0.0);
+  }
+  return st;
 }
 
 SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
@@ -500,7 +587,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   });
   DFMI_HIP(hipGetLastError());
   Red red = L.after(p1, 2);
-  WS.hscal.resize((size_t)nsys * NSCAL);
+  Poller poll(x, WS.scal.p, nsys);
   const int check = 2;
   for (int it = 0;; ++it) {
     { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, C, Ce, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red, WS.scal.p, b); }
@@ -523,26 +610,11 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, C, Ce, red, q, smap, WS.scal.p, b, p1); }
     DFMI_HIP(hipGetLastError());
     red = L.after(p1, 2);
-    if ((it + 1) % check == 0) {
-      DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-      DFMI_HIP(hipStreamSynchronize(x.stream));
-      bool any = false;
-      for (int s = 0; s < nsys; ++s) any |= WS.hscal[s * NSCAL + 6] != 0.0;
-      if (!any) break;
-    }
+    if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
   }
   DFMI_HIP(hipGetLastError());
-  DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-  DFMI_HIP(hipStreamSynchronize(x.stream));
-  SolveStats st;
-  for (int s = 0; s < nsys; ++s) {
-    const double* h = &WS.hscal[s * NSCAL];
-    st.iters = std::max(st.iters, (int)h[7]);
-    st.res0 = std::max(st.res0, h[4]);
-    st.res = std::max(st.res, h[4] > 0 ? h[5] / h[4] : 0.0);
-  }
-  x.last_stats[eqn] = st;
-  return st;
+  record_stats(x, eqn, WS.scal.p, nsys);
+  return SolveStats{};
 }
 
 SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double* upper, const double* diag,
@@ -584,17 +656,18 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   });
   DFMI_HIP(hipGetLastError());
   // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
-  auto reds = [&](Red& rz, Red& rr) {
+  // act: the solve's active flag (after the first iteration the V-cycle of a stopped solve is skipped)
+  auto reds = [&](Red& rz, Red& rr, const double* act) {
     Red r2 = L.after(q2, 2, 0);
     rr = r2; rr.p += 1;
     if (amg) {
-      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk);
+      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, act);
       rz = L.after(q3, 1, 1);
     } else rz = r2;
   };
   Red red_rz, red_rr;
-  reds(red_rz, red_rr);
-  WS.hscal.resize(NSCAL);
+  reds(red_rz, red_rr, nullptr);
+  Poller poll(x, WS.scal.p, 1);
   const int check = amg ? 2 : 8;
   double* pold = v.pa;
   double* pnew = v.pb;
@@ -614,23 +687,13 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       else hipLaunchKernelGGL(k_cg_x<true>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
     }
     DFMI_HIP(hipGetLastError());
-    reds(red_rz, red_rr);
+    reds(red_rz, red_rr, WS.scal.p + 6);
     std::swap(pold, pnew);
-    if ((it + 1) % check == 0) {
-      DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-      DFMI_HIP(hipStreamSynchronize(x.stream));
-      if (WS.hscal[6] == 0.0) break;
-    }
+    if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
   }
   DFMI_HIP(hipGetLastError());
-  DFMI_HIP(hipMemcpyAsync(WS.hscal.data(), WS.scal.p, NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-  DFMI_HIP(hipStreamSynchronize(x.stream));
-  SolveStats st;
-  st.iters = (int)WS.hscal[7];
-  st.res0 = WS.hscal[4];
-  st.res = WS.hscal[4] > 0 ? WS.hscal[5] / WS.hscal[4] : 0.0;
-  x.last_stats[eqn] = st;
-  return st;
+  record_stats(x, eqn, WS.scal.p, 1);
+  return SolveStats{};
 }
 
 }  // namespace dfmi

@@ -56,6 +56,7 @@ SIGNATURES = {
     "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
     "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
+    "dfmi_solver_work": [_P, C.c_char_p, _DP, C.c_int],
     "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
     "dfmi_amg_info": [_P, C.c_int, _IP, _IP, _IP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
@@ -270,6 +271,12 @@ class Context:
         it = C.c_int(); r0 = C.c_double(); rel = C.c_double()
         self._call("dfmi_solver_stats", self.h, eqn.encode(), C.byref(it), C.byref(r0), C.byref(rel))
         return it.value, r0.value, rel.value
+
+    def solver_work(self, eqn, reset=False):
+        """system-iterations performed by the solves of `eqn` since the last reset"""
+        v = C.c_double()
+        self._call("dfmi_solver_work", self.h, eqn.encode(), C.byref(v), int(reset))
+        return v.value
 
     def time_step(self, n_corr=2):
         self._call("dfmi_time_step", self.h, int(n_corr))

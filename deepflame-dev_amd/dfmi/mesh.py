@@ -97,6 +97,11 @@ class Mesh:
         return int(sum(p.slots for p in self.patches))
 
     @property
+    def n_coupled_slots(self) -> int:
+        """primary slots of coupled patches (cyclic / processor): one off-diagonal matrix entry each"""
+        return int(sum(p.size for p in self.patches if p.kind in ("cyclic", "processor", "processorCyclic")))
+
+    @property
     def patch_sizes(self) -> np.ndarray:
         return np.array([p.size for p in self.patches], dtype=np.int32)
 

@@ -128,6 +128,10 @@ int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
 int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width);
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
+/* work done by the solves of `eqn` since the last reset: the sum over solves and systems of the
+ * iterations performed (each one = one PCG SpMV, or two BiCGStab SpMVs, of one system); reset != 0
+ * zeroes the counter after reading. Measurement aid for bench.py (no reference counterpart). */
+int dfmi_solver_work(dfmi_ctx* ctx, const char* eqn, double* system_iterations, int reset);
 
 /* ---- chemistry (dfChemistryModel::solveSingle, dfChemistryModel.C:737-780; GPU ABI
  * precedent opencc_ode_init/opencc_ode_all, YEqn.H:45-77) ------------------------------------- */

@@ -24,9 +24,10 @@ def main(fetch_csv, write_csv, out):
         fv = sorted(f[k]); wv = sorted(w[k])
         fm, wm = fv[len(fv) // 2], wv[len(wv) // 2]
         fmax, wmax = fv[-1], wv[-1]
+        fa, wa = sum(fv) / len(fv), sum(wv) / len(wv)
         res[k] = {"dispatches": len(fv), "fetch_kb_median": fm, "write_kb_median": wm, "fetch_kb_max": fmax,
                   "write_kb_max": wmax, "hbm_bytes_median": (2 * fm + wm) * 1024.0,
-                  "hbm_bytes_max": (2 * fmax + wmax) * 1024.0}
+                  "hbm_bytes_max": (2 * fmax + wmax) * 1024.0, "hbm_bytes_mean": (2 * fa + wa) * 1024.0}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_max"])[:15]:
         print(f"{v['hbm_bytes_max'] / 1e6:10.1f} MB  {k}")
