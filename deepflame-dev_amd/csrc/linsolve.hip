@@ -156,9 +156,29 @@ __global__ void k_copy_x(long C, long Ce, Sys q, const int* __restrict__ sys_map
 }
 
 // ============================================================== BiCGStab (AmgX PBiCGStab semantics)
+// Jacobi-scaled BiCGStab: the iteration runs on D^-1 A x = D^-1 b (D = diag + internalCoeffs), so the
+// operator has a unit diagonal, no preconditioned copies of p and s are stored, and the convergence
+// test uses the true residual norm ||b - A x|| = ||D r|| (AmgX RELATIVE_INI_CORE, L2). Four kernels
+// per iteration: v = A p, s = r - alpha v, t = A s, and one fused update x += alpha p + omega s,
+// r = s - omega t, p = r + beta (p - omega v) -- rho_new = r0.r comes from the recurrence
+// r0.s - omega r0.t, whose two dot products the previous kernels already reduced, so the next
+// direction is formed in the same pass as the solution update.
 // scal[s*16 + k]: 0 rho, 1 rho_old, 2 alpha, 3 omega, 4 res0, 5 res, 6 active, 7 iters
-struct BV { double *dS, *rhs, *r, *r0, *p, *v, *phat, *sv, *shat, *t, *xw; };
+struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; };
+constexpr int BCG_VECS = 9;
 
+// y = (A in)_c / D_c = in_c + (sum_k val in_j) / D_c
+template <int WT> __device__ __forceinline__ double scaled_mv(int W_, long C, const int* __restrict__ col,
+                                                              const double* __restrict__ val, double d,
+                                                              const double* __restrict__ xv, int c) {
+  const int W = WT > 0 ? WT : W_;
+  double o = 0.0;
+#pragma unroll
+  for (int k = 0; k < W; ++k) o += val[k * C + c] * xv[col[k * C + c]];
+  return xv[c] + o / d;
+}
+
+// r = D^-1 (b - A x); r0 = p = r; partials (||D r||^2, r0.r)
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const int* __restrict__ col,
                                                   const double* __restrict__ val, BV b, double* partial) {
@@ -167,105 +187,114 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const 
   double acc[2] = {0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double ax = ell_mv<WT>(W, C, col, vs, b.dS[i], b.xw + s * Ce, c);
-    const double rr = b.rhs[i] - ax;
-    b.r[i] = rr; b.r0[i] = rr; b.p[i] = 0.0; b.v[i] = 0.0;
-    acc[0] += rr * rr;
+    const double d = b.dS[i];
+    const double res = b.rhs[i] - ell_mv<WT>(W, C, col, vs, d, b.xw + s * Ce, c);
+    const double rr = res / d;
+    b.r[i] = rr; b.r0[i] = rr; b.p[i] = rr;
+    acc[0] += res * res;
     acc[1] += rr * rr;
   }
   block_partials<2>(acc, partial, s);
 }
 
-// prologue: res, rho from (r.r, r0.r); convergence; p = r + beta (p - omega v); phat = p / dS
-__global__ void __launch_bounds__(TPB) k_bcg_p(long C, long Ce, int it, int max_iter, double tol, double abs_tol,
-                                               Red red, double* scal, BV b) {
+// prologue: res = ||D r||, rho; convergence; v = D^-1 A p; partial r0.v
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const int* __restrict__ col,
+                                                   const double* __restrict__ val, int it, int max_iter, double tol,
+                                                   double abs_tol, Red red, double* scal, BV b, double* partial) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (it > 0 && st[6] == 0.0) return;   // stopped earlier (uniform per block)
-  double v[2];
-  red_sum<2>(red, s, v);
-  const double res = sqrt(v[0]), rho = v[1];
+  double v2[2];
+  red_sum<2>(red, s, v2);
+  const double res = sqrt(v2[0]);
+  const double rho = it == 0 ? v2[1] : st[0];
   const double res0 = it == 0 ? res : st[4];
-  const double omega = st[3];
-  const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || omega == 0.0));
+  const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || st[3] == 0.0));
   if (leader()) {
-    if (it == 0) st[4] = res;
-    if (it == 0 || st[6] != 0.0) { st[5] = res; st[7] = it; }
+    if (it == 0) { st[4] = res; st[0] = rho; }
+    st[5] = res; st[7] = it;
     st[6] = stop ? 0.0 : 1.0;
-    st[0] = rho;
   }
   if (stop) return;
-  const double beta = it == 0 ? 0.0 : (rho / st[1]) * (st[2] / omega);
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const long i = s * Ce + c;
-    const double pv = it == 0 ? b.r[i] : b.r[i] + beta * (b.p[i] - omega * b.v[i]);
-    b.p[i] = pv;
-    b.phat[i] = pv / b.dS[i];
-  }
-}
-
-// out = A in; partial dots (NV = 1: r0.out; NV = 2: out.sv, out.out)
-template <int WT, int NV>
-__global__ void __launch_bounds__(TPB) k_bcg_spmv(long C, long Ce, int W, const int* __restrict__ col,
-                                                  const double* __restrict__ val, const double* scal,
-                                                  const double* __restrict__ dS, const double* __restrict__ in,
-                                                  double* __restrict__ out, const double* __restrict__ dotv,
-                                                  double* partial) {
-  const int s = blockIdx.y;
-  if (scal[s * NSCAL + 6] == 0.0) return;   // uniform per block
   const double* vs = val + (long)s * W * C;
-  double acc[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  double acc[1] = {0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double y = ell_mv<WT>(W, C, col, vs, dS[i], in + s * Ce, c);
-    out[i] = y;
-    if (NV == 1) acc[0] += dotv[i] * y;
-    else { acc[0] += y * dotv[i]; acc[NV - 1] += y * y; }
+    const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], b.p + s * Ce, c);
+    b.v[i] = y;
+    acc[0] += b.r0[i] * y;
   }
-  block_partials<NV>(acc, partial, s);
+  block_partials<1>(acc, partial, s);
 }
 
-// prologue: alpha = rho / (r0.v); s = r - alpha v; shat = s / dS
-__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b) {
+// prologue: alpha = rho / (r0.v); s = r - alpha v; partial r0.s
+__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b, double* partial) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
   double v[1];
   red_sum<1>(red, s, v);
-  const double rho = st[0];
-  const double alpha = v[0] != 0.0 ? rho / v[0] : 0.0;
-  if (leader()) { st[2] = alpha; st[1] = rho; }
+  const double alpha = v[0] != 0.0 ? st[0] / v[0] : 0.0;
+  if (leader()) st[2] = alpha;
+  double acc[1] = {0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double ss = b.r[i] - alpha * b.v[i];
-    b.sv[i] = ss;
-    b.shat[i] = ss / b.dS[i];
+    const double sv = b.r[i] - alpha * b.v[i];
+    b.sv[i] = sv;
+    acc[0] += b.r0[i] * sv;
   }
+  block_partials<1>(acc, partial, s);
 }
 
-// prologue: omega = (t.s)/(t.t); x += alpha phat + omega shat; r = s - omega t; partials (r.r, r0.r)
-__global__ void __launch_bounds__(TPB) k_bcg_x(long C, long Ce, Red red, Sys q, const int* __restrict__ sys_map,
-                                               double* scal, BV b, double* partial) {
+// t = D^-1 A s; partials (t.s, t.t, r0.t)
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W, const int* __restrict__ col,
+                                                   const double* __restrict__ val, const double* scal, BV b,
+                                                   double* partial) {
+  const int s = blockIdx.y;
+  if (scal[s * NSCAL + 6] == 0.0) return;   // uniform per block
+  const double* vs = val + (long)s * W * C;
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const long i = s * Ce + c;
+    const double* sv = b.sv + s * Ce;
+    const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], sv, c);
+    b.t[i] = y;
+    acc[0] += y * sv[c];
+    acc[1] += y * y;
+    acc[2] += b.r0[i] * y;
+  }
+  block_partials<3>(acc, partial, s);
+}
+
+// prologue: omega = (t.s)/(t.t); rho_new = r0.s - omega r0.t; beta = (rho_new / rho)(alpha / omega);
+// x += alpha p + omega s; r = s - omega t; p = r + beta (p - omega v); partials (||D r||^2, 0)
+__global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_s, Red red_t, Sys q,
+                                                const int* __restrict__ sys_map, double* scal, BV b, double* partial) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
-  double v[2];
-  red_sum<2>(red, s, v);
-  const double omega = v[1] != 0.0 ? v[0] / v[1] : 0.0;
-  const double alpha = st[2];
-  if (leader()) st[3] = omega;
+  double r0s[1], tv[3];
+  red_sum<1>(red_s, s, r0s);
+  red_sum<3>(red_t, s, tv);
+  const double omega = tv[1] != 0.0 ? tv[0] / tv[1] : 0.0;
+  const double alpha = st[2], rho = st[0];
+  const double rho_new = r0s[0] - omega * tv[2];
+  const double beta = (rho != 0.0 && omega != 0.0) ? (rho_new / rho) * (alpha / omega) : 0.0;
+  if (leader()) { st[3] = omega; st[1] = rho; st[0] = rho_new; }
   const int ms = sys_map ? sys_map[s] : s;
   double* xv = q.x + ms * q.xstride;
   double acc[2] = {0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    xv[c] = xv[c] + alpha * b.phat[i] + omega * b.shat[i];
-    const double rr = b.sv[i] - omega * b.t[i];
+    const double pv = b.p[i], sv = b.sv[i];
+    xv[c] = xv[c] + alpha * pv + omega * sv;
+    const double rr = sv - omega * b.t[i];
     b.r[i] = rr;
-    acc[0] += rr * rr;
-    acc[1] += b.r0[i] * rr;
+    b.p[i] = rr + beta * (pv - omega * b.v[i]);
+    const double tr = b.dS[i] * rr;
+    acc[0] += tr * tr;
   }
   block_partials<2>(acc, partial, s);
 }
@@ -411,13 +440,14 @@ struct Launch {
   // reductions that are alive at the same time)
   Red after(double* partial, int NV, int slot = 0) {
     if (x.nranks == 1) return Red{partial, nblk, NV, (long)nblk * NV};
-    const size_t per = (size_t)nsys * 2;
+    const size_t per = (size_t)nsys * 4;   // up to 3 values per system per slot
     if (x.ws.red_local.n < 2 * per) x.ws.red_local.alloc(2 * per);
     if (x.ws.red_all.n < 2 * per * x.nranks) x.ws.red_all.alloc(2 * per * x.nranks);
     double* loc = x.ws.red_local.p + slot * per;
     double* all = x.ws.red_all.p + slot * per * x.nranks;
     if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
-    else hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    else if (NV == 2) hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    else hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
     DFMI_HIP(hipGetLastError());
     halo_allgather(x, loc, all, (long)nsys * NV);
     return Red{all, x.nranks, (long)nsys * NV, NV};
@@ -500,19 +530,19 @@ void record_stats(Ctx& x, const char* eqn, const double* scal, int nsys) {
 
 }  // namespace
 
-// BiCGStab workspace: 11 vectors of nsys * (C + H), then the ELL values [nsys][W][C], then partials.
+// BiCGStab workspace: BCG_VECS vectors of nsys * (C + H), then the ELL values [nsys][W][C], then partials.
 // Assembly kernels that emit the ELL form directly (y_assemble_ell) write into it before the solve.
 void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   if (!x.ell.ready) build_ell(x);
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
-  const size_t need = 11 * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 6 + 64;
+  const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 8 + 64;
   if (x.ws.buf.n < need) x.ws.buf.alloc(need);
   const long N = nsys * Ce;
   *dS = x.ws.buf.p;
   *rhs = x.ws.buf.p + N;
-  *val = x.ws.buf.p + 11 * N;
+  *val = x.ws.buf.p + BCG_VECS * N;
 }
 
 double solver_work(Ctx& x, const std::string& eqn, bool reset) {
@@ -563,12 +593,13 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   const long N = nsys * Ce;
   double* base = WS.buf.p;
   BV b{base, base + N, base + 2 * N, base + 3 * N, base + 4 * N, base + 5 * N, base + 6 * N, base + 7 * N,
-       base + 8 * N, base + 9 * N, base + 10 * N};
-  double* val = base + 11 * N;
-  // one partial buffer per reduction site, so a converged system's last sums stay intact
-  double* p1 = val + (size_t)nsys * W * C;          // (r.r, r0.r)
-  double* p2 = p1 + (size_t)nsys * nblk * 2;        // r0.v
-  double* p3 = p2 + (size_t)nsys * nblk * 2;        // (t.s, t.t)
+       base + 8 * N};
+  double* val = base + BCG_VECS * N;
+  // one partial buffer per reduction site (a converged system's last sums stay intact)
+  double* pR = val + (size_t)nsys * W * C;          // (||D r||^2, rho0 | 0): init, xp
+  double* pV = pR + (size_t)nsys * nblk * 2;        // r0.v
+  double* pS = pV + (size_t)nsys * nblk;            // r0.s
+  double* pT = pS + (size_t)nsys * nblk;            // (t.s, t.t, r0.t)
   Sys q{lower, upper, diag, source, ic, bc, lstride, ustride, dstride, sstride, bstride, xsol, xstride};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
@@ -583,33 +614,34 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   halo_vecs(x, {b.xw}, nsys, Ce);
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
-    { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, b, p1); }
+    { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, b, pR); }
   });
   DFMI_HIP(hipGetLastError());
-  Red red = L.after(p1, 2);
+  Red red = L.after(pR, 2);
   Poller poll(x, WS.scal.p, nsys);
   const int check = 2;
   for (int it = 0;; ++it) {
-    { KScope _ks(x, "k_bcg_p"); hipLaunchKernelGGL(k_bcg_p, g, bl, 0, x.stream, C, Ce, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red, WS.scal.p, b); }
+    halo_vecs(x, {b.p}, nsys, Ce);
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_spmv");
+      hipLaunchKernelGGL((k_bcg_spmv1<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
+                         cfg.abs_tol, red, WS.scal.p, b, pV);
+    });
     if (it >= cfg.max_iter) break;
-    halo_vecs(x, {b.phat}, nsys, Ce);
+    red = L.after(pV, 1);
+    { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b, pS); }
+    const Red red_s = L.after(pS, 1, 1);
+    halo_vecs(x, {b.sv}, nsys, Ce);
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL((k_bcg_spmv<WT, 1>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.phat, b.v, b.r0, p2);
+      hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b, pT);
     });
-    red = L.after(p2, 1);
-    { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
-    halo_vecs(x, {b.shat}, nsys, Ce);
-    dispatch_W(W, [&](auto wt) {
-      constexpr int WT = decltype(wt)::value;
-      KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL((k_bcg_spmv<WT, 2>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b.dS, b.shat, b.t, b.sv, p3);
-    });
-    red = L.after(p3, 2);
-    { KScope _ks(x, "k_bcg_x"); hipLaunchKernelGGL(k_bcg_x, g, bl, 0, x.stream, C, Ce, red, q, smap, WS.scal.p, b, p1); }
+    const Red red_t = L.after(pT, 3, 0);
+    { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_bcg_xp, g, bl, 0, x.stream, C, Ce, red_s, red_t, q, smap, WS.scal.p, b, pR); }
     DFMI_HIP(hipGetLastError());
-    red = L.after(p1, 2);
+    red = L.after(pR, 2, 0);
     if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
   }
   DFMI_HIP(hipGetLastError());
