@@ -20,67 +20,77 @@ constexpr double SQRT8 = 2.8284271247461903;
 
 struct TC {   // coefficient table pointers
   const double *W, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;
+  int sym;      // bdiff[i][j] == bdiff[j][i] bitwise (binary diffusion fits are symmetric)
 };
 
-template <int S>
-__device__ __forceinline__ double h_mix(const TC& t, double T, const double* y) {
-  double h = 0.;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const double* a = t.nasa + i * 15;
-    const int o = (T > a[0]) ? 1 : 8;
-    h += (a[o] + a[o + 1] * T / 2 + a[o + 2] * T * T / 3 + a[o + 3] * T * T * T / 4 + a[o + 4] * T * T * T * T / 5 +
-          a[o + 5] / T) * R_GAS * T / t.W[i] * y[i];
-  }
-  return h;
+// NASA7 polynomials of species i at T: cp/R and h/(R T)
+__device__ __forceinline__ void nasa_cp_h(const double* a, double T, double& cpR, double& hRT) {
+  const int o = (T > a[0]) ? 1 : 8;
+  const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;
+  cpR = a[o] + a[o + 1] * T + a[o + 2] * T2 + a[o + 3] * T3 + a[o + 4] * T4;
+  hRT = a[o] + a[o + 1] * T / 2 + a[o + 2] * T2 / 3 + a[o + 3] * T3 / 4 + a[o + 4] * T4 / 5 + a[o + 5] / T;
 }
+
+// mixture h and cp at T, ryw[i] = R Y_i / W_i
 template <int S>
-__device__ __forceinline__ double cp_mix(const TC& t, double T, const double* y) {
-  double cp = 0.;
+__device__ __forceinline__ void hcp_mix(const TC& t, double T, const double* ryw, double& h, double& cp) {
+  h = 0.; cp = 0.;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const double* a = t.nasa + i * 15;
-    const int o = (T > a[0]) ? 1 : 8;
-    cp += y[i] * (a[o] + a[o + 1] * T + a[o + 2] * T * T + a[o + 3] * T * T * T + a[o + 4] * T * T * T * T) * R_GAS / t.W[i];
+    double c, hh;
+    nasa_cp_h(t.nasa + i * 15, T, c, hh);
+    h += hh * T * ryw[i];
+    cp += c * ryw[i];
   }
-  return cp;
 }
 
 // state (T or he), p, Y -> T, he, psi, rho, mu, alpha, rhoD[S], hai[S]; mirrors oracle thermo_point
+// (same formulas; divisions hoisted out of the O(S^2) loops -- reciprocals of the species
+// viscosities, one reciprocal per binary-diffusion pair when the fit table is symmetric -- so the
+// result agrees with the sequential evaluation to rounding, not bitwise)
 template <int S>
 __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, double& he, double p, const double* y,
                                              double& psi, double& rho, double& mu, double& alpha, double* rhoD,
                                              double* hai) {
-  double X[S];
+  double X[S], rw[S], ryw[S];
   double sum = 0.;
 #pragma unroll
-  for (int i = 0; i < S; ++i) sum += y[i] / t.W[i];
+  for (int i = 0; i < S; ++i) { rw[i] = R_GAS / t.W[i]; ryw[i] = rw[i] * y[i]; sum += y[i] / t.W[i]; }
   double Wm = 0.;
+  const double rsum = 1.0 / sum;
 #pragma unroll
-  for (int i = 0; i < S; ++i) { X[i] = y[i] / (t.W[i] * sum); Wm += X[i] * t.W[i]; }
-  if (fixT) he = h_mix<S>(t, T, y);
-  else {
+  for (int i = 0; i < S; ++i) { X[i] = y[i] / t.W[i] * rsum; Wm += X[i] * t.W[i]; }
+  double cpm;
+  if (fixT) {
+    hcp_mix<S>(t, T, ryw, he, cpm);
+  } else {
     double tt = T;
     for (int n = 0; n < 20; ++n) {
-      const double h = h_mix<S>(t, tt, y), cp = cp_mix<S>(t, tt, y);
+      double h, cp;
+      hcp_mix<S>(t, tt, ryw, h, cp);
       const double dT = (h - he) / cp;
       tt -= dT;
       if (fabs(h - he) < 1e-7 || fabs(dT / tt) < 1e-7) break;
     }
     T = tt;
+    double h_;
+    hcp_mix<S>(t, T, ryw, h_, cpm);
   }
   const double lnT = log(T);
   double poly[5];
   poly[0] = 1.0; poly[1] = lnT; poly[2] = poly[1] * poly[1]; poly[3] = poly[1] * poly[2]; poly[4] = poly[2] * poly[2];
   psi = Wm / (R_GAS * T);
   rho = p * psi;
-  double sv[S];
+  // Wilke mixture viscosity
+  double sv[S], rsv[S], xs[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     double dp = 0.;
 #pragma unroll
     for (int j = 0; j < 5; ++j) dp += t.visc[i * 5 + j] * poly[j];
     sv[i] = dp;
+    rsv[i] = 1.0 / dp;
+    xs[i] = X[i] * (1.0 / SQRT8);
   }
   double mumix = 0.;
 #pragma unroll
@@ -88,8 +98,8 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
     double s2 = 0.;
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      const double tmp = 1.0 + (sv[i] / sv[j]) * t.vc2[i * S + j];
-      s2 += X[j] / SQRT8 * t.vc1[i * S + j] * (tmp * tmp);
+      const double tmp = 1.0 + (sv[i] * rsv[j]) * t.vc2[i * S + j];
+      s2 += xs[j] * t.vc1[i * S + j] * (tmp * tmp);
     }
     mumix += X[i] * (sv[i] * sv[i]) / s2;
   }
@@ -105,31 +115,48 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
     sc += X[i] * lam;
     sic += X[i] / lam;
   }
-  alpha = 0.5 * (sc + 1.0 / sic) / cp_mix<S>(t, T, y);
+  alpha = 0.5 * (sc + 1.0 / sic) / cpm;
+  // mixture-averaged diffusion: s1_i = sum_j X_j / D_ij, s2_i = sum_j X_j W_j / D_ij (j != i, ascending j)
   const double powT = T * sT, rdp = rho / p;
+  double s1[S], s2[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) {
-    if (X[i] + 1e-10 > 1.) { rhoD[i] = 0.; continue; }
-    double s1 = 0., s2 = 0.;
+  for (int i = 0; i < S; ++i) { s1[i] = 0.; s2[i] = 0.; }
+  if (t.sym) {   // D_ij = D_ji: one fit evaluation and one reciprocal per pair
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      if (i == j) continue;
-      double tmp = 0.;
+    for (int i = 0; i < S; ++i)
 #pragma unroll
-      for (int k = 0; k < 5; ++k) tmp += t.bdiff[(i * S + j) * 5 + k] * poly[k];
-      const double Dl = tmp * powT;
-      s1 += X[j] / Dl;
-      s2 += X[j] * t.W[j] / Dl;
-    }
-    s2 *= X[i] / (Wm - X[i] * t.W[i]);
-    rhoD[i] = 1 / (s1 + s2) * rdp;
+      for (int j = i + 1; j < S; ++j) {
+        double tmp = 0.;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) tmp += t.bdiff[(i * S + j) * 5 + k] * poly[k];
+        const double inv = 1.0 / (tmp * powT);
+        s1[i] += X[j] * inv; s2[i] += X[j] * t.W[j] * inv;
+        s1[j] += X[i] * inv; s2[j] += X[i] * t.W[i] * inv;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        if (i == j) continue;
+        double tmp = 0.;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) tmp += t.bdiff[(i * S + j) * 5 + k] * poly[k];
+        const double inv = 1.0 / (tmp * powT);
+        s1[i] += X[j] * inv; s2[i] += X[j] * t.W[j] * inv;
+      }
   }
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const double* a = t.nasa + i * 15;
-    const int o = (T > a[0]) ? 1 : 8;
-    hai[i] = (a[o] + a[o + 1] * T / 2 + a[o + 2] * T * T / 3 + a[o + 3] * T * T * T / 4 + a[o + 4] * T * T * T * T / 5 +
-              a[o + 5] / T) * R_GAS * T / t.W[i];
+    if (X[i] + 1e-10 > 1.) { rhoD[i] = 0.; continue; }
+    const double q2 = s2[i] * (X[i] / (Wm - X[i] * t.W[i]));
+    rhoD[i] = 1 / (s1[i] + q2) * rdp;
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    double c, hh;
+    nasa_cp_h(t.nasa + i * 15, T, c, hh);
+    hai[i] = hh * T * rw[i];
   }
 }
 
@@ -197,7 +224,12 @@ void thermo_upload(Ctx& x) {
 void thermo_correct(Ctx& x, bool from_T) {
   Thermo& th = x.thermo;
   DFMI_CHECK(th.S == x.S, "thermo coefficients not set or species count mismatch");
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2};
+  int sym = 1;
+  for (int i = 0; i < th.S && sym; ++i)
+    for (int j = 0; j < th.S && sym; ++j)
+      for (int k = 0; k < 5; ++k)
+        if (th.bdiff[(i * th.S + j) * 5 + k] != th.bdiff[(j * th.S + i) * 5 + k]) { sym = 0; break; }
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                   \
   do {                                                                                                            \
