@@ -12,8 +12,9 @@
 // hidden layer of all S-1 nets is ONE batched GEMM launch (grid.z = net) on MFMA
 // v_mfma_f32_32x32x16_f16 with fp32 accumulation and the bias + exact-erf GELU + fp16 rounding fused
 // into the epilogue; the 1-wide output layer and the BCT post-processing are fused into one kernel.
-// GEMM tile 128x128x32, 4 waves (2x2, 64x64 each = 2x2 MFMA tiles), LDS double buffer, A and W both
-// K-contiguous (W in torch Linear [out][in] layout), K padded to a multiple of 32.
+// GEMM tile 128x128x32, 4 waves (2x2, 64x64 each = 2x2 MFMA tiles), both operands streamed
+// global -> LDS by DMA (global_load_lds, swizzled rows) through a 3-buffer ring, A and W both
+// K-contiguous (W in torch Linear [out][in] layout), K and activation row strides padded to 64.
 #include "dfmi_ctx.h"
 #include <cmath>
 
@@ -24,47 +25,76 @@ using half8 = __attribute__((ext_vector_type(8))) _Float16;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDK = BK + 8;   // LDS row stride in halves (80 B) against bank conflicts
+constexpr int NBUF = 3;                   // LDS ring: two K tiles in flight while one feeds the MFMAs
 constexpr int GT = 256;
-constexpr int LD_IT = BM * BK / 8 / GT;   // 16-byte global loads per thread per operand per K tile
+constexpr int KPAD = 64;                  // every GEMM K (and activation row stride) is a multiple of this
+constexpr int TILE_H = BM * BK;           // halves per staged operand tile (8 KiB)
 
-__device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f)); }
+// GELU for the GEMM epilogue: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, branch-free), three
+// orders of magnitude below the fp16 rounding the result goes through (torch's GELU is the exact-erf
+// form); the library erff branches per lane on |x| < 1 and dominated the epilogue of the shallow
+// (K = 11) first layer
+__device__ __forceinline__ float gelu_fast(float v) {
+  const float u = v * 0.70710678118654752440f, a = fabsf(u);
+  const float t = __frcp_rn(1.0f + 0.3275911f * a);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = 1.0f - poly * __expf(-a * a);
+  return 0.5f * v * (1.0f + copysignf(e, u));
+}
 
-// C[z][M][N] = act(A[z][M][K] . W[z][N][K]^T + b[z][N]), fp16 in/out, fp32 accumulate.
-// Block 128x128, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles), K tile 32,
-// LDS double buffer fed through registers: the next tile's global loads are in flight during this
-// tile's 16 MFMAs per wave.
+// 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_wave + 16 l
+__device__ __forceinline__ void glds16(const _Float16* g, _Float16* lds_wave) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave, 16, 0, 0);
+}
+
+// 16-B chunk c (of 4 per 64-B row) of row `row` lives at chunk c ^ ((row >> 2) & 3): the 16 rows a
+// ds_read_b128 lane group reads ({0-3,12-15,20-27}, {4-11,16-19,28-31} of each half-wave) then hit 16
+// distinct bank slots (conflict-free)
+__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 2) & 3); }
+
+// C[z][M][ldc] = act(A[z][M][lda] . W[z][N][K]^T + b[z][N]) for columns < N, 0 for N <= col < ldc;
+// fp16 in/out, fp32 accumulate. K, lda, ldc multiples of 64.
+// Block tile 128x128x32, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles).
+// Both operand tiles are streamed global -> LDS by DMA (global_load_lds, 16 B per lane, 4 DMA
+// instructions per thread per K tile) through a 3-buffer ring: tiles k+1 and k+2 are in flight while
+// tile k feeds the MFMAs; the wait before each barrier is counted (vmcnt(4): the newest tile stays in
+// flight) and the barrier is a raw s_barrier, so nothing drains the DMA queue inside the loop. The
+// swizzle is applied on the global source address (each DMA still writes 1 KiB contiguously). 48 KiB
+// LDS: three blocks per CU. Block ids are remapped so the consecutive ids that share an XCD walk the
+// N tiles of one M tile (A rows re-read from that XCD's L2).
 template <bool GELU>
-__global__ void __launch_bounds__(GT, 2) k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, long sA,
-                                                    const _Float16* __restrict__ W, long sW,
+__global__ void __launch_bounds__(GT, 3) k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, int lda,
+                                                    long sA, const _Float16* __restrict__ W, long sW,
                                                     const float* __restrict__ bias, long sb,
-                                                    _Float16* __restrict__ Cout, long sC) {
-  __shared__ _Float16 As[2][BM * LDK];
-  __shared__ _Float16 Ws[2][BN * LDK];
+                                                    _Float16* __restrict__ Cout, int ldc, long sC) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[NBUF * 2 * TILE_H];   // [buf][A | W][128][32]
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM, nwg = ntn * ntm;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  half8 ra[LD_IT], rw[LD_IT];
-  auto gload = [&](int k0) {
+  // staging: wave w fills rows [32 w, 32 w + 32) of both tiles, 16 rows (1 KiB) per DMA instruction
+  const _Float16* pa[2];
+  const _Float16* pw[2];
 #pragma unroll
-    for (int it = 0; it < LD_IT; ++it) {
-      const int idx = tid + it * GT;
-      const int r = idx / (BK / 8), c = (idx % (BK / 8)) * 8;
-      const int gm = m0 + r, gn = n0 + r;
-      ra[it] = (gm < M && k0 + c < K) ? *reinterpret_cast<const half8*>(A + (long)gm * K + k0 + c) : half8{};
-      rw[it] = (gn < N && k0 + c < K) ? *reinterpret_cast<const half8*>(W + (long)gn * K + k0 + c) : half8{};
-    }
-  };
-  auto lstore = [&](int buf) {
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 32 + i * 16 + (lane >> 2);
+    const int gc = swz(row, lane & 3);
+    const int ga = min(m0 + row, M - 1), gw = min(n0 + row, N - 1);   // clamped rows are masked on store
+    pa[i] = A + (long)ga * lda + gc * 8;
+    pw[i] = W + (long)gw * K + gc * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    _Float16* la = lds + buf * 2 * TILE_H;
+    _Float16* lw = la + TILE_H;
 #pragma unroll
-    for (int it = 0; it < LD_IT; ++it) {
-      const int idx = tid + it * GT;
-      const int r = idx / (BK / 8), c = (idx % (BK / 8)) * 8;
-      *reinterpret_cast<half8*>(&As[buf][r * LDK + c]) = ra[it];
-      *reinterpret_cast<half8*>(&Ws[buf][r * LDK + c]) = rw[it];
-    }
+    for (int i = 0; i < 2; ++i) glds16(pa[i] + k0, la + (wave * 32 + i * 16) * BK);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(pw[i] + k0, lw + (wave * 32 + i * 16) * BK);
   };
   f32x16 acc[2][2];
 #pragma unroll
@@ -73,45 +103,70 @@ __global__ void __launch_bounds__(GT, 2) k_mlp_gemm(int M, int N, int K, const _
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  const int nk = (K + BK - 1) / BK;
-  gload(0);
-  lstore(0);
-  __syncthreads();
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int r = lane & 31, h = lane >> 5;
+  const int nk = K / BK;
+  stage(0, 0);
+  if (nk > 1) stage(1, BK);
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    // tile kt landed (this wave's DMAs; the newer tile may stay in flight), then the barrier makes
+    // every wave's DMAs visible and frees the buffer read in iteration kt-1
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
+    const _Float16* la = lds + cur * 2 * TILE_H;
+    const _Float16* lw = la + TILE_H;
 #pragma unroll
-    for (int ks = 0; ks < BK; ks += 16) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      const int c = ks * 2 + h;   // logical 16-B chunk of this lane's 8 k values
       half8 af[2], bf[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const half8*>(&As[cur][(wm + 32 * i + r) * LDK + ks + 8 * h]);
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm + 32 * i + r;
+        af[i] = *reinterpret_cast<const half8*>(la + row * BK + swz(row, c) * 8);
+      }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const half8*>(&Ws[cur][(wn + 32 * j + r) * LDK + ks + 8 * h]);
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn + 32 * j + r;
+        bf[j] = *reinterpret_cast<const half8*>(lw + row * BK + swz(row, c) * 8);
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
-    __syncthreads();
+    cur = cur == NBUF - 1 ? 0 : cur + 1;
   }
-  // epilogue: C/D map col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+  // epilogue: bias + GELU in registers (C/D map col = lane & 31, row = (e & 3) + 8 (e >> 2) +
+  // 4 (lane >> 5)), the fp16 tile staged through LDS, written back as 16-B row chunks
+  __syncthreads();   // every wave is done with the ring (no DMA outstanding after the last wait)
+  constexpr int CLD = BN + 8;   // halves per LDS row of the output tile (row starts 16-B aligned)
+  static_assert(BM * CLD <= NBUF * 2 * TILE_H, "output tile must fit the staging ring");
+  _Float16* cs = lds;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn + 32 * j + (lane & 31);
-    if (col >= N) continue;
-    const float bv = bias[col];
+    const int cl = wn + 32 * j + (lane & 31), col = n0 + cl;
+    const bool live = col < N;
+    const float bv = live ? bias[col] : 0.0f;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        if (row >= M) continue;
+        const int rl = wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
         float v = acc[i][j][e] + bv;
-        if (GELU) v = gelu(v);
-        Cout[(long)row * N + col] = (_Float16)v;
+        if (GELU) v = gelu_fast(v);
+        cs[rl * CLD + cl] = live ? (_Float16)v : (_Float16)0.0f;
       }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < BM * BN / 8 / GT; ++it) {
+    const int idx = tid + it * GT, rl = idx / (BN / 8), ch = idx % (BN / 8);
+    const int row = m0 + rl, col = n0 + ch * 8;
+    if (row < M && col < ldc)
+      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
   }
 }
 
@@ -172,7 +227,7 @@ __global__ void k_dnn_input(int n, int C, int S, int Kp, const int* __restrict__
 }
 
 // output layer (K -> 1) of every net + calculate_y_new + calculate_RR
-__global__ void k_dnn_output(int n, int C, int S, int K, int nmod, const int* __restrict__ idx,
+__global__ void k_dnn_output(int n, int C, int S, int K, int ldh, int nmod, const int* __restrict__ idx,
                              const _Float16* __restrict__ H, long sH, const _Float16* __restrict__ w, long sw,
                              const float* __restrict__ b, const double* __restrict__ Ymu,
                              const double* __restrict__ Ystd, const double* __restrict__ Y,
@@ -184,7 +239,7 @@ __global__ void k_dnn_output(int n, int C, int S, int K, int nmod, const int* __
   double yn[32];
   double sum = 0.0;
   for (int m = 0; m < nmod; ++m) {
-    const _Float16* hr = H + m * sH + (long)i * K;
+    const _Float16* hr = H + m * sH + (long)i * ldh;
     const _Float16* wm = w + m * sw;
     float a = 0.0f;
     for (int k = 0; k < K; k += 8) {
@@ -224,10 +279,9 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
   d.dims.assign(dims, dims + nlayers + 1);
   d.Kp.resize(nlayers);
   for (int l = 0; l < nlayers; ++l) {
-    d.Kp[l] = (dims[l] + 31) / 32 * 32;
-    // hidden widths feeding another GEMM must equal their padded K; the last hidden width feeds the
-    // fused output kernel (16-byte loads)
-    if (l >= 1 && l + 1 < nlayers) DFMI_CHECK(dims[l] % 32 == 0, "DNN: hidden widths feeding a GEMM must be multiples of 32");
+    // K of every layer padded to the GEMM K tile; activations are stored with that row stride (the
+    // padding columns are written as 0, the padded weight columns are 0)
+    d.Kp[l] = (dims[l] + KPAD - 1) / KPAD * KPAD;
     if (l == nlayers - 1) DFMI_CHECK(dims[l] % 8 == 0, "DNN: last hidden width must be a multiple of 8");
   }
   // repack weights: per layer [module][out][Kp] fp16 (K zero-padded), biases fp32 [module][out]
@@ -282,7 +336,7 @@ void dnn_solve(Ctx& x) {
   const int chunk = std::min(nr, d.chunk);
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
-  for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.dims[l]);
+  for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
   const size_t act = (size_t)d.nmod * chunk * wmax;
   if (d.h0.n < act) { d.h0.alloc(act); d.h1.alloc(act); }
   if (d.x0.n < (size_t)chunk * d.Kp[0]) d.x0.alloc((size_t)chunk * d.Kp[0]);
@@ -294,24 +348,26 @@ void dnn_solve(Ctx& x) {
     const _Float16* in = d.x0.p;
     long sIn = 0;
     _Float16* bufs[2] = {d.h0.p, d.h1.p};
+    int lda = d.Kp[0];
     for (int l = 0; l + 1 < L; ++l) {
-      const int N = d.dims[l + 1], K = d.Kp[l];
+      const int N = d.dims[l + 1], K = d.Kp[l], ldc = d.Kp[l + 1];
       _Float16* out = bufs[l & 1];
-      d.gemm_flops += 2.0 * n * N * d.dims[l] * d.nmod;
-      const dim3 g(blocks_for(N, BN), blocks_for(n, BM), d.nmod);
+      d.gemm_flops += 2.0 * n * N * d.dims[l] * d.nmod;   // algorithmic flops (unpadded K)
+      const dim3 g(blocks_for(N, BN) * blocks_for(n, BM), 1, d.nmod);
       KScope _ks(x, "k_mlp_gemm");
-      hipLaunchKernelGGL(k_mlp_gemm<true>, g, dim3(GT), 0, x.stream, n, N, K, in, sIn, d.W[l].p, (long)N * K,
-                         d.b[l].p, (long)N, out, (long)n * N);
+      hipLaunchKernelGGL(k_mlp_gemm<true>, g, dim3(GT), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K,
+                         d.b[l].p, (long)N, out, ldc, (long)n * ldc);
       DFMI_HIP(hipGetLastError());
       in = out;
-      sIn = (long)n * N;
+      sIn = (long)n * ldc;
+      lda = ldc;
     }
     const int K = d.dims[L - 1];
-    DFMI_CHECK(K % 8 == 0 && d.Kp[L - 1] == (K + 31) / 32 * 32, "DNN: output layer width");
+    DFMI_CHECK(K % 8 == 0, "DNN: output layer width");
     KScope _ks(x, "k_dnn_output");
-    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, K, d.nmod, idx, in,
-                       sIn, d.W[L - 1].p, (long)d.Kp[L - 1], d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f("rho"),
-                       x.f("p"), d.dt, RR);
+    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, K, lda, d.nmod, idx,
+                       in, sIn, d.W[L - 1].p, (long)d.Kp[L - 1], d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"),
+                       x.f("rho"), x.f("p"), d.dt, RR);
     DFMI_HIP(hipGetLastError());
   }
 }
