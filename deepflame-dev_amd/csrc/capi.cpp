@@ -47,6 +47,7 @@ void allocate_fields(Ctx& x) {
   alloc_field(x, "tauU", C, 9, false);
   alloc_field(x, "chem_stats", C, 2, false);   // per cell: accepted / rejected integrator steps
   alloc_field(x, "boundary_tauU", B, 9, true);
+  alloc_field(x, "boundary_heGradient", B, 1, true);   // gradientEnergy patches (dfEEqn.cu:266-287)
   for (auto n : {"Y", "rhoD", "hai", "RR"}) {
     alloc_field(x, n, C, S, false);
     alloc_field(x, std::string("boundary_") + n, B, S, true);
@@ -350,7 +351,8 @@ int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type
       DFMI_CHECK(t >= 0 && t <= 10 && t != COUPLED, "patch " + std::to_string(p) + ": unsupported boundary condition code " + std::to_string(t));
       DFMI_CHECK((x.pkind[p] == 1) == (t == CYCLIC) && (x.pkind[p] == 2) == bc_proc(t),
                  "patch " + std::to_string(p) + ": field '" + f + "' type disagrees with the mesh patch kind");
-      if (t == GRADIENT_ENERGY) DFMI_CHECK(false, "gradientEnergy boundary not supported yet (energy BCs are a SURVEY 8f item)");
+      DFMI_CHECK(t != GRADIENT_ENERGY || f == "he", "gradientEnergy is an energy boundary condition (field 'he')");
+      DFMI_CHECK(t != FIXED_ENERGY || f == "he", "fixedEnergy is an energy boundary condition (field 'he')");
     }
     set_ptype(x, f, patch_type);
     DFMI_HIP(hipStreamSynchronize(x.stream));

@@ -230,6 +230,8 @@ void thermo_correct_psip_rho(Ctx& x);
 // thermo.hip
 void thermo_upload(Ctx& x);
 void thermo_correct(Ctx& x, bool from_T);
+// boundary_heGradient on gradientEnergy slots of he (0 elsewhere)
+void thermo_energy_gradient(Ctx& x);
 // linsolve.hip
 SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_host, const double* lower, long lstride,
                           const double* upper, long ustride, const double* diag, long dstride, const double* source,

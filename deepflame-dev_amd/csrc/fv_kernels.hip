@@ -60,8 +60,10 @@ template <class FN> __device__ __forceinline__ void each_slot(const MeshView& m,
 
 // ------------------------------------------------------------------ boundary correction
 // correct_boundary_conditions_scalar/vector (dfMatrixOpBase.cu:2402-2491)
+// gradientEnergy: cell value + gradient / deltaCoeffs (correct_boundary_conditions_gradientEnergy_scalar,
+// dfMatrixOpBase.cu:351-366)
 __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
-                             double* __restrict__ bvf, int ncomp) {
+                             double* __restrict__ bvf, int ncomp, const double* __restrict__ egrad) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= m.B) return;
   const int t = ty[b];
@@ -72,6 +74,7 @@ __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const do
     if (t == ZERO_GRADIENT || t == EXTRAPOLATED) bv[b] = v[c];
     else if (t == CYCLIC) bv[b] = interp_b(m.bw[b], v[c], v[m.partner[b]]);
     else if (bc_proc(t) && !m.sprim[b]) bv[b] = v[c];
+    else if (t == GRADIENT_ENERGY && egrad) bv[b] = v[c] + egrad[b] / m.bdc[b];
   }
 }
 
@@ -831,7 +834,8 @@ template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim
        DFMI_HIP(hipGetLastError()); } while (0)
 
 void k_bc_correct(Ctx& x, const char* tf, double* vf, double* bvf, int ncomp) {
-  LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp);
+  const double* eg = std::string(tf) == "he" ? x.f("boundary_heGradient") : nullptr;
+  LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp, eg);
 }
 
 void copy_old(Ctx& x) {   // dfMatrixDataBase::preTimeStep (dfMatrixDataBase.cu:503-517)
@@ -972,8 +976,9 @@ void y_post_solve(Ctx& x) {
 void e_assemble(Ctx& x) {
   Matrix& A = x.mE;
   MeshView m = x.view();
+  thermo_energy_gradient(x);   // eeqn_calculate_energy_gradient (dfEEqn.cu:148, :266-287)
   k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
-  const double* eg = x.fields.count("boundary_heGradient") ? x.f("boundary_heGradient") : nullptr;
+  const double* eg = x.f("boundary_heGradient");
   LAUNCH(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
          x.f("K"), x.f("K_old"), x.f("boundary_K"), x.f("phi"), x.f("boundary_phi"), x.f("alpha"),
          x.f("boundary_alpha"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("dpdt"), x.f("diffAlphaD"),

@@ -208,6 +208,35 @@ __global__ void __launch_bounds__(256) k_thermo_slots(MeshView m, TC t, const in
   for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = rd[i]; hai[(long)i * B + b] = ha[i]; }
 }
 
+// mixture enthalpy summed exactly as calculate_enthalpy_device_kernel (dfThermo.cu:257-274) and the
+// oracle's h_mix do it (same operation order: the energy gradient is compared bitwise)
+template <int S>
+__device__ __forceinline__ double h_ref(const TC& t, double T, const double* y, long ys) {
+  double h = 0.;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double* a = t.nasa + i * 15;
+    const int o = (T > a[0]) ? 1 : 8;
+    h += (a[o] + a[o + 1] * T / 2 + a[o + 2] * T * T / 3 + a[o + 3] * T * T * T / 4 + a[o + 4] * T * T * T * T / 5 +
+          a[o + 5] / T) * R_GAS * T / t.W[i] * y[i * ys];
+  }
+  return h;
+}
+
+// calculate_energy_gradient_kernel (dfThermo.cu:276-294): on gradientEnergy slots of he,
+// (h(T_c, Y_b) - h(T_c, Y_c)) * deltaCoeffs; 0 on every other slot
+template <int S>
+__global__ void k_energy_gradient(MeshView m, TC t, const int8_t* __restrict__ tyH, const double* __restrict__ T,
+                                  const double* __restrict__ Y, const double* __restrict__ bY, double* __restrict__ eg) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  if (tyH[b] != GRADIENT_ENERGY) { eg[b] = 0.0; return; }
+  const int c = m.bfc[b];
+  const double Tc = T[c];
+  const double hb = h_ref<S>(t, Tc, bY + b, m.B), hc = h_ref<S>(t, Tc, Y + c, m.C);
+  eg[b] = (hb - hc) * m.bdc[b];
+}
+
 }  // namespace
 
 void thermo_upload(Ctx& x) {
@@ -219,6 +248,30 @@ void thermo_upload(Ctx& x) {
   t.dbdiff.upload(t.bdiff, x.stream);
   t.dvc1.upload(t.vc1, x.stream);
   t.dvc2.upload(t.vc2, x.stream);
+}
+
+void thermo_energy_gradient(Ctx& x) {
+  Thermo& th = x.thermo;
+  DFMI_CHECK(th.S == x.S, "thermo coefficients not set or species count mismatch");
+  if (x.B == 0) return;
+  const auto& pt = x.pt("he");
+  bool any = false;
+  for (int p = 0; p < x.P; ++p) any = any || pt[p] == GRADIENT_ENERGY;
+  if (!any) return;   // the field stays zero
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0};
+  MeshView m = x.view();
+#define CALL(NS)                                                                                                  \
+  hipLaunchKernelGGL(k_energy_gradient<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t, x.st("he"), \
+                     x.f("T"), x.f("Y"), x.f("boundary_Y"), x.f("boundary_heGradient"))
+  switch (x.S) {
+    case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break;
+    case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break;
+    case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break; case 13: CALL(13); break;
+    case 14: CALL(14); break; case 15: CALL(15); break; case 16: CALL(16); break;
+    default: throw Error("dfmi: thermo species count " + std::to_string(x.S) + " not instantiated (2..16)");
+  }
+#undef CALL
+  DFMI_HIP(hipGetLastError());
 }
 
 void thermo_correct(Ctx& x, bool from_T) {

@@ -50,6 +50,29 @@ def read_field(path: str):
     return vals, types
 
 
+def read_boundary(path: str) -> dict:
+    """boundaryField of a field file -> {patch: (type, value or None)}; `value uniform v` entries
+    only (scalar or vector)."""
+    txt = _open(path).read()
+    b = txt.find("boundaryField")
+    out = {}
+    if b < 0:
+        return out
+    for pm in re.finditer(r"(\w+)\s*\{([^{}]*)\}", txt[b + len("boundaryField"):]):
+        body = pm.group(2)
+        t = re.search(r"type\s+(\w+);", body)
+        if not t:
+            continue
+        v = re.search(r"value\s+uniform\s+(\([^)]*\)|[^;\s]+)\s*;", body)
+        val = None
+        if v:
+            txtv = v.group(1).strip("()")
+            val = np.array([float(x) for x in txtv.split()])
+            val = val[0] if val.size == 1 else val
+        out[pm.group(1)] = (t.group(1), val)
+    return out
+
+
 def write_field(path: str, name: str, values: np.ndarray, patch_types: dict, dims="[0 0 0 0 0 0 0]"):
     vector = values.ndim == 2
     cls = "volVectorField" if vector else "volScalarField"

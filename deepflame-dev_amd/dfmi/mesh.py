@@ -149,13 +149,29 @@ class Mesh:
         return self.patch_types(default)
 
 
-def _axis_nodes(n: int, length: float, grading: float = 1.0) -> np.ndarray:
-    if grading == 1.0:
-        return np.linspace(0.0, length, n + 1)
-    r = grading ** (1.0 / (n - 1))
-    d = np.array([r ** i for i in range(n)])
-    d = d / d.sum() * length
-    return np.concatenate([[0.0], np.cumsum(d)])
+def _axis_nodes(n: int, length: float, grading=1.0) -> np.ndarray:
+    """Node coordinates of one block edge. `grading` is blockMesh's simpleGrading entry for the
+    axis: an expansion ratio (last / first cell size), or a multi-grading list of sections
+    (length fraction, cell fraction, expansion ratio), e.g. the 1D flame's
+    ((0.55 0.625 1) (0.45 0.375 2)) (test/Tu500K-Phi1/system/blockMeshDict)."""
+    if np.ndim(grading) == 0:
+        grading = [(1.0, 1.0, float(grading))]
+    secs = np.asarray(grading, dtype=np.float64)
+    lf = secs[:, 0] / secs[:, 0].sum()
+    cf = secs[:, 1] / secs[:, 1].sum()
+    counts = np.rint(cf * n).astype(int)
+    counts[-1] = n - counts[:-1].sum()
+    sizes = []
+    for (_, _, ratio), nc, L in zip(secs, counts, lf * length):
+        if nc == 0:
+            continue
+        r = ratio ** (1.0 / (nc - 1)) if nc > 1 else 1.0
+        d = np.array([r ** i for i in range(nc)])
+        sizes.append(d / d.sum() * L)
+    d = np.concatenate(sizes)
+    x = np.concatenate([[0.0], np.cumsum(d)])
+    x[-1] = length
+    return x
 
 
 def hex_box(nx: int, ny: int, nz: int, lengths=(6.283185307179586e-3,) * 3,

@@ -149,6 +149,8 @@ void correct_bc_scalar(const M& m, const int* type, const double* vf, double* bv
     if (t == ZG || t == EXTRAP) bvf[b] = vf[c];
     else if (t == CYCLIC) bvf[b] = interp_b(m.bw[b], vf[c], vf[m.partner_cell[b]]);
     else if (is_proc(t) && !m.primary[b]) bvf[b] = vf[c];
+    else if (t == GRAD_E && has("boundary_heGradient"))   // dfMatrixOpBase.cu:351-366
+      bvf[b] = vf[c] + d("boundary_heGradient")[b] / m.bdc[b];
   }
 }
 void correct_bc_vec(const M& m, const int* type, const double* vf, double* bvf, int ncomp) {
@@ -731,6 +733,20 @@ void thermo_point(const Thermo& th, bool fixT, double& T, double& he, double p, 
   for (int i = 0; i < S; ++i) hai[i * os] = h_species(th, i, T);
 }
 
+// eeqn_calculate_energy_gradient (dfEEqn.cu:266-287 -> calculate_energy_gradient_kernel,
+// dfThermo.cu:276-294): gradientEnergy slots of he get (h(T_c, Y_b) - h(T_c, Y_c)) * deltaCoeffs
+void energy_gradient(const M& m) {
+  const int* the = ia("ptype_he");
+  double *T = d("T"), *Y = d("Y"), *bY = d("boundary_Y"), *eg = d("boundary_heGradient");
+  for (int b = 0; b < m.B; ++b) {
+    eg[b] = 0.0;
+    if (the[m.slot_patch[b]] != GRAD_E) continue;
+    int c = m.bfc[b];
+    double hb = h_mix(g_th, T[c], bY + b, m.B), hc = h_mix(g_th, T[c], Y + c, m.C);
+    eg[b] = (hb - hc) * m.bdc[b];
+  }
+}
+
 // dfThermo::correctThermo (dfThermo.cu:572-671) / updateEnergy (from_T) (:567)
 void thermo_correct(const M& m, bool from_T) {
   const int* tT = ia("ptype_T");
@@ -792,6 +808,7 @@ int orc_y_assemble() { ORC_CALL(y_assemble(m)) }
 int orc_y_inert() { ORC_CALL(y_inert(m)) }
 int orc_e_assemble() { ORC_CALL(e_assemble(m)) }
 int orc_thermo_correct(int from_T) { ORC_CALL(thermo_correct(m, from_T != 0)) }
+int orc_energy_gradient() { ORC_CALL(energy_gradient(m)) }
 int orc_correct_bc(const char* field, const char* bfield, const char* ptype, int ncomp) {
   ORC_CALL(correct_bc_vec(m, ia(ptype), d(field), d(bfield), ncomp))
 }

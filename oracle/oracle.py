@@ -79,6 +79,8 @@ class Oracle:
         self.ptypes = ptypes
         for k, v in state.items():
             self._d(k, v)
+        if "boundary_heGradient" not in self.arr:
+            self._d("boundary_heGradient", np.zeros(m.n_boundary_slots))
         self.L.orc_set_thermo(table.S, _dp(np.ascontiguousarray(table.W)), _dp(np.ascontiguousarray(table.nasa)),
                               _dp(np.ascontiguousarray(table.visc)), _dp(np.ascontiguousarray(table.cond)),
                               _dp(np.ascontiguousarray(table.bdiff)))
@@ -182,6 +184,10 @@ class Oracle:
         self.eeqn = {k: v.copy() for k, v in o.items()}
         return self.eeqn
 
+    def energy_gradient(self):
+        """boundary_heGradient on gradientEnergy slots (dfEEqn.cu:148, :266-287)"""
+        self._run("orc_energy_gradient")
+
     def thermo_correct(self, from_T=False):
         self._run("orc_thermo_correct", 1 if from_T else 0)
 
@@ -267,6 +273,7 @@ class Oracle:
                                        y["diag"][s * C_:(s + 1) * C_], y["source"][s * C_:(s + 1) * C_],
                                        y["internal_coeffs"][s * B:(s + 1) * B], y["boundary_coeffs"][s * B:(s + 1) * B], "Y")
         self.y_inert()
+        self.energy_gradient()                    # dfEEqn.cu:148 (gradientEnergy patches)
         self.correct_bc("he", "he", 1)
         e = self.e_assemble()
         a["he"][...] = self.solve_ldu(e["lower"], e["upper"], e["diag"], e["source"], e["internal_coeffs"],

@@ -1,0 +1,108 @@
+"""BASELINE config 2: the reference's 1D freely-propagating H2/air flame,
+test/Tu500K-Phi1 -- 880 graded cells (multi-grading blockMesh), Burke2012 9 species, inlet fixedValue
+U/T/Y (he fixedEnergy) with p zeroGradient, outlet zeroGradient U/T/Y (he gradientEnergy) with p
+fixed (the case's waveTransmissive outlet, which the reference GPU path rejects), dt 1e-6, initial T
+and species profiles of its 0/ directory (tests/golden/flame1d, copied from the reference).
+
+- one dfLowMachFoam outer iteration vs the oracle with exact solves (same chemistry source on both);
+- the GPU integrator's source terms vs the oracle's SciPy-BDF chemistry on the developed flame front;
+- 200 steps with chemistry: bounded, inlet values held, the front evolves.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup():
+    from dfmi import case
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.kinetics import parse_mechanism
+    from dfmi.lib import Context
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, "Burke2012_s9r23.yaml"))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    mech = parse_mechanism(os.path.join(GOLDEN, "Burke2012_s9r23.yaml"))
+    m = case.flame1d_mesh()
+    pt = case.flame1d_patch_types(m)
+    inert = ym["species"].index("N2")
+    dt = 1e-6
+    ctx = Context(0)
+    case.setup_context(ctx, m, t, inert, dt, pt)
+    ctx.chem_set_mechanism(mech)
+    f, bv = case.flame1d_fields(os.path.join(GOLDEN, "flame1d"), ym["species"])
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], bvals=bv)
+    return ctx, m, t, ym, mech, pt, inert, dt, bv
+
+
+def test_flame1d_outer_iteration_matches_oracle():
+    import oracle as O
+    from dfmi import case
+    ctx, m, t, ym, mech, pt, inert, dt, bv = _setup()
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    ctx.chem_solve(dt)                          # chemistry source on the initial state ...
+    ctx.chem_set_options(0)                     # ... shared by both sides of the comparison
+    for e in ("U", "Y", "E"):
+        ctx.set_solver(e, 300, 1e-15, 1e-300)
+    ctx.set_solver("p", 3000, 1e-15, 1e-300)
+    st = case.pull_state(ctx, m, t.S)
+    o = O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt)
+    o.time_step(2)
+    ctx.time_step(2)
+    for n, tl in {"T": 1e-10, "p": 1e-11, "rho": 1e-10, "he": 1e-10}.items():
+        got = ctx.get_field(n, (m.n_cells,))
+        assert rel_err(got, o[n]) < tl, (n, rel_err(got, o[n]))
+        bgot = ctx.get_field("boundary_" + n, (m.n_boundary_slots,))
+        assert rel_err(bgot, o["boundary_" + n]) < tl, ("boundary_" + n, rel_err(bgot, o["boundary_" + n]))
+    assert rel_err(ctx.get_field("U", (3, m.n_cells)), o["U"]) < 1e-9
+    assert rel_err(ctx.get_field("Y", (t.S, m.n_cells)), o["Y"]) < 1e-9
+    assert rel_err(ctx.get_field("phi", (m.n_faces,)), o["phi"]) < 1e-9
+    # the energy BCs were live: fixedEnergy inlet = h(500 K, inlet Y); gradientEnergy outlet gradient
+    bT = ctx.get_field("boundary_T", (m.n_boundary_slots,))
+    assert bT[case.patch_slots(m, "left")][0] == 500.0
+    eg = ctx.get_field("boundary_heGradient", (m.n_boundary_slots,))
+    assert rel_err(eg, o["boundary_heGradient"]) < 1e-12
+
+
+def test_flame1d_front_chemistry_matches_oracle():
+    from chem_oracle import Kinetics
+    ctx, m, t, ym, mech, pt, inert, dt, bv = _setup()
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    for _ in range(20):                         # let the step profile diffuse into a reaction zone
+        ctx.time_step(2)
+    T = ctx.get_field("T", (m.n_cells,))
+    rho = ctx.get_field("rho", (m.n_cells,))
+    Y = ctx.get_field("Y", (t.S, m.n_cells))
+    front = np.flatnonzero((T > 700.0) & (T < 2300.0))
+    assert front.size >= 3, "no reaction zone"
+    idx = front[:: max(1, front.size // 40)]
+    ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
+    ctx.chem_solve(dt)
+    rr = ctx.get_field("RR", (t.S, m.n_cells))[:, idx]
+    ref = Kinetics(mech, ym["nasa"], ym["W"]).reaction_rates(T[idx], None, rho[idx], Y[:, idx], dt)
+    scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
+    assert (np.abs(rr - ref) / scale).max() < 1e-4
+
+
+def test_flame1d_runs_bounded():
+    from dfmi import case
+    ctx, m, t, ym, mech, pt, inert, dt, bv = _setup()
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    left, right = case.patch_slots(m, "left"), case.patch_slots(m, "right")
+    T0 = ctx.get_field("T", (m.n_cells,))
+    for _ in range(200):
+        ctx.time_step(2)
+    T = ctx.get_field("T", (m.n_cells,))
+    Y = ctx.get_field("Y", (t.S, m.n_cells))
+    assert np.isfinite(T).all() and np.isfinite(Y).all()
+    assert T.min() > 480.0 and T.max() < 2700.0      # (acoustic transients of the fixed-p outlet: ~1 K)
+    assert np.abs(Y.sum(axis=0) - 1.0).max() < 1e-10
+    assert np.abs(T - T0).max() > 100.0                 # the front has moved / spread
+    bT = ctx.get_field("boundary_T", (m.n_boundary_slots,))
+    bY = ctx.get_field("boundary_Y", (t.S, m.n_boundary_slots))
+    bp = ctx.get_field("boundary_p", (m.n_boundary_slots,))
+    assert bT[left][0] == 500.0 and np.array_equal(bY[:, left][:, 0], bv["Y"]["left"])
+    assert bp[right][0] == 101325.0

@@ -60,14 +60,19 @@ def _oracle(m, t, st, pt, inert, dt):
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls"])
 def periodic(request):
     if request.param == "walls":      # non-periodic box: zeroGradient walls (+ fixedValue T/Y/U on two sides)
-        from dfmi.mesh import FIXED_VALUE
+        from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY
 
         def walls(m):
             fv = {}
+            fixed = [i for i, p in enumerate(m.patches) if p.name in ("left", "right")]
             for f in ("U", "T", "Y"):
                 t = m.patch_types(0).copy()
-                t[[i for i, p in enumerate(m.patches) if p.name in ("left", "right")]] = FIXED_VALUE
+                t[fixed] = FIXED_VALUE
                 fv[f] = t
+            # he follows T (OpenFOAM heBoundaryTypes): fixedEnergy where T is fixed, gradientEnergy elsewhere
+            t = m.patch_types(GRADIENT_ENERGY).copy()
+            t[fixed] = FIXED_ENERGY
+            fv["he"] = t
             return fv
         return _case(periodic=False, walls=walls, mech="burke9")
     return _case(mech=request.param)
@@ -149,8 +154,18 @@ def test_y_eqn_assembly_bitwise(periodic):
 
 def test_e_eqn_assembly_bitwise(periodic):
     ctx, m, t, st, pt, inert, dt = periodic
-    o = _oracle(m, t, st, pt, inert, dt)
+    # species on gradientEnergy walls off their cell values, so the energy gradient is non-trivial
+    from dfmi import case
+    from dfmi.mesh import GRADIENT_ENERGY
+    bY = st["boundary_Y"].copy()
+    slot_type = np.repeat(np.asarray(pt["he"]), [p.slots for p in m.patches])
+    ge = slot_type == GRADIENT_ENERGY
+    bY[:, ge] *= 1.0 + 1e-2 * np.random.default_rng(3).standard_normal((t.S, int(ge.sum())))
+    ctx.set_field("boundary_Y", bY)
+    st2 = dict(st, boundary_Y=bY)
+    o = _oracle(m, t, st2, pt, inert, dt)
     o.y_prep()
+    o.energy_gradient()
     o.correct_bc("he", "he", 1)
     ref = o.e_assemble()
     ctx.assemble("Y")
@@ -159,6 +174,10 @@ def test_e_eqn_assembly_bitwise(periodic):
                       m.n_boundary_slots)
     bad = {k: v for k, v in res.items() if v[0] != 0}
     assert not bad, bad
+    assert ulp_diff(ctx.get_field("boundary_heGradient", (m.n_boundary_slots,)), o["boundary_heGradient"]) == 0
+    if ge.any():
+        assert np.abs(o["boundary_heGradient"][ge]).max() > 0
+    case.push_state(ctx, st)
 
 
 def test_thermo_correct(periodic):
