@@ -174,6 +174,38 @@ def host_state(m, table, f):
     return s
 
 
+def flame1d_line(steps=100, warmup=10):
+    """BASELINE config 2: the reference's 1D H2/air flame (test/Tu500K-Phi1, 880 cells, 9 species,
+    direct chemistry, dt 1e-6) on one GPU -- a latency-bound case (one wave of cells), reported
+    beside the headline line, not as it."""
+    from dfmi import case
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.kinetics import parse_mechanism
+    from dfmi.lib import Context
+    golden = os.path.join(ROOT, "tests", "golden")
+    ym = read_yaml_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml"))
+    t = read_thermo_table(os.path.join(golden, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    m = case.flame1d_mesh()
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, case.flame1d_patch_types(m))
+    ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml")))
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    f, bv = case.flame1d_fields(os.path.join(golden, "flame1d"), ym["species"])
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], bvals=bv)
+    for _ in range(warmup):
+        ctx.time_step(2)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.time_step(2)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    ctx.close()
+    return {"workload": "1D freely-propagating H2/air flame (test/Tu500K-Phi1), 880 cells, Burke2012 9 species, "
+                        "direct integration, dt=1e-6, nCorr=2 (BASELINE config 2)",
+            "ms_per_step": el / steps * 1e3, "cell_updates_per_s": m.n_cells * steps / el, "steps": steps}
+
+
 def chem_step_stats(ctx, C):
     """Integrator steps per cell of the last chemistry solve and how evenly 64-lane waves are loaded:
     a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
@@ -344,6 +376,8 @@ def main():
                 if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
     }
+    if rank == 0 and world == 1 and n == 128:
+        out["other_configs"] = {"flame1d": flame1d_line()}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, table, ym, inert)
         out["cpu_baseline"]["ratio"] = value / out["cpu_baseline"]["value"]
