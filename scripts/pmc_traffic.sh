@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu ${BENCH_ARGS} > gpurun_out/pmc_$c.log 2>&1
+  timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-flame ${BENCH_ARGS} > gpurun_out/pmc_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 f=$(find gpurun_out/pmc_FETCH_SIZE -name "*counter_collection.csv" | sort | tail -1)
