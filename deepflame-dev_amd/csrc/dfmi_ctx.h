@@ -72,6 +72,7 @@ struct Dnn {
   double gemm_flops = 0;                  // algorithmic GEMM flops issued since the last query
   DevBuf<int> bc, idx;
   DevBuf<_Float16> x0, h0, h1;
+  DevBuf<float> part;           // fused output layer: per-row partial dot products [net][2 N tiles][chunk]
 };
 
 // per-cell chemistry (chem.hip): mechanism arrays (dfmi/kinetics.py layout) and integrator controls

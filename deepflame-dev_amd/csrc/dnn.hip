@@ -10,11 +10,11 @@
 //
 // MI355X design: the reacting cells are compacted on the device (deterministic scan), then every
 // hidden layer of all S-1 nets is ONE batched GEMM launch (grid.z = net) on MFMA
-// v_mfma_f32_32x32x16_f16 with fp32 accumulation and the bias + exact-erf GELU + fp16 rounding fused
-// into the epilogue; the 1-wide output layer and the BCT post-processing are fused into one kernel.
-// GEMM tile 128x128x32, 4 waves (2x2, 64x64 each = 2x2 MFMA tiles), both operands streamed
+// v_mfma_f32_16x16x32_f16 with fp32 accumulation and the bias + erf GELU + fp16 rounding fused into the
+// epilogue; the 1-wide output layer and the BCT post-processing are fused into one kernel.
+// GEMM tile 256x128x32, 4 waves (2x2, 128x64 each = 8x4 MFMA tiles), both operands streamed
 // global -> LDS by DMA (global_load_lds, swizzled rows) through a 3-buffer ring, A and W both
-// K-contiguous (W in torch Linear [out][in] layout), K and activation row strides padded to 64.
+// K-contiguous (W in torch Linear [out][in] layout), K and activation row strides padded to 32.
 #include "dfmi_ctx.h"
 #include <cmath>
 
@@ -22,24 +22,34 @@ namespace dfmi {
 namespace {
 
 using half8 = __attribute__((ext_vector_type(8))) _Float16;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int BN = 128, BK = 32;
 constexpr int NBUF = 3;                   // LDS ring: two K tiles in flight while one feeds the MFMAs
-constexpr int GT = 256;
-constexpr int KPAD = 64;                  // every GEMM K (and activation row stride) is a multiple of this
-constexpr int TILE_H = BM * BK;           // halves per staged operand tile (8 KiB)
+constexpr int KPAD = 32;                  // every GEMM K (and activation row stride) is a multiple of this
+constexpr int TILE_W = BN * BK;           // halves per staged W tile (8 KiB)
 
-// GELU for the GEMM epilogue: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, branch-free), three
-// orders of magnitude below the fp16 rounding the result goes through (torch's GELU is the exact-erf
-// form); the library erff branches per lane on |x| < 1 and dominated the epilogue of the shallow
-// (K = 11) first layer
-__device__ __forceinline__ float gelu_fast(float v) {
-  const float u = v * 0.70710678118654752440f, a = fabsf(u);
-  const float t = __frcp_rn(1.0f + 0.3275911f * a);
-  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const float e = 1.0f - poly * __expf(-a * a);
-  return 0.5f * v * (1.0f + copysignf(e, u));
+// GELU for the GEMM epilogue, two values at a time: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7,
+// branch-free), three orders of magnitude below the fp16 rounding the result goes through (torch's GELU is
+// the exact-erf form; the library erff branches per lane on |x| < 1). Packed fp32 arithmetic (v_pk_mul_f32 / v_pk_fma_f32, two values per instruction: no MFMA competes for the
+// issue slots in the epilogue), hardware reciprocal and exp2 (<= 1 ulp each; __frcp_rn expands to the
+// correctly-rounded division sequence, which dominated the epilogue), explicit fmas (-ffp-contract=off).
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 v) {
+  const f32x2 u = v * 0.70710678118654752440f;
+  const f32x2 a = __builtin_elementwise_abs(u);
+  const f32x2 d = __builtin_elementwise_fma(a, f32x2(0.3275911f), f32x2(1.0f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 q = __builtin_elementwise_fma(t, f32x2(1.061405429f), f32x2(-1.453152027f));
+  q = __builtin_elementwise_fma(t, q, f32x2(1.421413741f));
+  q = __builtin_elementwise_fma(t, q, f32x2(-0.284496736f));
+  q = __builtin_elementwise_fma(t, q, f32x2(0.254829592f));
+  const f32x2 poly = t * q;
+  const f32x2 w = (a * a) * -1.44269504088896340736f;
+  const f32x2 ex = {__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+  const f32x2 e = __builtin_elementwise_fma(-poly, ex, f32x2(1.0f));
+  const f32x2 hv = v * 0.5f;
+  const f32x2 se = {copysignf(e.x, u.x), copysignf(e.y, u.y)};
+  return __builtin_elementwise_fma(hv, se, hv);
 }
 
 // 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_wave + 16 l
@@ -48,122 +58,164 @@ __device__ __forceinline__ void glds16(const _Float16* g, _Float16* lds_wave) {
                                    (__attribute__((address_space(3))) void*)lds_wave, 16, 0, 0);
 }
 
-// 16-B chunk c (of 4 per 64-B row) of row `row` lives at chunk c ^ ((row >> 2) & 3): the 16 rows a
-// ds_read_b128 lane group reads ({0-3,12-15,20-27}, {4-11,16-19,28-31} of each half-wave) then hit 16
-// distinct bank slots (conflict-free)
-__device__ __forceinline__ int swz(int row, int c) { return c ^ ((row >> 2) & 3); }
+// 16x16x32 operand reads: lane l reads row (l & 15) of a 16-row block at logical chunk (l >> 4). A
+// ds_read_b128 lane group then holds rows {0-3,12-15} at chunk c and rows {4-11} at chunk c ^ 1 (or the
+// converse); chunk c of row r lives at c ^ H((r >> 2) & 3), H = {0, 2, 3, 1}, which puts the four rows of
+// each bank-row position on four distinct 16-B slots (conflict-free)
+__device__ __forceinline__ int swz16(int row, int c) { return c ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
 
 // C[z][M][ldc] = act(A[z][M][lda] . W[z][N][K]^T + b[z][N]) for columns < N, 0 for N <= col < ldc;
-// fp16 in/out, fp32 accumulate. K, lda, ldc multiples of 64.
-// Block tile 128x128x32, 4 waves each owning a 64x64 quadrant (2x2 v_mfma_f32_32x32x16_f16 tiles).
-// Both operand tiles are streamed global -> LDS by DMA (global_load_lds, 16 B per lane, 4 DMA
-// instructions per thread per K tile) through a 3-buffer ring: tiles k+1 and k+2 are in flight while
-// tile k feeds the MFMAs; the wait before each barrier is counted (vmcnt(4): the newest tile stays in
-// flight) and the barrier is a raw s_barrier, so nothing drains the DMA queue inside the loop. The
-// swizzle is applied on the global source address (each DMA still writes 1 KiB contiguously). 48 KiB
-// LDS: three blocks per CU. Block ids are remapped so the consecutive ids that share an XCD walk the
-// N tiles of one M tile (A rows re-read from that XCD's L2).
-template <bool GELU>
-__global__ void __launch_bounds__(GT, 3) k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, int lda,
-                                                    long sA, const _Float16* __restrict__ W, long sW,
-                                                    const float* __restrict__ bias, long sb,
-                                                    _Float16* __restrict__ Cout, int ldc, long sC) {
-  __shared__ __attribute__((aligned(16))) _Float16 lds[NBUF * 2 * TILE_H];   // [buf][A | W][128][32]
+// fp16 in/out, fp32 accumulate, K, lda, ldc multiples of 32.
+// Block tile 256 x 128 x 32, 4 waves (2 x 2) each owning a 128 x 64 tile of 8 x 4 v_mfma_f32_16x16x32_f16
+// accumulators (12 fragment reads per 32 MFMAs: half the LDS read traffic per flop of a 64 x 64 wave tile,
+// twice the MFMA work between barriers). Both operand tiles are streamed global -> LDS by DMA
+// (global_load_lds, 16 B per lane, 6 DMA instructions per wave per K tile) through a 3-buffer ring: tiles
+// k+1 and k+2 are in flight while tile k feeds the MFMAs; the wait before each barrier is counted
+// (vmcnt(6): the newest tile stays in flight) and the barrier is a raw s_barrier, so nothing drains the DMA
+// queue inside the loop. The swizzle is applied on the global source address (each DMA still writes 1 KiB
+// contiguously). 72 KiB LDS: two blocks (8 waves) per CU. Block ids are remapped so the consecutive ids
+// that share an XCD walk the N tiles of one M tile (A rows re-read from that XCD's L2).
+//
+// OUT (the last hidden layer): the net's 1-wide output layer is fused into the epilogue instead of storing
+// the tile -- each fp16-rounded activation is multiplied by its output weight wo[col] and the products are
+// summed per row (fp32, fixed order: over the lane's 4 columns, then a 16-lane xor tree); the two waves of
+// a row band write separate partial sums P[z][2 tile_n + wave_n][M], which k_dnn_output adds in order.
+template <bool GELU, bool OUT>
+__global__ void __launch_bounds__(256, 2)
+    k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
+               long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
+               const _Float16* __restrict__ wo, long swo, float* __restrict__ P, long sP) {
+  constexpr int BMW = 256, GTW = 256;
+  constexpr int TILE_A = BMW * BK, STAGE = TILE_A + TILE_W;
+  using f32x4 = __attribute__((ext_vector_type(4))) float;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[NBUF * STAGE];   // [buf][A (256 x 32) | W (128 x 32)]
   const int z = blockIdx.z;
-  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
-  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM, nwg = ntn * ntm;
+  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC; wo += z * swo; P += z * sP;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  const int m0 = (wg / ntn) * BMW, n0 = (wg % ntn) * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // staging: wave w fills rows [32 w, 32 w + 32) of both tiles, 16 rows (1 KiB) per DMA instruction
-  const _Float16* pa[2];
+  // staging: wave w fills A rows [64 w, 64 w + 64) and W rows [32 w, 32 w + 32), 16 rows per DMA
+  const _Float16* pa[4];
   const _Float16* pw[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 64 + i * 16 + (lane >> 2);
+    pa[i] = A + (long)min(m0 + row, M - 1) * lda + swz16(row, lane & 3) * 8;   // clamped rows masked on store
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = wave * 32 + i * 16 + (lane >> 2);
-    const int gc = swz(row, lane & 3);
-    const int ga = min(m0 + row, M - 1), gw = min(n0 + row, N - 1);   // clamped rows are masked on store
-    pa[i] = A + (long)ga * lda + gc * 8;
-    pw[i] = W + (long)gw * K + gc * 8;
+    pw[i] = W + (long)min(n0 + row, N - 1) * K + swz16(row, lane & 3) * 8;
   }
   auto stage = [&](int buf, int k0) {
-    _Float16* la = lds + buf * 2 * TILE_H;
-    _Float16* lw = la + TILE_H;
+    _Float16* la = lds + buf * STAGE;
+    _Float16* lw = la + TILE_A;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(pa[i] + k0, la + (wave * 32 + i * 16) * BK);
+    for (int i = 0; i < 4; ++i) glds16(pa[i] + k0, la + (wave * 64 + i * 16) * BK);
 #pragma unroll
     for (int i = 0; i < 2; ++i) glds16(pw[i] + k0, lw + (wave * 32 + i * 16) * BK);
   };
-  f32x16 acc[2][2];
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int r = lane & 31, h = lane >> 5;
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 64;
+  const int r = lane & 15, c = lane >> 4;
   const int nk = K / BK;
   stage(0, 0);
   if (nk > 1) stage(1, BK);
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's DMAs; the newer tile may stay in flight), then the barrier makes
-    // every wave's DMAs visible and frees the buffer read in iteration kt-1
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
-    const _Float16* la = lds + cur * 2 * TILE_H;
-    const _Float16* lw = la + TILE_H;
+    const _Float16* la = lds + cur * STAGE;
+    const _Float16* lw = la + TILE_A;
+    half8 af[8], bf[4];
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const int c = ks * 2 + h;   // logical 16-B chunk of this lane's 8 k values
-      half8 af[2], bf[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wm + 32 * i + r;
-        af[i] = *reinterpret_cast<const half8*>(la + row * BK + swz(row, c) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wn + 32 * j + r;
-        bf[j] = *reinterpret_cast<const half8*>(lw + row * BK + swz(row, c) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int row = wn + 16 * j + r;
+      bf[j] = *reinterpret_cast<const half8*>(lw + row * BK + swz16(row, c) * 8);
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wm + 16 * i + r;
+      af[i] = *reinterpret_cast<const half8*>(la + row * BK + swz16(row, c) * 8);
+    }
+    // all 12 fragment reads issued before the first MFMA (counted lgkmcnt waits follow): left to itself the
+    // compiler re-reads A two fragments at a time behind lgkmcnt(0), exposing the LDS latency 4x per tile
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     cur = cur == NBUF - 1 ? 0 : cur + 1;
   }
-  // epilogue: bias + GELU in registers (C/D map col = lane & 31, row = (e & 3) + 8 (e >> 2) +
-  // 4 (lane >> 5)), the fp16 tile staged through LDS, written back as 16-B row chunks
-  __syncthreads();   // every wave is done with the ring (no DMA outstanding after the last wait)
-  constexpr int CLD = BN + 8;   // halves per LDS row of the output tile (row starts 16-B aligned)
-  static_assert(BM * CLD <= NBUF * 2 * TILE_H, "output tile must fit the staging ring");
+  // epilogue: bias + GELU in registers (C/D map col = lane & 15, row = 4 (lane >> 4) + e)
+  if constexpr (OUT) {
+    float bv[4], wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      bv[j] = col < N ? bias[col] : 0.0f;
+      wv[j] = col < N ? (float)wo[col] : 0.0f;   // dead columns contribute 0
+    }
+    float* Pw = P + (long)(2 * (wg % ntn) + (wave & 1)) * M;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        f32x2 sacc = {0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x2 v = f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j];
+          if (GELU) v = gelu_fast2(v);
+          const f32x2 hq = {(float)(_Float16)v.x, (float)(_Float16)v.y};   // the fp16 activation
+          sacc = __builtin_elementwise_fma(hq, f32x2(wv[j]), sacc);
+        }
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) {
+          sacc.x += __shfl_xor(sacc.x, off);
+          sacc.y += __shfl_xor(sacc.y, off);
+        }
+        const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+        if ((lane & 15) == 0) {
+          if (row < M) Pw[row] = sacc.x;
+          if (row + 1 < M) Pw[row + 1] = sacc.y;
+        }
+      }
+    return;
+  }
+  // the fp16 tile staged through LDS, written back as 16-B row chunks
+  __syncthreads();
+  constexpr int CLD = BN + 8;
+  static_assert(BMW * CLD <= NBUF * STAGE, "output tile must fit the staging ring");
   _Float16* cs = lds;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int cl = wn + 32 * j + (lane & 31), col = n0 + cl;
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
     const bool live = col < N;
     const float bv = live ? bias[col] : 0.0f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rl = wm + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        float v = acc[i][j][e] + bv;
-        if (GELU) v = gelu_fast(v);
-        cs[rl * CLD + cl] = live ? (_Float16)v : (_Float16)0.0f;
+      for (int e = 0; e < 4; e += 2) {
+        const int rl = wm + 16 * i + 4 * (lane >> 4) + e;
+        f32x2 v = f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv;
+        if (GELU) v = gelu_fast2(v);
+        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
+        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
       }
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < BM * BN / 8 / GT; ++it) {
-    const int idx = tid + it * GT, rl = idx / (BN / 8), ch = idx % (BN / 8);
+  for (int it = 0; it < BMW * BN / 8 / GTW; ++it) {
+    const int idx = tid + it * GTW, rl = idx / (BN / 8), ch = idx % (BN / 8);
     const int row = m0 + rl, col = n0 + ch * 8;
     if (row < M && col < ldc)
       *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
@@ -227,27 +279,19 @@ __global__ void k_dnn_input(int n, int C, int S, int Kp, const int* __restrict__
 }
 
 // output layer (K -> 1) of every net + calculate_y_new + calculate_RR
-__global__ void k_dnn_output(int n, int C, int S, int K, int ldh, int nmod, const int* __restrict__ idx,
-                             const _Float16* __restrict__ H, long sH, const _Float16* __restrict__ w, long sw,
-                             const float* __restrict__ b, const double* __restrict__ Ymu,
-                             const double* __restrict__ Ystd, const double* __restrict__ Y,
-                             const double* __restrict__ rho, const double* __restrict__ p, double dt,
-                             double* __restrict__ RR) {
+__global__ void k_dnn_output(int n, int C, int S, int nq, int nmod, const int* __restrict__ idx,
+                             const float* __restrict__ P, long sP, const float* __restrict__ b,
+                             const double* __restrict__ Ymu, const double* __restrict__ Ystd,
+                             const double* __restrict__ Y, const double* __restrict__ rho,
+                             const double* __restrict__ p, double dt, double* __restrict__ RR) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int c = idx[i];
   double yn[32];
   double sum = 0.0;
   for (int m = 0; m < nmod; ++m) {
-    const _Float16* hr = H + m * sH + (long)i * ldh;
-    const _Float16* wm = w + m * sw;
     float a = 0.0f;
-    for (int k = 0; k < K; k += 8) {
-      const half8 hv = *reinterpret_cast<const half8*>(hr + k);
-      const half8 wv = *reinterpret_cast<const half8*>(wm + k);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a += (float)hv[j] * (float)wv[j];
-    }
+    for (int q = 0; q < nq; ++q) a += P[m * sP + (long)q * n + i];   // the GEMM's partial dot products, in order
     const double out = (double)(_Float16)(a + b[m]);   // the net's fp16 output, as .to(kDouble)
     const double ybct = (pow(Y[(long)m * C + c], 0.1) - 1.0) * 10.0;
     const double v = out * Ystd[m] + Ymu[m] + ybct;
@@ -349,25 +393,32 @@ void dnn_solve(Ctx& x) {
     long sIn = 0;
     _Float16* bufs[2] = {d.h0.p, d.h1.p};
     int lda = d.Kp[0];
+    const int nq = 2 * blocks_for(d.dims[L - 1], BN);   // partial sums per row of the fused output layer
+    const long sP = (long)nq * n;
+    if (d.part.n < (size_t)d.nmod * sP) d.part.alloc((size_t)d.nmod * sP);
     for (int l = 0; l + 1 < L; ++l) {
       const int N = d.dims[l + 1], K = d.Kp[l], ldc = d.Kp[l + 1];
       _Float16* out = bufs[l & 1];
       d.gemm_flops += 2.0 * n * N * d.dims[l] * d.nmod;   // algorithmic flops (unpadded K)
-      const dim3 g(blocks_for(N, BN) * blocks_for(n, BM), 1, d.nmod);
+      const dim3 g(blocks_for(N, BN) * blocks_for(n, 256), 1, d.nmod);
       KScope _ks(x, "k_mlp_gemm");
-      hipLaunchKernelGGL(k_mlp_gemm<true>, g, dim3(GT), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K,
-                         d.b[l].p, (long)N, out, ldc, (long)n * ldc);
+      if (l + 2 == L) {   // last hidden layer: the output layer fused into the epilogue
+        d.gemm_flops += 2.0 * n * N * d.nmod;
+        hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+                           (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
+                           d.part.p, sP);
+      } else {
+        hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+                           (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
+      }
       DFMI_HIP(hipGetLastError());
       in = out;
       sIn = (long)n * ldc;
       lda = ldc;
     }
-    const int K = d.dims[L - 1];
-    DFMI_CHECK(K % 8 == 0, "DNN: output layer width");
     KScope _ks(x, "k_dnn_output");
-    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, K, lda, d.nmod, idx,
-                       in, sIn, d.W[L - 1].p, (long)d.Kp[L - 1], d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"),
-                       x.f("rho"), x.f("p"), d.dt, RR);
+    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, nq, d.nmod, idx,
+                       d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f("rho"), x.f("p"), d.dt, RR);
     DFMI_HIP(hipGetLastError());
   }
 }
