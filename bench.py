@@ -52,8 +52,9 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
         # ELL gather stores the same 2 x 12 B per face from the two cells' sides); coupled slots 12 B
         return C * 40.0 + F * 24.0 + Bc * 12.0
     if kernel == "k_bcg_spmv":
-        # out = A in (+ dot with r0 or s): cells dS, in, out, dot partner (32 B); matrix as above
-        return C * 32.0 + F * 24.0 + Bc * 12.0
+        # mean of the two SpMVs of an iteration: v = A p reads dS, p, r0, writes v (32 B / cell);
+        # t = A s with s = r - alpha v formed on the fly reads dS, r, v, r0, writes t (40 B); matrix as above
+        return C * 36.0 + F * 24.0 + Bc * 12.0
     if kernel == "k_thermo_cells":
         # T, he, p in; Y in (S); T, psi, rho, mu, alpha out; rhoD, hai out (S each)
         return C * 8.0 * (3 + S + 5 + 2 * S)

@@ -228,59 +228,74 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
   block_partials<1>(acc, partial, s);
 }
 
-// prologue: alpha = rho / (r0.v); s = r - alpha v; partial r0.s
-__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b, double* partial) {
+// multi-rank only: s = r - alpha v into sv, whose processor-boundary values the halo exchange sends
+__global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double* scal, BV b) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
   double v[1];
   red_sum<1>(red, s, v);
   const double alpha = v[0] != 0.0 ? st[0] / v[0] : 0.0;
-  if (leader()) st[2] = alpha;
-  double acc[1] = {0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double sv = b.r[i] - alpha * b.v[i];
-    b.sv[i] = sv;
-    acc[0] += b.r0[i] * sv;
+    b.sv[i] = b.r[i] - alpha * b.v[i];
   }
-  block_partials<1>(acc, partial, s);
 }
 
-// t = D^-1 A s; partials (t.s, t.t, r0.t)
+// prologue: alpha = rho / (r0.v). s = r - alpha v is formed on the fly (own cell and every neighbour:
+// the gathers of r and v hit the same lines as the own-cell reads of other threads), so no kernel writes
+// s and nothing re-reads it; halo entries (processor neighbours, j >= C) read the exchanged copy sv.
+// t = D^-1 A s; partials (t.s, t.t, r0.t, r0.s)
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W, const int* __restrict__ col,
-                                                   const double* __restrict__ val, const double* scal, BV b,
+__global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, const int* __restrict__ col,
+                                                   const double* __restrict__ val, Red red, double* scal, BV b,
                                                    double* partial) {
   const int s = blockIdx.y;
-  if (scal[s * NSCAL + 6] == 0.0) return;   // uniform per block
+  double* st = scal + s * NSCAL;
+  if (st[6] == 0.0) return;   // uniform per block
+  double v1[1];
+  red_sum<1>(red, s, v1);
+  const double alpha = v1[0] != 0.0 ? st[0] / v1[0] : 0.0;
+  if (leader()) st[2] = alpha;
+  const int W = WT > 0 ? WT : W_;
   const double* vs = val + (long)s * W * C;
-  double acc[3] = {0.0, 0.0, 0.0};
+  const double* rs = b.r + s * Ce;
+  const double* ws = b.v + s * Ce;
+  const double* hs = b.sv + s * Ce;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double* sv = b.sv + s * Ce;
-    const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], sv, c);
+    const double sc = rs[c] - alpha * ws[c];
+    double o = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int j = col[k * C + c];
+      const double sj = j < C ? rs[j] - alpha * ws[j] : hs[j];
+      o += vs[k * C + c] * sj;
+    }
+    const double y = sc + o / b.dS[i];
     b.t[i] = y;
-    acc[0] += y * sv[c];
+    const double r0 = b.r0[i];
+    acc[0] += y * sc;
     acc[1] += y * y;
-    acc[2] += b.r0[i] * y;
+    acc[2] += r0 * y;
+    acc[3] += r0 * sc;
   }
-  block_partials<3>(acc, partial, s);
+  block_partials<4>(acc, partial, s);
 }
 
 // prologue: omega = (t.s)/(t.t); rho_new = r0.s - omega r0.t; beta = (rho_new / rho)(alpha / omega);
 // x += alpha p + omega s; r = s - omega t; p = r + beta (p - omega v); partials (||D r||^2, 0)
-__global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_s, Red red_t, Sys q,
-                                                const int* __restrict__ sys_map, double* scal, BV b, double* partial) {
+__global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys q, const int* __restrict__ sys_map,
+                                                double* scal, BV b, double* partial) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
-  double r0s[1], tv[3];
-  red_sum<1>(red_s, s, r0s);
-  red_sum<3>(red_t, s, tv);
+  double tv[4];
+  red_sum<4>(red_t, s, tv);
   const double omega = tv[1] != 0.0 ? tv[0] / tv[1] : 0.0;
   const double alpha = st[2], rho = st[0];
-  const double rho_new = r0s[0] - omega * tv[2];
+  const double rho_new = tv[3] - omega * tv[2];
   const double beta = (rho != 0.0 && omega != 0.0) ? (rho_new / rho) * (alpha / omega) : 0.0;
   if (leader()) { st[3] = omega; st[1] = rho; st[0] = rho_new; }
   const int ms = sys_map ? sys_map[s] : s;
@@ -288,11 +303,12 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_s, Red 
   double acc[2] = {0.0, 0.0};
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
-    const double pv = b.p[i], sv = b.sv[i];
+    const double pv = b.p[i], vv = b.v[i];
+    const double sv = b.r[i] - alpha * vv;   // the s of k_bcg_spmv2, same expression
     xv[c] = xv[c] + alpha * pv + omega * sv;
     const double rr = sv - omega * b.t[i];
     b.r[i] = rr;
-    b.p[i] = rr + beta * (pv - omega * b.v[i]);
+    b.p[i] = rr + beta * (pv - omega * vv);
     const double tr = b.dS[i] * rr;
     acc[0] += tr * tr;
   }
@@ -440,14 +456,15 @@ struct Launch {
   // reductions that are alive at the same time)
   Red after(double* partial, int NV, int slot = 0) {
     if (x.nranks == 1) return Red{partial, nblk, NV, (long)nblk * NV};
-    const size_t per = (size_t)nsys * 4;   // up to 3 values per system per slot
+    const size_t per = (size_t)nsys * 4;   // up to 4 values per system per slot
     if (x.ws.red_local.n < 2 * per) x.ws.red_local.alloc(2 * per);
     if (x.ws.red_all.n < 2 * per * x.nranks) x.ws.red_all.alloc(2 * per * x.nranks);
     double* loc = x.ws.red_local.p + slot * per;
     double* all = x.ws.red_all.p + slot * per * x.nranks;
     if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
     else if (NV == 2) hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
-    else hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    else if (NV == 3) hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    else hipLaunchKernelGGL(k_red_local<4>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
     DFMI_HIP(hipGetLastError());
     halo_allgather(x, loc, all, (long)nsys * NV);
     return Red{all, x.nranks, (long)nsys * NV, NV};
@@ -598,8 +615,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   // one partial buffer per reduction site (a converged system's last sums stay intact)
   double* pR = val + (size_t)nsys * W * C;          // (||D r||^2, rho0 | 0): init, xp
   double* pV = pR + (size_t)nsys * nblk * 2;        // r0.v
-  double* pS = pV + (size_t)nsys * nblk;            // r0.s
-  double* pT = pS + (size_t)nsys * nblk;            // (t.s, t.t, r0.t)
+  double* pT = pV + (size_t)nsys * nblk;            // (t.s, t.t, r0.t, r0.s)
   Sys q{lower, upper, diag, source, ic, bc, lstride, ustride, dstride, sstride, bstride, xsol, xstride};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
@@ -630,16 +646,17 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     });
     if (it >= cfg.max_iter) break;
     red = L.after(pV, 1);
-    { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b, pS); }
-    const Red red_s = L.after(pS, 1, 1);
-    halo_vecs(x, {b.sv}, nsys, Ce);
+    if (halo_active(x)) {   // processor neighbours read s from the exchanged sv
+      { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
+      halo_vecs(x, {b.sv}, nsys, Ce);
+    }
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, WS.scal.p, b, pT);
+      hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, red, WS.scal.p, b, pT);
     });
-    const Red red_t = L.after(pT, 3, 0);
-    { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_bcg_xp, g, bl, 0, x.stream, C, Ce, red_s, red_t, q, smap, WS.scal.p, b, pR); }
+    const Red red_t = L.after(pT, 4, 0);
+    { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_bcg_xp, g, bl, 0, x.stream, C, Ce, red_t, q, smap, WS.scal.p, b, pR); }
     DFMI_HIP(hipGetLastError());
     red = L.after(pR, 2, 0);
     if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
