@@ -163,7 +163,9 @@ __global__ void k_copy_x(long C, long Ce, Sys q, const int* __restrict__ sys_map
 // r = s - omega t, p = r + beta (p - omega v) -- rho_new = r0.r comes from the recurrence
 // r0.s - omega r0.t, whose two dot products the previous kernels already reduced, so the next
 // direction is formed in the same pass as the solution update.
-// scal[s*16 + k]: 0 rho, 1 rho_old, 2 alpha, 3 omega, 4 res0, 5 res, 6 active, 7 iters
+// scal[s*16 + k]: 0 rho, 1 rho_old, 2 alpha, 3 omega, 4 res0, 5 res, 6 active, 7 iters, 8 rho_new (the
+// update kernel writes it, the next SpMV publishes it as rho: no scalar is rewritten by the kernel whose
+// other blocks read it)
 struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; };
 constexpr int BCG_VECS = 9;
 
@@ -208,11 +210,12 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
   double v2[2];
   red_sum<2>(red, s, v2);
   const double res = sqrt(v2[0]);
-  const double rho = it == 0 ? v2[1] : st[0];
+  const double rho = it == 0 ? v2[1] : st[8];   // r0.r: initial, or the previous update's recurrence
   const double res0 = it == 0 ? res : st[4];
   const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || st[3] == 0.0));
   if (leader()) {
-    if (it == 0) { st[4] = res; st[0] = rho; }
+    if (it == 0) st[4] = res;
+    st[0] = rho;
     st[5] = res; st[7] = it;
     st[6] = stop ? 0.0 : 1.0;
   }
@@ -297,7 +300,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys 
   const double alpha = st[2], rho = st[0];
   const double rho_new = tv[3] - omega * tv[2];
   const double beta = (rho != 0.0 && omega != 0.0) ? (rho_new / rho) * (alpha / omega) : 0.0;
-  if (leader()) { st[3] = omega; st[1] = rho; st[0] = rho_new; }
+  if (leader()) { st[3] = omega; st[1] = rho; st[8] = rho_new; }   // st[0] is read by every block of this kernel
   const int ms = sys_map ? sys_map[s] : s;
   double* xv = q.x + ms * q.xstride;
   double acc[2] = {0.0, 0.0};
