@@ -19,7 +19,22 @@ MECHS = {"es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt"),
          "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt")}
 
 
-def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80"):
+def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
+    """a walled hex box whose interior points are moved by up to `amp` cells at random (non-orthogonal,
+    non-planar faces), written as constant/polyMesh and read back through dfmi.polymesh"""
+    import tempfile
+    from dfmi.polymesh import hex_polymesh, read_polymesh, write_polymesh
+    P, faces, own, nei, bnd = hex_polymesh(nx, ny, nz, lengths=lengths, periodic=(False,) * 3)
+    h = np.array(lengths) / np.array([nx, ny, nz])
+    inner = np.all((P > 1e-12) & (P < np.array(lengths) - 1e-12), axis=1)
+    P = P.copy()
+    P[inner] += amp * h * np.random.default_rng(seed).uniform(-1, 1, (inner.sum(), 3))
+    with tempfile.TemporaryDirectory() as d:
+        write_polymesh(d, P, faces, own, nei, bnd)
+        return read_polymesh(d)
+
+
+def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi.lib import Context
@@ -27,7 +42,10 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
     ym = read_yaml_mechanism(os.path.join(GOLDEN, MECHS[mech][0]))
     t = read_thermo_table(os.path.join(GOLDEN, MECHS[mech][1]), ym["species"])
     L = 1e-3
-    m = hex_box(nx, ny, nz, lengths=(2 * np.pi * L,) * 3, periodic=(periodic,) * 3, gradings=gradings)
+    if distorted:
+        m = _distorted_mesh(nx, ny, nz, (2 * np.pi * L,) * 3)
+    else:
+        m = hex_box(nx, ny, nz, lengths=(2 * np.pi * L,) * 3, periodic=(periodic,) * 3, gradings=gradings)
     ctx = Context(0)
     pt = case.default_patch_types(m)
     if walls:
@@ -57,9 +75,9 @@ def _oracle(m, t, st, pt, inert, dt):
     return O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt)
 
 
-@pytest.fixture(scope="module", params=["es80", "burke9", "walls"])
+@pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted"])
 def periodic(request):
-    if request.param == "walls":      # non-periodic box: zeroGradient walls (+ fixedValue T/Y/U on two sides)
+    if request.param in ("walls", "distorted"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
         from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY
 
         def walls(m):
@@ -74,7 +92,8 @@ def periodic(request):
             t[fixed] = FIXED_ENERGY
             fv["he"] = t
             return fv
-        return _case(periodic=False, walls=walls, mech="burke9")
+        # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
+        return _case(periodic=False, walls=walls, mech="burke9", distorted=request.param == "distorted")
     return _case(mech=request.param)
 
 
