@@ -208,6 +208,62 @@ def flame1d_line(steps=100, warmup=10):
             "ms_per_step": el / steps * 1e3, "cell_updates_per_s": m.n_cells * steps / el, "steps": steps}
 
 
+def dnn53_line(m, T, p, steps=3, warmup=1):
+    """BASELINE config 4's surrogate shape: 53 species, 52 DF-ODENet nets [55, 1600, 800, 400, 1]
+    (the repository has no 53-species mechanism or trained nets: seeded N(0, 1/fan_in) weights, Dirichlet-like
+    mass fractions, synthetic normalisation), on the headline's 2M-cell mesh and temperature field (cells at
+    T >= 610 K infer). The FV kernels are instantiated for <= 16 species, so this line times the surrogate
+    alone: chem-integrations/s = reacting cells inferred per second."""
+    import numpy as np
+    from dfmi import case, dnn_model
+    from dfmi.lib import Context
+    S = 53
+    C = m.n_cells
+    rng = np.random.default_rng(0)
+    Y = rng.gamma(0.3, 1.0, (S, C))
+    Y /= Y.sum(axis=0)
+    Wm = 1.0 / (Y / np.linspace(2.0, 44.0, S)[:, None]).sum(axis=0)
+    rho = p * Wm / (8314.46261815324 * T)
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    pt = case.default_patch_types(m)
+    rows, cols = m.proc_rows_cols()
+    ctx.set_constant_values(C, C, m.n_faces, m.n_boundary_slots, m.n_patches, int(rows.size), m.patch_sizes, S, 1e6)
+    ctx.set_cyclic_info(m.cyclic_neighbour())
+    ctx.set_constant_indexes(m.owner, m.neighbour, rows, cols, 0)
+    ctx.init_constant_fields_internal(m.sf, m.mag_sf, m.weight, m.delta_coeffs, m.volume, m.mesh_distance)
+    bsf, bmag, bdc, bw, bfc = m.boundary_arrays()
+    ctx.init_constant_fields_boundary(bsf, bmag, bdc, bw, bfc, pt["calculated"], pt["extrapolated"])
+    ctx.set_inert_index(S - 1)
+    dims = [S + 2, 1600, 800, 400, 1]
+    ctx.dnn_set_model(dims, dnn_model.seeded_weights(n_modules=S - 1, dims=dims), np.zeros(S + 2), np.ones(S + 2),
+                      np.zeros(S - 1), np.full(S - 1, 0.01))
+    ctx.chem_set_options(2)
+    for n_, v in (("T", T), ("p", p), ("rho", rho), ("Y", Y)):
+        ctx.set_field(n_, v)
+    del Y
+    for _ in range(warmup):
+        ctx.dnn_infer()
+    ctx.kernel_timer("k_mlp_gemm")
+    ctx.dnn_stats()
+    ctx.sync()
+    t0 = time.perf_counter()
+    nr = 0
+    for _ in range(steps):
+        nr = ctx.dnn_infer()
+    ctx.sync()
+    el = time.perf_counter() - t0
+    gemm_ms, gemm_n = ctx.kernel_time("k_mlp_gemm")
+    _, flops = ctx.dnn_stats()
+    ctx.close()
+    tf = flops / (gemm_ms / 1e3) / 1e12 if gemm_ms > 0 else None
+    return {"workload": "DF-ODENet surrogate alone, 53 species (52 nets [55,1600,800,400,1], seeded weights), "
+                        "2097152-cell mesh with the headline T field (BASELINE config 4 shape)",
+            "metric": "chem-integrations/s", "value": nr * steps / el, "reacting_cells": nr,
+            "ms_per_inference": el / steps * 1e3, "gemm_ms_per_inference": gemm_ms / steps,
+            "mfma_roofline": {"bound": "mfma", "achieved": tf, "peak": 2500.0, "unit": "TFLOP/s",
+                              "frac": tf / 2500.0 if tf else None}}
+
+
 def chem_step_stats(ctx, C):
     """Integrator steps per cell of the last chemistry solve and how evenly 64-lane waves are loaded:
     a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
@@ -272,6 +328,7 @@ def main():
     else:
         f = case.tgv_fields(m, ym["species"])
     case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
+    T0, p0 = f["T"].copy(), f["p"].copy()
     del f
 
     for _ in range(args.warmup):
@@ -387,12 +444,12 @@ def main():
                 if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
     }
+    ctx.close()
     if rank == 0 and world == 1 and n == 128 and not args.no_flame:
-        out["other_configs"] = {"flame1d": flame1d_line()}
+        out["other_configs"] = {"flame1d": flame1d_line(), "dnn53": dnn53_line(m, T0, p0)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, table, ym, inert)
         out["cpu_baseline"]["ratio"] = value / out["cpu_baseline"]["value"]
-    ctx.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -287,7 +287,7 @@ __global__ void k_dnn_output(int n, int C, int S, int nq, int nmod, const int* _
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int c = idx[i];
-  double yn[32];
+  double yn[63];
   double sum = 0.0;
   for (int m = 0; m < nmod; ++m) {
     float a = 0.0f;
@@ -315,7 +315,7 @@ __global__ void k_zero(long n, double* __restrict__ v) {
 void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* params, const double* xmu,
                 const double* xstd, const double* ymu, const double* ystd, double T_react, double dt_infer) {
   Dnn& d = x.dnn;
-  DFMI_CHECK(nmod == x.S - 1 && nmod <= 32, "DNN: one net per non-inert species (S - 1 <= 32) expected");
+  DFMI_CHECK(nmod == x.S - 1 && nmod <= 63, "DNN: one net per non-inert species (S - 1 <= 63) expected");
   DFMI_CHECK(nlayers >= 2 && nlayers <= 8, "DNN: 2..8 linear layers supported");
   DFMI_CHECK(dims[0] == x.S + 2 && dims[nlayers] == 1, "DNN: input must be S + 2 wide and output 1 wide");
   DFMI_CHECK(x.inert == x.S - 1, "DNN: the reference layout needs the inert species last");
