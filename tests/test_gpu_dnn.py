@@ -99,3 +99,67 @@ def test_dnn_matches_torch_fp32():
     assert np.all(np.isfinite(RR))
     assert np.median(err) < 2e-3, np.median(err)
     assert err.max() < 2e-2, err.max()
+
+
+def test_dnn_53_species_matches_torch_fp32():
+    """BASELINE config 4's surrogate shape: 53 species, 52 nets [55, 1600, 800, 400, 1] with
+    seeded weights and synthetic normalisation, on a small mesh; the context takes 53 species for the
+    surrogate path (the FV kernels are not instantiated for it)."""
+    import torch
+    from dfmi.mesh import hex_box
+    from dfmi.lib import Context
+    from dfmi import case, dnn_model
+    S = 53
+    m = hex_box(8, 8, 4)
+    C = m.n_cells
+    ctx = Context(0)
+    pt = case.default_patch_types(m)
+    rows, cols = m.proc_rows_cols()
+    ctx.set_constant_values(C, C, m.n_faces, m.n_boundary_slots, m.n_patches, int(rows.size), m.patch_sizes, S, 1e6)
+    ctx.set_cyclic_info(m.cyclic_neighbour())
+    ctx.set_constant_indexes(m.owner, m.neighbour, rows, cols, 0)
+    ctx.init_constant_fields_internal(m.sf, m.mag_sf, m.weight, m.delta_coeffs, m.volume, m.mesh_distance)
+    bsf, bmag, bdc, bw, bfc = m.boundary_arrays()
+    ctx.init_constant_fields_boundary(bsf, bmag, bdc, bw, bfc, pt["calculated"], pt["extrapolated"])
+    ctx.set_inert_index(S - 1)
+    dims = [S + 2, 1600, 800, 400, 1]
+    mods = dnn_model.seeded_weights(n_modules=S - 1, dims=dims, seed=2)
+    xmu, xstd = np.zeros(S + 2), np.ones(S + 2)
+    xmu[0], xstd[0], xmu[1], xstd[1] = 1300.0, 400.0, 101325.0, 1.0
+    ymu, ystd = np.zeros(S - 1), np.full(S - 1, 0.01)
+    ctx.dnn_set_model(dims, mods, xmu, xstd, ymu, ystd)
+    rng = np.random.default_rng(4)
+    Y = rng.gamma(0.3, 1.0, (S, C)) + 1e-8
+    Y /= Y.sum(axis=0)
+    T = 300.0 + 2200.0 * rng.random(C)
+    p = 101325.0 * (1 + 0.05 * rng.standard_normal(C))
+    rho = p / (300.0 * T)
+    for n, v in (("T", T), ("p", p), ("rho", rho), ("Y", Y)):
+        ctx.set_field(n, v)
+    nr = ctx.dnn_infer()
+    react = T >= 610.0
+    assert nr == int(react.sum())
+    RR = ctx.get_field("RR", (S, C))
+    ctx.close()
+    # torch fp32 restatement (dfChemistrySolver.cu:4-75 with these normalisation constants)
+    Yr = Y[:, react]
+    bct = (Yr ** 0.1 - 1) * 10
+    x = np.concatenate([T[react][None, :], np.full((1, react.sum()), 101325.0), bct], axis=0).T
+    xt = torch.tensor((x - xmu) / xstd, dtype=torch.float32)
+    yn = np.zeros((S - 1, react.sum()))
+    for k, layers in enumerate(mods):
+        h = xt
+        for l, (W, b) in enumerate(layers):
+            h = h @ torch.tensor(W).T + torch.tensor(b)
+            if l < len(layers) - 1:
+                h = torch.nn.functional.gelu(h)
+        out = h[:, 0].double().numpy()
+        yn[k] = ((out * ystd[k] + ymu[k] + bct[k]) * 0.1 + 1) ** 10
+    yn = yn / (yn.sum(axis=0) + Yr[S - 1])
+    ref = np.zeros((S, C))
+    ref[:S - 1, react] = (yn - Yr[:S - 1]) * rho[react] * (p[react] / 101325.0) / 1e-6
+    assert np.all(RR[:, ~react] == 0.0) and np.all(np.isfinite(RR))
+    scale = np.abs(ref).max(axis=1, keepdims=True)[:S - 1]
+    err = np.abs(RR[:S - 1] - ref[:S - 1]) / scale
+    assert np.median(err) < 2e-3, np.median(err)
+    assert err.max() < 2e-2, err.max()
