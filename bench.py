@@ -269,7 +269,7 @@ def chem_step_stats(ctx, C):
     a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
     cell order and in the descending-cost order the binned launch approximates."""
     import numpy as np
-    st = ctx.get_field("chem_stats", (2, C))
+    st = ctx.get_field("chem_stats", (3, C))[:2]
     cost = np.maximum(st[0], 0) + st[1]
     pad = (-C) % 64
     nat = np.concatenate([cost, np.zeros(pad)]).reshape(-1, 64).max(axis=1).mean()

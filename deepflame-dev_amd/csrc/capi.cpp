@@ -45,7 +45,7 @@ void allocate_fields(Ctx& x) {
     alloc_field(x, std::string("boundary_") + n, B, 3, true);
   }
   alloc_field(x, "tauU", C, 9, false);
-  alloc_field(x, "chem_stats", C, 2, false);   // per cell: accepted / rejected integrator steps
+  alloc_field(x, "chem_stats", C, 3, false);   // per cell: accepted / rejected integrator steps, next step size
   alloc_field(x, "boundary_tauU", B, 9, true);
   alloc_field(x, "boundary_heGradient", B, 1, true);   // gradientEnergy patches (dfEEqn.cu:266-287)
   for (auto n : {"Y", "rhoD", "hai", "RR"}) {

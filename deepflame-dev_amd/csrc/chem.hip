@@ -395,12 +395,15 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 #pragma unroll
   for (int i = 0; i < S; ++i) { Y0[i] = Yf[(long)i * n + c]; y[i] = rho * Y0[i] / m.W[i]; }
   int steps = 0, rejects = 0;
+  double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
     rate_constants<S>(m, L, T);
     double sc[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) sc[i] = rho / m.W[i];   // Y -> C scale for the tolerances
-    double t = 0.0, h = dt;
+    // first step: the size the previous solve of this cell ended with (OpenFOAM's per-cell deltaTChem)
+    const double hp = stats[2 * n + c];
+    double t = 0.0, h = hp > 0.0 ? fmin(dt, hp) : dt;
     while (t < dt) {
       if (steps + rejects >= max_steps) { steps = -1; break; }
       if (t + h > dt) h = dt - t;
@@ -410,9 +413,13 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
       double err = 0.0;
       if (method == 0) {   // ROS3
         ok = ros3<S>(m, L, T, y, f0, h, r2, r1);
-        if (ok) {
+        if (ok) {   // weighted RMS error norm (KPP / CVODE)
 #pragma unroll
-          for (int i = 0; i < S; ++i) err = fmax(err, fabs(r1[i]) / (atol * sc[i] + rtol * fmax(fabs(y[i]), fabs(r2[i]))));
+          for (int i = 0; i < S; ++i) {
+            const double e = r1[i] / (atol * sc[i] + rtol * fmax(fabs(y[i]), fabs(r2[i])));
+            err += e * e;
+          }
+          err = sqrt(err / S);
           if (!(err == err)) ok = false;
         }
       } else {             // linearly-implicit Euler extrapolation, sequence 1, 2, 3
@@ -448,6 +455,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
         h = h * fmin(0.5, fmax(0.1, fac));
       }
     }
+    if (steps >= 0) hnext = h;
   }
 #pragma unroll
   for (int i = 0; i < S; ++i) {
@@ -456,6 +464,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
   }
   stats[c] = steps;
   stats[n + c] = rejects;
+  if (hnext > 0.0) stats[2 * n + c] = hnext;
 }
 
 // ---- generated fast path: the mechanism compiled in (dfmi/chem_codegen.py), state in registers
@@ -488,10 +497,13 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
     sc[i] = atol * rho / G::W[i];
   }
   int steps = 0, rejects = 0;
+  double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
     double k[G::NK];
     G::consts(T, k);
-    double t = 0.0, h = dt;
+    // first step: the size the previous solve of this cell ended with (OpenFOAM's per-cell deltaTChem)
+    const double hp = stats[2 * n + c];
+    double t = 0.0, h = hp > 0.0 ? fmin(dt, hp) : dt;
     while (t < dt) {
       if (steps + rejects >= max_steps) { steps = -1; break; }
       if (t + h > dt) h = dt - t;
@@ -522,9 +534,10 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
 #pragma unroll
         for (int i = 0; i < S; ++i) {
           yn[i] = y[i] + k1[i] + m2 * k2[i] + m3 * k3[i];
-          const double e = e1 * k1[i] + e2 * k2[i] + e3 * k3[i];
-          err = fmax(err, fabs(e) / (sc[i] + rtol * fmax(fabs(y[i]), fabs(yn[i]))));
+          const double e = (e1 * k1[i] + e2 * k2[i] + e3 * k3[i]) / (sc[i] + rtol * fmax(fabs(y[i]), fabs(yn[i])));
+          err += e * e;   // weighted RMS error norm (KPP / CVODE)
         }
+        err = sqrt(err / S);
         if (!(err == err)) ok = false;
       }
       if (ok && err <= 1.0) {
@@ -540,6 +553,7 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
         h = h * fmin(0.5, fmax(0.1, fac));
       }
     }
+    if (steps >= 0) hnext = h;
   }
 #pragma unroll
   for (int i = 0; i < S; ++i) {
@@ -548,6 +562,7 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
   }
   stats[c] = steps;
   stats[n + c] = rejects;
+  if (hnext > 0.0) stats[2 * n + c] = hnext;
 }
 
 // FNV-1a over the packed mechanism, NASA7 rows and molecular weights (dfmi/chem_codegen.py:fingerprint)

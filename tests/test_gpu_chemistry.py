@@ -65,7 +65,7 @@ def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
     ctx.chem_solve(dt)
-    assert ctx.get_field("chem_stats", (2, C))[0].min() >= 1      # no cell hit the step limit
+    assert ctx.get_field("chem_stats", (3, C))[:2][0].min() >= 1      # no cell hit the step limit
     if method == "ros3" and mech[0].startswith("Burke"):
         assert ctx.chem_info() == 1                               # the compiled-in mechanism ran
     rr = ctx.get_field("RR", (mc.S, C))[:, idx]
@@ -78,7 +78,7 @@ def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     ctx.chem_solve(dt)
     rr = ctx.get_field("RR", (mc.S, C))[:, idx]
     assert (np.abs(rr - ref) / scale).max() < 2e-3
-    st = ctx.get_field("chem_stats", (2, C))
+    st = ctx.get_field("chem_stats", (3, C))[:2]
     assert st[0].min() >= 1
 
 
@@ -112,10 +112,11 @@ def test_chem_cost_binning_bitwise(mech, generic, monkeypatch):
     out = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("DFMI_CHEM_BIN", flag)
+        ctx.set_field("chem_stats", np.zeros((3, C)))   # same start: no carried step sizes
         ctx.chem_solve(1e-6)
         ctx.chem_solve(1e-6)
         assert (ctx.chem_info() > 0) != generic
-        out[flag] = (ctx.get_field("RR", (mc.S, C)), ctx.get_field("chem_stats", (2, C)))
+        out[flag] = (ctx.get_field("RR", (mc.S, C)), ctx.get_field("chem_stats", (3, C))[:2])
     st = out["1"][1]
     assert st[0].min() >= 1 and (st[0] + st[1]).max() > (st[0] + st[1]).min()   # costs really differ
     assert np.array_equal(out["0"][0], out["1"][0])
