@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __
                                                     const TB* __restrict__ b, T omega,
                                                     T* __restrict__ x, T* __restrict__ r, const double* act) {
   const int W = WT > 0 ? WT : W_;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= n || (act && *act == 0.0)) return;
   const T bc = (T)b[c];
   const T xc = omega * bc / D[c];
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int
   if (act && *act == 0.0) return;   // uniform: no barrier below is reached by part of the block
   __shared__ double sh[TPB / 64];
   double acc = 0.0;
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = x[c] + sc * xc[agg[c]];
     T ay = D[c] * yc;
 #pragma unroll

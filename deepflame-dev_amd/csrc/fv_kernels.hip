@@ -11,6 +11,7 @@
 //
 // Compiled with -ffp-contract=off: the arithmetic sequence is the oracle's, op for op.
 #include "dfmi_ctx.h"
+#include <cstdlib>
 
 namespace dfmi {
 
@@ -93,7 +94,7 @@ __global__ void k_copy_multi(CopyList L) {
 __global__ void k_rho(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ rho_old,
                       const double* __restrict__ phi, const double* __restrict__ bphi, double* __restrict__ rho,
                       double* __restrict__ odiag, double* __restrict__ osrc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   double div = 0.0;
   each_face(m, c, [&](int f, int, bool own) { if (own) div += phi[f]; else div -= phi[f]; });
@@ -118,7 +119,7 @@ __device__ __forceinline__ void dev2T(double sc, const double* v, double* o) {
 __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
                          const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
                          double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double s[9];
@@ -184,7 +185,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
     const double* __restrict__ bp, const double* __restrict__ T, const double* __restrict__ bT,
     double* __restrict__ lower, double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src,
     double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
@@ -257,7 +258,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
 
 // K = 0.5*magSqr(U) on cells (boundary K is done per slot below)
 __global__ void k_kinetic(int C, const double* __restrict__ U, double* __restrict__ K) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double x = U[c], y = U[(long)C + c], z = U[2L * C + c];
   K[c] = 0.5 * (x * x + y * y + z * z);
@@ -268,7 +269,7 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
     const double* __restrict__ bU, const double* __restrict__ lower, const double* __restrict__ upper,
     const double* __restrict__ src, const double* __restrict__ ic, const double* __restrict__ bc,
     double* __restrict__ H) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
 #pragma unroll
@@ -291,7 +292,7 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
 }
 
 __global__ void k_hbya_scale_cells(int C, const double* __restrict__ rAU, double* __restrict__ H) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= C) return;
 #pragma unroll
   for (int k = 0; k < 3; ++k) H[(long)k * C + c] = rAU[c] * H[(long)k * C + c];
@@ -383,7 +384,7 @@ __global__ void k_p_cell(MeshView m, const int8_t* __restrict__ tyP, const doubl
                          const double* __restrict__ ph, const double* __restrict__ bph, const double* __restrict__ p,
                          const double* __restrict__ p_old, const double* __restrict__ psi, const double* __restrict__ rho,
                          const double* __restrict__ rho_old, double* __restrict__ diag, double* __restrict__ src) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   double dL = 0.0, div = 0.0;
   each_face(m, c, [&](int f, int, bool own) {
@@ -428,7 +429,7 @@ __global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const 
                               const double* __restrict__ bp, const double* __restrict__ p_old,
                               const double* __restrict__ H, const double* __restrict__ rAU, double* __restrict__ U,
                               double* __restrict__ K, double* __restrict__ dpdt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double g[3] = {0.0, 0.0, 0.0};
@@ -466,7 +467,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
     const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
     const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
     double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   // One pass over the cell's faces computes every species' Gauss gradient AND its diffAlphaD
@@ -618,7 +619,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
     double* __restrict__ bc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, d2 = 0.0;
@@ -678,7 +679,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
     double* __restrict__ dS, double* __restrict__ rhs) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
   double d1 = 0.0, d2 = 0.0;
@@ -745,7 +746,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
 
 template <int S>
 __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double sum = 0;
 #pragma unroll
@@ -769,7 +770,7 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
     const double* __restrict__ bhD, const double* __restrict__ dpdt, const double* __restrict__ dAD,
     const double* __restrict__ egrad, double* __restrict__ lower, double* __restrict__ upper,
     double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic, double* __restrict__ bc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0, divK = 0.0, divh = 0.0;

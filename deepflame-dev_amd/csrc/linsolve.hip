@@ -119,7 +119,7 @@ __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, co
   const double* ic = q.ic + ms * q.bstride;
   const double* bc = q.bc + ms * q.bstride;
   double* vs = val + (long)s * W * C;
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
     for (int k = 0; k < W; ++k) {
       const int e = esrc[k * C + c];
       double v;
@@ -151,7 +151,7 @@ __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, co
 __global__ void k_copy_x(long C, long Ce, Sys q, const int* __restrict__ sys_map, double* __restrict__ xw) {
   const int s = blockIdx.y;
   const int ms = sys_map ? sys_map[s] : s;
-  for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < C; c += (long)gridDim.x * blockDim.x)
+  for (long c = xcd_block() * (long)blockDim.x + threadIdx.x; c < C; c += (long)gridDim.x * blockDim.x)
     xw[s * Ce + c] = q.x[ms * q.xstride + c];
 }
 
@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const 
   const int s = blockIdx.y;
   const double* vs = val + (long)s * W * C;
   double acc[2] = {0.0, 0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     const double d = b.dS[i];
     const double res = b.rhs[i] - ell_mv<WT>(W, C, col, vs, d, b.xw + s * Ce, c);
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
   if (stop) return;
   const double* vs = val + (long)s * W * C;
   double acc[1] = {0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], b.p + s * Ce, c);
     b.v[i] = y;
@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double*
   double v[1];
   red_sum<1>(red, s, v);
   const double alpha = v[0] != 0.0 ? st[0] / v[0] : 0.0;
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     b.sv[i] = b.r[i] - alpha * b.v[i];
   }
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, cons
   const double* ws = b.v + s * Ce;
   const double* hs = b.sv + s * Ce;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     const double sc = rs[c] - alpha * ws[c];
     double o = 0.0;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys 
   const int ms = sys_map ? sys_map[s] : s;
   double* xv = q.x + ms * q.xstride;
   double acc[2] = {0.0, 0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     const double pv = b.p[i], vv = b.v[i];
     const double sv = b.r[i] - alpha * vv;   // the s of k_bcg_spmv2, same expression
@@ -326,7 +326,7 @@ template <int WT>
 __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, const int* __restrict__ col,
                                                  const double* __restrict__ val, CV v, double* partial) {
   double acc[2] = {0.0, 0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const double ax = ell_mv<WT>(W, C, col, val, v.dS[c], v.xw, c);
     const double rr = v.rhs[c] - ax;
     const double zz = rr / v.dS[c];
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
   const double* z = v.z;
   const int Wr = WT > 0 ? WT : W;
   double acc[1] = {0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const double pc = z[c] + beta * pold[c];
     pnew[c] = pc;
     double y = v.dS[c] * pc;
@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
   const double alpha = pv[0] != 0.0 ? rz / pv[0] : 0.0;
   if (leader()) { scal[2] = alpha; scal[1] = rz; }
   double acc[2] = {0.0, 0.0};
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
     const double rr = v.r[c] - alpha * v.q[c];
     v.r[c] = rr;
