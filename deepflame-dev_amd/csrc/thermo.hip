@@ -164,7 +164,7 @@ template <int S>
 __global__ void __launch_bounds__(256) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
     const double* __restrict__ p, const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho,
     double* __restrict__ mu, double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= n) return;
   double y[S], rd[S], ha[S];
 #pragma unroll
