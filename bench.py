@@ -342,10 +342,12 @@ def main():
         ctx.solver_work(e, reset=True)
     if args.chem == "dnn":
         ctx.dnn_stats()
+    torch.cuda.synchronize(local)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.time_step(args.ncorr)
-    ctx.sync()
+    ctx.sync()                                     # the context's stream (all the step's work)
+    torch.cuda.synchronize(local)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
