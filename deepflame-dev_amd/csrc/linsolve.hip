@@ -710,6 +710,21 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
   // act: the solve's active flag (after the first iteration the V-cycle of a stopped solve is skipped)
   auto reds = [&](Red& rz, Red& rr, const double* act) {
+    if (amg && x.nranks > 1) {
+      // several ranks: both sums (r.r from the update, r.z from the V-cycle) go out in ONE all-gather
+      // of three values per rank instead of two collectives per iteration
+      if (x.ws.red_local.n < 8) x.ws.red_local.alloc(8);
+      if (x.ws.red_all.n < (size_t)8 * x.nranks) x.ws.red_all.alloc((size_t)8 * x.nranks);
+      double* loc = x.ws.red_local.p;
+      hipLaunchKernelGGL(k_red_local<2>, dim3(1), dim3(TPB), 0, x.stream, q2, nblk, loc);
+      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, act);
+      hipLaunchKernelGGL(k_red_local<1>, dim3(1), dim3(TPB), 0, x.stream, q3, nblk, loc + 2);
+      DFMI_HIP(hipGetLastError());
+      halo_allgather(x, loc, x.ws.red_all.p, 3);
+      rr = Red{x.ws.red_all.p + 1, x.nranks, 3, 0};
+      rz = Red{x.ws.red_all.p + 2, x.nranks, 3, 0};
+      return;
+    }
     Red r2 = L.after(q2, 2, 0);
     rr = r2; rr.p += 1;
     if (amg) {
