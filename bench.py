@@ -35,17 +35,39 @@ MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species 
 }
 
 
-def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None) -> float:
-    """Bytes one unit of a kernel's work must move at minimum (each input read once, each output
-    written once; fp64 values, int32 indices). Units: k_y_assemble_ell one launch (all S-1 solved
-    species); k_cg_spmv one active PCG iteration; k_bcg_spmv one SpMV of one active system.
-    Bc = coupled boundary slots (cyclic / processor: one matrix entry each). DESIGN.md 5 lists them."""
+def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None, W: int = 6) -> float:
+    """Bytes one unit of a kernel's work must move at minimum: every input element read once and every
+    output element written once (fp64 values, int32 indices, int8 slot types), shared face/cell arrays
+    counted ONCE per launch however many species use them. Units: one launch for the assembly/thermo
+    kernels (all species of that launch); k_cg_spmv one active PCG iteration; k_bcg_spmv one SpMV of
+    one active system. Bc = coupled boundary slots (cyclic / processor), W = solver row width.
+    Gather topology of the cell-centric kernels: 12 B per cell (nbrStart, ownStart, cbStart) + 12 B per
+    face (nbrFace, own, nei) + 9 B per coupled slot (cbSlot, partner, type). DESIGN.md 5 lists them."""
     Sa = S - 1                                     # solved species (inert excluded)
     Bc = B if Bc is None else Bc
-    if kernel == "k_y_assemble_ell" or kernel == "k_y_assemble":
-        # SURVEY.md 8(d): fused Y-species assembly (ddt + div phi + div phiUc + lap rhoD + RR),
-        # 64 F + 64 C bytes per solved species
-        return Sa * (64.0 * F + 64.0 * C)
+    topo = 12.0 * C + 12.0 * F + 9.0 * Bc
+    if kernel == "k_y_prep":
+        # Y, hai, rhoD (S each), alpha, V in; sumYDiffError, hDiffCorrFlux (3 each), diffAlphaD out;
+        # faces w, Sf, magSf, dc; coupled slots bw, bSf, bmagSf, bdc
+        return C * 8.0 * (3 * S + 2) + C * 56.0 + F * 48.0 + Bc * 48.0 + topo
+    if kernel in ("k_y_assemble_ell", "k_y_assemble"):
+        # rhoD, Y, RR (S each), rho, rho_old, V in; per solved species W row values + dS + rhs out;
+        # faces phi, phiUc, w, dc, magSf; coupled slots bphi, bphiUc, bw, bdc, bmagSf
+        return C * 8.0 * (3 * S + 3) + Sa * C * (8.0 * W + 16.0) + F * 40.0 + Bc * 40.0 + topo
+    if kernel == "k_u_grad":
+        # U (3), mu, V in; mu*dev2(T(grad U)) (9) out; faces w, Sf; coupled slots bw, bSf
+        return C * 40.0 + C * 72.0 + F * 32.0 + Bc * 32.0 + topo
+    if kernel == "k_u_assemble":
+        # rho, rho_old, U_old (3), mu, p, tau (9), V in; diag, source (3), source_solve (3), rAU out;
+        # faces w, phi, dc, magSf, Sf in, lower/upper out; slots bphi, bw, bdc, bmagSf, bSf in, ic/bc (3 each) out
+        return C * 136.0 + C * 64.0 + F * (56.0 + 16.0) + Bc * (56.0 + 48.0) + topo
+    if kernel == "k_e_assemble":
+        # he, rho, rho_old, K, K_old, alpha, hDiffCorrFlux (3), dpdt, diffAlphaD, V in; diag, source out;
+        # faces phi, w, dc, magSf, Sf in, lower/upper out; slots bphi, bw, bdc, bmagSf, bSf in, ic/bc out
+        return C * 104.0 + C * 16.0 + F * (56.0 + 16.0) + Bc * (56.0 + 16.0) + topo
+    if kernel == "k_u_hbya":
+        # U (3), source (3), V in; HbyA (3) out; faces lower, upper; slots internal/boundaryCoeffs (3 each)
+        return C * 56.0 + C * 24.0 + F * 16.0 + Bc * 48.0 + topo
     if kernel == "k_cg_spmv":
         # fused PCG step p = z + beta p_old; q = A p: cells z, p_old, dS in, p, q out (40 B);
         # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
@@ -56,12 +78,14 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
         # t = A s with s = r - alpha v formed on the fly reads dS, r, v, r0, writes t (40 B); matrix as above
         return C * 36.0 + F * 24.0 + Bc * 12.0
     if kernel == "k_thermo_cells":
-        # T, he, p in; Y in (S); T, psi, rho, mu, alpha out; rhoD, hai out (S each)
-        return C * 8.0 * (3 + S + 5 + 2 * S)
+        # T, he, p, Y (S) in; T, he, psi, rho, mu, alpha, rhoD (S), hai (S) out
+        return C * 8.0 * (3 + S) + C * 8.0 * (6 + 2 * S)
     raise KeyError(kernel)
 
 
-ROOF_KERNELS = ("k_bcg_spmv", "k_cg_spmv", "k_y_assemble_ell")
+SOLVER_KERNELS = ("k_bcg_spmv", "k_cg_spmv")
+ASSEMBLY_KERNELS = ("k_y_assemble_ell", "k_y_prep", "k_u_grad", "k_u_assemble", "k_e_assemble", "k_u_hbya")
+ROOF_KERNELS = SOLVER_KERNELS + ASSEMBLY_KERNELS + ("k_thermo_cells",)
 
 
 def parse():
@@ -81,6 +105,7 @@ def parse():
     ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
                     help="chemistry source: stiff ODE integration per cell (BASELINE config 3), the DF-ODENet "
                          "surrogate (MFMA fp16, config 4's path on the H2 nets) or off")
+    ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-flame", action="store_true", help="skip the BASELINE config 2 (1D flame) side line")
@@ -124,7 +149,7 @@ def cpu_baseline(args, table, ym, inert):
         rng = np.random.default_rng(0)
         idx = rng.choice(m.n_cells, 24, replace=False)
         t1 = time.perf_counter()
-        kin.reaction_rates(st["T"][idx], None, st["rho"][idx], st["Y"][:, idx], args.dt, rtol=1e-6, atol=1e-10)
+        kin.reaction_rates(st["T"][idx], st["p"][idx], st["rho"][idx], st["Y"][:, idx], args.dt, rtol=1e-6, atol=1e-10)
         chem_s_per_cell = (time.perf_counter() - t1) / idx.size
         sample += (f"; chemistry: oracle/chem_oracle.py SciPy BDF (rtol 1e-6, atol 1e-10) on {idx.size} sampled cells, "
                    f"{chem_s_per_cell * 1e3:.2f} ms/cell")
@@ -264,6 +289,72 @@ def dnn53_line(m, T, p, steps=3, warmup=1):
                               "frac": tf / 2500.0 if tf else None}}
 
 
+def zero_d_line(n_steps=1000):
+    """BASELINE config 1: the reference df0DFoam case (examples/df0DFoam/zeroD_cubicReactor/H2/
+    cvodeIntegrator: 10^3 cells of the same reactor, ES80_H2-7-16, T0 = 1000 K, 1 atm, dt 1e-6, 1000 steps,
+    constant pressure) through dfmi_zero_d_step; chem-integrations/s = cells x steps / wall time."""
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.kinetics import parse_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    import numpy as np
+    golden = os.path.join(ROOT, "tests", "golden")
+    ref = json.load(open(os.path.join(golden, "zeroD_cubicReactor.json")))
+    ym = read_yaml_mechanism(os.path.join(golden, ref["mechanism"]))
+    t = read_thermo_table(os.path.join(golden, "thermo_ES80_H2-7-16.txt"), ym["species"])
+    m = hex_box(10, 10, 10, lengths=(5e-3,) * 3, periodic=(False,) * 3)
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), ref["dt"])
+    ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, ref["mechanism"])))
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    C = m.n_cells
+    case.init_state(ctx, m, t.S, np.full(C, ref["T0"]), np.full(C, ref["p"]), np.zeros((3, C)),
+                    np.repeat(np.asarray(ref["Y0"])[:, None], C, axis=1))
+    t0 = time.perf_counter()
+    ctx.zero_d_step(ref["dt"], n_steps)
+    el = time.perf_counter() - t0
+    T_end = float(ctx.get_field("T", (C,))[0])
+    ctx.close()
+    return {"workload": "df0DFoam zeroD_cubicReactor (reference example): 1000 identical cells, ES80 7 species, "
+                        "T0=1000 K, p=1 atm, dt=1e-6, 1000 steps, constant pressure, rtol 1e-6 atol 1e-10",
+            "ms_total": el * 1e3, "ms_per_step": el / n_steps * 1e3, "chem_integrations_per_s": C * n_steps / el,
+            "T_end": T_end, "T_end_oracle": ref["T"][n_steps] if n_steps <= ref["n_steps"] else None}
+
+
+def config4_line(m, T, U, p, steps=3, warmup=1):
+    """BASELINE config 4 as a full dfLowMachFoam step: the 2M-cell box with 53 species (SURVEY 8d synthetic
+    table: gri30's 36 species fitted by dfmi.transport_fit, cycled to 53, N2 last; Dirichlet-like mass
+    fractions) and the DF-ODENet surrogate (52 seeded nets [55,1600,800,400,1]) as the chemistry source."""
+    from dfmi.mech import read_thermo_table
+    from dfmi.lib import Context
+    from dfmi import case
+    from dfmi.synthetic import gri53_species, gri53_mass_fractions, gri53_dnn
+    golden = os.path.join(ROOT, "tests", "golden")
+    sp = gri53_species(os.path.join(golden, "gri30.yaml"))
+    t = read_thermo_table(os.path.join(golden, "thermo_gri53_synthetic.txt"), sp)
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6)
+    gri53_dnn(ctx)
+    ctx.chem_set_options(2)
+    case.init_state(ctx, m, t.S, T, p, U, gri53_mass_fractions(m.n_cells))
+    for _ in range(warmup):
+        ctx.time_step(2)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.time_step(2)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    iters = {e: ctx.solver_stats(e)[0] for e in ("U", "Y", "E", "p")}
+    nr = ctx.dnn_stats()[0]
+    ctx.close()
+    return {"workload": f"dfLowMachFoam 3D periodic box {m.n_cells} cells, 53 species (synthetic GRI table), "
+                        "DF-ODENet surrogate source (52 nets, fp16 MFMA), nCorr=2, dt=1e-6 (BASELINE config 4)",
+            "metric": "cell-updates/s", "value": m.n_cells * steps / el, "ms_per_step": el / steps * 1e3,
+            "steps": steps, "reacting_cells": nr, "solver_iters": iters}
+
+
 def chem_step_stats(ctx, C):
     """Integrator steps per cell of the last chemistry solve and how evenly 64-lane waves are loaded:
     a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
@@ -336,12 +427,7 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    extra = {"ode": ["k_chem", "k_bin"], "dnn": ["k_mlp_gemm"], "off": []}[args.chem]
-    ctx.kernel_timer(",".join(ROOF_KERNELS + tuple(extra)))
-    for e in ("U", "Y", "E", "p"):
-        ctx.solver_work(e, reset=True)
-    if args.chem == "dnn":
-        ctx.dnn_stats()
+    # ---- headline: K steps, nothing armed (no timing events inside the timed region)
     torch.cuda.synchronize(local)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -351,6 +437,24 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    el = t1 - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    stats = {e: ctx.solver_stats(e) for e in ("U", "Y", "E", "p")}
+
+    # ---- roofline pass: the same step, HIP events around every launch of the measured kernels and the
+    # solver work counted on the device (after the headline, so the instrumentation never inflates it)
+    extra = {"ode": ["k_chem", "k_bin"], "dnn": ["k_mlp_gemm"], "off": []}[args.chem]
+    ctx.kernel_timer(",".join(ROOF_KERNELS + tuple(extra)))
+    for e in ("U", "Y", "E", "p"):
+        ctx.solver_work(e, reset=True)
+    if args.chem == "dnn":
+        ctx.dnn_stats()
+    for _ in range(args.roof_steps):
+        ctx.time_step(args.ncorr)
+    ctx.sync()
     ktime = {k: ctx.kernel_time(k) for k in ROOF_KERNELS}
     work = {e: ctx.solver_work(e) for e in ("U", "Y", "E", "p")}
     chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
@@ -358,12 +462,6 @@ def main():
     gemm_ms, gemm_n = ctx.kernel_time("k_mlp_gemm") if args.chem == "dnn" else (0.0, 0)
     n_react, gemm_flops = ctx.dnn_stats() if args.chem == "dnn" else (0, 0.0)
     ctx.kernel_timer("")
-    el = t1 - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    stats = {e: ctx.solver_stats(e) for e in ("U", "Y", "E", "p")}
     T = ctx.get_field("T", (m.n_cells,))
     finite = bool(np.isfinite(T).all())
 
@@ -378,7 +476,8 @@ def main():
         for fam in ROOF_KERNELS:
             # every instantiation of the family (k_bcg_spmv -> k_bcg_spmv1<6>, k_bcg_spmv2<6>); variants
             # moving < 1 % of the largest one's bytes are other workloads' (the 1D flame line's W = 2)
-            ent = [v for key, v in tab.items() if key.split("::")[-1].startswith(fam)]
+            ent = [v for key, v in tab.items()
+                   if key.split("::")[-1].split("<")[0].rstrip("12") == fam or key.split("::")[-1].startswith(fam + "<")]
             if not ent:
                 continue
             top = max(v["hbm_bytes_mean"] for v in ent)
@@ -386,8 +485,9 @@ def main():
             nd = sum(v["dispatches"] for v in ent)
             pmc[fam] = {"hbm_bytes_mean": sum(v["hbm_bytes_mean"] * v["dispatches"] for v in ent) / nd}
     Bc = m.n_coupled_slots
-    units = {"k_bcg_spmv": 2.0 * (work["U"] + work["Y"] + work["E"]), "k_cg_spmv": work["p"],
-             "k_y_assemble_ell": float(ktime["k_y_assemble_ell"][1])}
+    units = {"k_bcg_spmv": 2.0 * (work["U"] + work["Y"] + work["E"]), "k_cg_spmv": work["p"]}
+    for k in ASSEMBLY_KERNELS + ("k_thermo_cells",):
+        units[k] = float(ktime[k][1])              # one unit = one launch
     roofs = {}
     for k in ROOF_KERNELS:
         ms, nl = ktime[k]
@@ -397,12 +497,14 @@ def main():
         total_bytes = per_unit * units[k]
         achieved = total_bytes / (ms / 1e3) / 1e9
         tr = pmc.get(k)
-        roofs[k] = {"kernel": k, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        roofs[k] = {"kernel": k, "bound": "hbm" if k != "k_thermo_cells" else "fp64-valu",
+                    "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS,
                     "traffic": tr["hbm_bytes_mean"] if tr else None,
                     "algorithmic_bytes": total_bytes / nl, "launches": nl, "work_units": units[k],
                     "bytes_per_unit": per_unit, "avg_us": ms * 1e3 / nl, "total_ms": ms}
-    primary = args.kernel if args.kernel != "auto" else max(roofs, key=lambda k: roofs[k]["total_ms"])
+    hbm = {k: v for k, v in roofs.items() if v["bound"] == "hbm"}
+    primary = args.kernel if args.kernel != "auto" else max(hbm, key=lambda k: hbm[k]["total_ms"])
     out = {
         "metric": "cell-updates/s (dfLowMachFoam outer iter)",
         "value": value,
@@ -426,12 +528,13 @@ def main():
                    else "single"},
         "roofline": dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "
                          "WRITE_SIZE passes, mean per dispatch, gfx950 read correction)",
-                         note="achieved = algorithmic bytes of the work done (active systems/iterations) / "
-                              "summed HIP-event kernel time over the timed steps; algorithmic_bytes and traffic "
-                              "are per launch"),
-        "rooflines": {k: {kk: v[kk] for kk in ("achieved", "frac", "traffic", "algorithmic_bytes", "avg_us",
+                         note=f"achieved = algorithmic bytes of the work done (active systems/iterations) / summed "
+                              f"HIP-event kernel time over {args.roof_steps} extra steps after the timed region "
+                              "(the headline runs with no events armed); algorithmic_bytes and traffic are per launch"),
+        "rooflines": {k: {kk: v[kk] for kk in ("bound", "achieved", "frac", "traffic", "algorithmic_bytes", "avg_us",
                                                "launches")} for k, v in roofs.items()},
         "solver_iters": {e: s[0] for e, s in stats.items()},
+        "solver_work_roof_pass": work,
         "amg_levels": ctx.amg_info(),
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
@@ -442,13 +545,15 @@ def main():
                  "mfma_roofline": {"bound": "mfma", "achieved": gemm_flops / (gemm_ms / 1e3) / 1e12,
                                    "peak": 2500.0, "unit": "TFLOP/s",
                                    "frac": gemm_flops / (gemm_ms / 1e3) / 1e12 / 2500.0},
-                 "inferences_per_s_gemm_time": n_react * args.steps / (gemm_ms / 1e3)}
+                 "inferences_per_s_gemm_time": n_react * args.roof_steps / (gemm_ms / 1e3)}
                 if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
     }
+    U0 = ctx.get_field("U", (3, m.n_cells)) if (rank == 0 and world == 1 and n == 128 and not args.no_flame) else None
     ctx.close()
     if rank == 0 and world == 1 and n == 128 and not args.no_flame:
-        out["other_configs"] = {"flame1d": flame1d_line(), "dnn53": dnn53_line(m, T0, p0)}
+        out["other_configs"] = {"config1_zeroD": zero_d_line(), "config2_flame1d": flame1d_line(),
+                                "config4_gri53_dnn": config4_line(m, T0, U0, p0), "dnn53_surrogate": dnn53_line(m, T0, p0)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, table, ym, inert)
         out["cpu_baseline"]["ratio"] = value / out["cpu_baseline"]["value"]

@@ -168,8 +168,10 @@ void do_U(Ctx& x) {
 }
 void do_Y(Ctx& x) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
-  if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt);   // chemistry->solve(deltaT) before YEqn (YEqn.H)
-  else if (x.chem.mode == 2) dnn_solve(x);              // chemistrySolver_GPU.Inference (YEqn_GPU.H)
+  // chemistry->solve(deltaT) before YEqn (YEqn.H); the thermo density of that call is rho before this
+  // step's rhoEqn, i.e. rho_old (dfChemistryModel.C:87,771; the GPU reference passes d_rho_old, dfYEqn.cu:449)
+  if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt, "rho_old");
+  else if (x.chem.mode == 2) dnn_solve(x, "rho_old");   // chemistrySolver_GPU.Inference (YEqn_GPU.H)
   y_prep(x);
   Matrix& A = x.mY;
   std::vector<int> map;
@@ -416,7 +418,13 @@ int dfmi_pre_time_step(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x)
 int dfmi_post_time_step(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); }); }
 int dfmi_rho_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); rho_process(ctx->x, false); }); }
 int dfmi_U_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_U(ctx->x); }); }
-int dfmi_Y_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_Y(ctx->x); }); }
+int dfmi_Y_process(dfmi_ctx* ctx) {
+  return guard([&] {
+    require_ready(ctx->x);
+    do_Y(ctx->x);
+    if (ctx->x.chem.mode == 1) chem_check(ctx->x);   // the Y solve's polls have passed the chemistry
+  });
+}
 int dfmi_E_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_E(ctx->x); }); }
 int dfmi_p_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do_p(ctx->x); }); }
 int dfmi_U_get_HbyA(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); u_hbya(ctx->x); }); }
@@ -446,6 +454,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
       rho_process(x, false);
     }
     thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
+    if (x.chem.mode == 1) chem_check(x);   // the p solves' polls have already passed the chemistry
   });
 }
 
@@ -524,6 +533,16 @@ int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
     } else if (e == "Y") {
       if (!x.fields.count("dbg_gradY")) alloc_field(x, "dbg_gradY", x.C, 3 * x.S, false);
       y_prep(x); y_assemble(x);
+    } else if (e == "Y_ell") {        // production: fused assembly straight into the solver rows
+      std::vector<int> map;
+      for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
+      double *val, *dS, *rhs;
+      bicg_layout(x, (int)map.size(), &val, &dS, &rhs);
+      y_prep(x);
+      y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
+    } else if (e == "Y_ell_ref") {    // LDU assembly folded by the generic solver gather
+      y_prep(x); y_assemble(x);
+      bicg_rows_from_ldu_Y(x);
     } else if (e == "E") e_assemble(x);
     else if (e == "p") p_assemble(x);
     else if (e == "HbyA") u_hbya(x);
@@ -547,6 +566,14 @@ int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* ho
     DFMI_CHECK((size_t)count == b->n, "matrix part size mismatch: expected " + std::to_string(b->n));
     DFMI_HIP(hipMemcpyAsync(host, b->p, count * sizeof(double), hipMemcpyDeviceToHost, x.stream));
     DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_get_solver_rows(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(std::string(eqn) == "Y", "solver rows are inspectable for the YEqn batch only");
+    bicg_rows_get(x, x.S - 1, part, host, count);
   });
 }
 
@@ -589,7 +616,7 @@ int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting) {
   return guard([&] {
     Ctx& x = ctx->x;
     require_ready(x);
-    dnn_solve(x);
+    dnn_solve(x, "rho");
     DFMI_HIP(hipStreamSynchronize(x.stream));
     if (n_reacting) *n_reacting = x.dnn.last_reacting;
   });
@@ -613,8 +640,29 @@ int dfmi_chem_solve(dfmi_ctx* ctx, double dt) {
     Ctx& x = ctx->x;
     require_ready(x);
     DFMI_CHECK(dt > 0, "chemistry time step must be positive");
-    chem_solve(x, dt);
+    chem_solve(x, dt, "rho");
     DFMI_HIP(hipStreamSynchronize(x.stream));
+    chem_check(x);
+  });
+}
+
+int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    DFMI_CHECK(dt > 0 && n_steps >= 1, "0D step: dt and n_steps must be positive");
+    for (int i = 0; i < n_steps; ++i) {
+      zero_d_step(x, dt);
+      if (x.chem.mode == 1) chem_check(x);
+    }
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_chem_set_max_steps(dfmi_ctx* ctx, int max_steps) {
+  return guard([&] {
+    DFMI_CHECK(max_steps > 0, "max_steps must be positive");
+    ctx->x.chem.max_steps = max_steps;
   });
 }
 

@@ -374,12 +374,33 @@ __global__ void __launch_bounds__(BCB) k_bin_scatter(long n, const double* __res
   }
 }
 
+// Cantera's setState_TPY(T, p, Y) (dfChemistryModel.C:755): mass fractions clipped at 0 and
+// normalised (Phase::setMassFractions), density = p * meanW / (R T); returns that density and the
+// reactor's initial concentrations C_i = rho Y_i / W_i. The reactor then runs at this density (closed,
+// constant volume), while RR is scaled by the thermo density the caller passes (problem.rhoi =
+// rho_[celli], :771 and :807).
+template <int S, class WT>
+__device__ __forceinline__ double reactor_state(double T, double p, const double (&Y0)[S], const WT& W, double (&C)[S]) {
+  double ys = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) ys += fmax(Y0[i], 0.0);
+  const double iys = 1.0 / ys;
+  double sw = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) sw += fmax(Y0[i], 0.0) * iys / W[i];
+  const double rho = p / (sw * RU * T);
+#pragma unroll
+  for (int i = 0; i < S; ++i) C[i] = rho * (fmax(Y0[i], 0.0) * iys) / W[i];
+  return rho;
+}
+
 template <int S>
 __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ perm, ChemMech m,
-                                                const double* __restrict__ Tf,
+                                                const double* __restrict__ Tf, const double* __restrict__ pf,
                                                 const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                 double dt, double rtol, double atol, double Tmin, int max_steps,
-                                                int method, double* __restrict__ RR, double* __restrict__ stats) {
+                                                int method, double* __restrict__ RR, double* __restrict__ stats,
+                                                int* __restrict__ fail) {
   extern __shared__ double lds[];
   Lane<S> L;
   L.lane = threadIdx.x;
@@ -390,10 +411,11 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
   if (t >= n) return;   // no block-level synchronisation below: early exit is safe
   const long c = perm ? perm[t] : t;
-  const double T = Tf[c], rho = rhof[c];
+  const double T = Tf[c], rho_rr = rhof[c];
   double Y0[S], y[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) { Y0[i] = Yf[(long)i * n + c]; y[i] = rho * Y0[i] / m.W[i]; }
+  for (int i = 0; i < S; ++i) Y0[i] = Yf[(long)i * n + c];
+  const double rho = reactor_state<S>(T, pf[c], Y0, m.W, y);
   int steps = 0, rejects = 0;
   double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
@@ -460,11 +482,12 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double Yn = y[i] * m.W[i] / rho;
-    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho / dt : 0.0;
+    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho_rr / dt : 0.0;
   }
   stats[c] = steps;
   stats[n + c] = rejects;
   if (hnext > 0.0) stats[2 * n + c] = hnext;
+  if (steps < 0) atomicAdd(fail, 1);
 }
 
 // ---- generated fast path: the mechanism compiled in (dfmi/chem_codegen.py), state in registers
@@ -476,9 +499,10 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 
 template <class G>
 __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restrict__ perm, const double* __restrict__ Tf,
-                                                    const double* __restrict__ rhof, const double* __restrict__ Yf,
-                                                    double dt, double rtol, double atol, double Tmin, int max_steps,
-                                                    double* __restrict__ RR, double* __restrict__ stats) {
+                                                    const double* __restrict__ pf, const double* __restrict__ rhof,
+                                                    const double* __restrict__ Yf, double dt, double rtol, double atol,
+                                                    double Tmin, int max_steps, double* __restrict__ RR,
+                                                    double* __restrict__ stats, int* __restrict__ fail) {
   constexpr int S = G::S;
   constexpr double g = 0.43586652150845899941601945119356;
   constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
@@ -488,14 +512,13 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
   if (t >= n) return;
   const long c = perm ? perm[t] : t;
-  const double T = Tf[c], rho = rhof[c];
+  const double T = Tf[c], rho_rr = rhof[c];
   double Y0[S], y[S], sc[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) {
-    Y0[i] = Yf[(long)i * n + c];
-    y[i] = rho * Y0[i] / G::W[i];
-    sc[i] = atol * rho / G::W[i];
-  }
+  for (int i = 0; i < S; ++i) Y0[i] = Yf[(long)i * n + c];
+  const double rho = reactor_state<S>(T, pf[c], Y0, G::W, y);
+#pragma unroll
+  for (int i = 0; i < S; ++i) sc[i] = atol * rho / G::W[i];
   int steps = 0, rejects = 0;
   double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
@@ -558,11 +581,12 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double Yn = y[i] * G::W[i] / rho;
-    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho / dt : 0.0;
+    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho_rr / dt : 0.0;
   }
   stats[c] = steps;
   stats[n + c] = rejects;
   if (hnext > 0.0) stats[2 * n + c] = hnext;
+  if (steps < 0) atomicAdd(fail, 1);
 }
 
 // FNV-1a over the packed mechanism, NASA7 rows and molecular weights (dfmi/chem_codegen.py:fingerprint)
@@ -593,7 +617,7 @@ void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* 
   h.ready = true;
 }
 
-void chem_solve(Ctx& x, double dt) {
+void chem_solve(Ctx& x, double dt, const char* rho_field) {
   Chem& h = x.chem;
   DFMI_CHECK(h.ready, "chemistry mechanism not set (dfmi_chem_set_mechanism)");
   DFMI_CHECK(x.thermo.S == x.S, "chemistry needs the thermo coefficients (NASA7, W)");
@@ -601,6 +625,9 @@ void chem_solve(Ctx& x, double dt) {
   const size_t lds = ((size_t)3 * h.R + (size_t)x.S * x.S) * LANES * sizeof(double);
   DFMI_CHECK(lds <= 160 * 1024, "chemistry: mechanism too large for the LDS layout");
   double* stats = x.f("chem_stats");
+  const double* rho_rr = x.f(rho_field);
+  if (h.fail.n == 0) h.fail.alloc(1);
+  DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
   if (const char* e = std::getenv("DFMI_CHEM_METHOD")) h.method = std::string(e) == "extrap" ? 1 : 0;
   const dim3 g((unsigned)blocks_for(x.C, LANES));
   // compiled-in mechanism? (bitwise the same arrays, NASA7 and weights)
@@ -634,18 +661,21 @@ void chem_solve(Ctx& x, double dt) {
     KScope _ks(x, "k_chem");
     if (h.generated == 1)
       hipLaunchKernelGGL(k_chem_gen<ChemGen_burke9>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
-                         x.f("rho"), x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+                         x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats,
+                         h.fail.p);
     else
       hipLaunchKernelGGL(k_chem_gen<ChemGen_es80>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
-                         x.f("rho"), x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats);
+                         x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats,
+                         h.fail.p);
     DFMI_HIP(hipGetLastError());
+    chem_fail_snapshot(x);
     return;
   }
 #define CALL(NS)                                                                                                    \
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \
-    hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, perm, m, x.f("T"), x.f("rho"), x.f("Y"), dt, \
-                       h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats);                            \
+    hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, perm, m, x.f("T"), x.f("p"), rho_rr,      \
+                       x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats, h.fail.p);     \
   } while (0)
   switch (x.S) {
     case 4: CALL(4); break; case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break;
@@ -655,6 +685,28 @@ void chem_solve(Ctx& x, double dt) {
   }
 #undef CALL
   DFMI_HIP(hipGetLastError());
+  chem_fail_snapshot(x);
+}
+
+// The failure count leaves the device behind an event (no stream drain); chem_check reads it at the
+// next host synchronisation point the caller already has (end of the time step's solver polls).
+void chem_fail_snapshot(Ctx& x) {
+  Chem& h = x.chem;
+  h.fail_host.ensure(1);
+  if (!h.fail_ev) DFMI_HIP(hipEventCreateWithFlags(&h.fail_ev, hipEventDisableTiming));
+  DFMI_HIP(hipMemcpyAsync(h.fail_host.p, h.fail.p, sizeof(int), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipEventRecord(h.fail_ev, x.stream));
+  h.fail_pending = true;
+}
+
+void chem_check(Ctx& x) {
+  Chem& h = x.chem;
+  if (!h.fail_pending) return;
+  DFMI_HIP(hipEventSynchronize(h.fail_ev));
+  h.fail_pending = false;
+  const int nf = h.fail_host.p[0];
+  DFMI_CHECK(nf == 0, "chemistry: " + std::to_string(nf) + " cell(s) hit the integrator step limit (max_steps = " +
+                          std::to_string(h.max_steps) + "); their RR is not a completed integration");
 }
 
 }  // namespace dfmi

@@ -90,6 +90,11 @@ struct Chem {
   DevBuf<int> perm, bcnt;       // cost-binned cell order; per-block bucket counts / offsets
   std::vector<int> h_idata, h_irs;
   std::vector<double> h_dd;
+  DevBuf<int> fail;             // cells of the last solve that hit max_steps (device counter)
+  PinnedBuf<int> fail_host;     // its copy, behind fail_ev
+  hipEvent_t fail_ev = nullptr;
+  bool fail_pending = false;
+  ~Chem() { if (fail_ev) (void)hipEventDestroy(fail_ev); }
 };
 
 // HIP-event timing of one named kernel (dfmi_kernel_timer / dfmi_kernel_time)
@@ -225,6 +230,7 @@ void y_post_solve(Ctx& x);
 void e_assemble(Ctx& x);
 void e_post_solve(Ctx& x);
 void copy_old(Ctx& x);
+void zero_d_step(Ctx& x, double dt);   // df0DFoam loop body for every cell
 void thermo_rho_from_psi(Ctx& x);
 void thermo_psip0(Ctx& x);
 void thermo_correct_psip_rho(Ctx& x);
@@ -239,6 +245,9 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
                           long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
                           double* xsol, long xstride, const SolverCfg& cfg, bool prebuilt = false);
 void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs);
+void bicg_rows_from_ldu_Y(Ctx& x);
+void bicg_rows_get(Ctx& x, int nsys, const std::string& part, double* host, long count);
+bool species_generic(int S);   // fv_kernels.hip: chunked kernels for S > 16 (or DFMI_SPECIES_GENERIC=1)
 // iterations / initial and final relative residual of the last solve of `eqn` (synchronises)
 SolveStats solve_stats(Ctx& x, const std::string& eqn);
 // system-iterations of the solves of `eqn` since the last reset (synchronises)
@@ -249,10 +258,15 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
 // dnn.hip
 void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* params, const double* xmu,
                 const double* xstd, const double* ymu, const double* ystd, double T_react, double dt_infer);
-void dnn_solve(Ctx& x);
+void dnn_solve(Ctx& x, const char* rho_field);   // RR scaled by rho_field (reference: d_rho_old, dfYEqn.cu:449)
 // chem.hip
 void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd);
-void chem_solve(Ctx& x, double dt);
+// rho_field: the thermo density RR is scaled by (dfChemistryModel.C:771, problem.rhoi = rho_[celli]);
+// inside dfmi_time_step that is rho_old (thermo.rho() before this step's rhoEqn), standalone "rho"
+void chem_solve(Ctx& x, double dt, const char* rho_field);
+void chem_fail_snapshot(Ctx& x);
+// throws when the last solve left cells at the step limit (waits on the snapshot event only)
+void chem_check(Ctx& x);
 // halo.hip
 // One exchange point: cell values of each item's components are sent across processor faces and land
 // in the receiver's neighbour slots (to_slots) or in the extended vector region [C, C+H) (solver vectors).

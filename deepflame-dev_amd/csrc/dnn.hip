@@ -359,7 +359,7 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
   d.ready = true;
 }
 
-void dnn_solve(Ctx& x) {
+void dnn_solve(Ctx& x, const char* rho_field) {
   Dnn& d = x.dnn;
   DFMI_CHECK(d.ready, "DNN model not set (dfmi_dnn_set_model)");
   const int C = x.C, S = x.S, L = (int)d.dims.size() - 1;
@@ -418,7 +418,7 @@ void dnn_solve(Ctx& x) {
     }
     KScope _ks(x, "k_dnn_output");
     hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, nq, d.nmod, idx,
-                       d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f("rho"), x.f("p"), d.dt, RR);
+                       d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f(rho_field), x.f("p"), d.dt, RR);
     DFMI_HIP(hipGetLastError());
   }
 }

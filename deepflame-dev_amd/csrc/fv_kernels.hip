@@ -761,6 +761,345 @@ __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
   Y[(long)inert * C + c] = sum > 0 ? sum : 0;
 }
 
+
+// ------------------------------------------------------------------ species-generic Y kernels
+// Mechanisms beyond the register-resident templates (S > 16, e.g. GRI-scale 53 species, BASELINE
+// config 4): the species loop runs in chunks of CH species held in registers. Every per-species
+// accumulator (gradient, laplacian, matrix coefficients) depends on its own species only, and every
+// cross-species sum (sumYDiffError, hDiffCorrFlux, diffAlphaD and their boundary fields) is carried
+// across chunks in species order, so the results are bitwise those of the sequential restatement
+// (oracle y_prep / y_assemble) -- the same sums in the same order. hDiffCorrFlux needs the finished
+// sumYDiffError, so a second pass re-forms the gradients chunk by chunk (neighbour values come from
+// L2 the second time; cheaper than spilling S x 3 gradients per cell to HBM).
+constexpr int YCH = 8;
+
+// gradient (and, with LAP, the diffAlphaD laplacian) of species s0 .. s0+CH-1 at cell c, divided by V
+template <int CH, bool LAP>
+__device__ __forceinline__ void y_chunk_grad(const MeshView& m, const int8_t* __restrict__ tyY, int S, int s0, int c,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ hai,
+    const double* __restrict__ bhai, const double* __restrict__ alpha, const double* __restrict__ balpha, double ac,
+    double (&g)[CH][3], double (&lap)[CH], double (&yc)[CH]) {
+  const long C = m.C, F = m.F, B = m.B;
+  double ahc[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int s = s0 + j;
+    g[j][0] = 0.0; g[j][1] = 0.0; g[j][2] = 0.0; lap[j] = 0.0;
+    yc[j] = s < S ? Y[s * C + c] : 0.0;
+    ahc[j] = (LAP && s < S) ? ac * hai[s * C + c] : 0.0;
+  }
+  each_face(m, c, [&](int f, int o2, bool own) {
+    const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+    const double ms = m.magSf[f], dcf = m.dc[f];
+    const double an = LAP ? alpha[o2] : 0.0;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int s = s0 + j;
+      if (s >= S) break;
+      const double yn = Y[s * C + o2];
+      const double yf = own ? interp_f(w, yc[j], yn) : interp_f(w, yn, yc[j]);
+      const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+      if (own) { g[j][0] += v0; g[j][1] += v1; g[j][2] += v2; } else { g[j][0] -= v0; g[j][1] -= v1; g[j][2] -= v2; }
+      if (LAP) {
+        const double ahn = an * hai[s * C + o2];
+        const double gam = own ? interp_f(w, ahc[j], ahn) : interp_f(w, ahn, ahc[j]);
+        const double dy = own ? yn - yc[j] : yc[j] - yn;
+        const double v = gam * ms * (dcf * dy);
+        if (own) lap[j] += v; else lap[j] -= v;
+      }
+    }
+  });
+  each_slot(m, tyY, c, [&](int b, int t) {
+    const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int s = s0 + j;
+      if (s >= S) break;
+      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
+      g[j][0] += bs0 * yf; g[j][1] += bs1 * yf; g[j][2] += bs2 * yf;
+      if (LAP) {
+        double v;
+        if (bc_coupled(t)) {
+          const int pc = m.partner[b];
+          const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+          v = interp_b(m.bw[b], ahc[j], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[j]));
+        } else {
+          const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - yc[j]) : 0.0;
+          v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+        }
+        lap[j] += v;
+      }
+    }
+  });
+  const double vol = m.V[c];
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[j][k] = g[j][k] / vol;
+}
+
+// corrected gradient of the chunk's species on a non-coupled slot b of cell c (fvc_grad ... correctBC)
+template <int CH>
+__device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, int S, int s0, int c,
+                                              const double* __restrict__ Y, const double* __restrict__ bY,
+                                              const double (&g)[CH][3], double (&bg)[CH][3]) {
+  const long C = m.C, B = m.B;
+  const double ms = m.bmagSf[b];
+  const double nv[3] = {m.bSf[b] / ms, m.bSf[B + b] / ms, m.bSf[2 * B + b] / ms};
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    const int s = s0 + j;
+    if (s >= S) break;
+    const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
+    const double corr = sn - (nv[0] * g[j][0] + nv[1] * g[j][1] + nv[2] * g[j][2]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bg[j][k] = g[j][k] + nv[k] * corr;
+  }
+}
+
+template <int CH>
+__global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int8_t* __restrict__ tyY,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ hai, const double* __restrict__ bhai,
+    const double* __restrict__ alpha, const double* __restrict__ balpha, double* __restrict__ sumE,
+    double* __restrict__ bsumE, double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD,
+    double* __restrict__ gout) {
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, B = m.B;
+  const double ac = alpha[c], vol = m.V[c];
+  double se[3] = {0.0, 0.0, 0.0}, dad = 0.0;
+  // pass 1: gradients + laplacians -> sumYDiffError, diffAlphaD; boundary sumYDiffError summed in place
+  for (int s0 = 0; s0 < S; s0 += CH) {
+    double g[CH][3], lap[CH], yc[CH];
+    y_chunk_grad<CH, true>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
+    if (gout) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (s0 + j < S)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) gout[(3L * (s0 + j) + k) * C + c] = g[j][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (s0 + j < S) se[k] += rhoD[(s0 + j) * C + c] * g[j][k];
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      if (s0 + j < S) dad = dad + lap[j] / vol;
+    each_slot(m, tyY, c, [&](int b, int t) {
+      if (bc_coupled(t)) return;
+      double bg[CH][3];
+      y_chunk_bgrad<CH>(m, t, b, S, s0, c, Y, bY, g, bg);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        double a = s0 == 0 ? 0.0 : bsumE[k * B + b];
+#pragma unroll
+        for (int j = 0; j < CH; ++j)
+          if (s0 + j < S) a += brhoD[(s0 + j) * B + b] * bg[j][k];
+        bsumE[k * B + b] = a;
+      }
+    });
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) sumE[k * C + c] = se[k];
+  dAD[c] = dad;
+  // pass 2: hDiffCorrFlux = sum_i hai_i (rhoD_i grad Y_i - Y_i sumYDiffError) (and on the slots)
+  double hd[3] = {0.0, 0.0, 0.0};
+  for (int s0 = 0; s0 < S; s0 += CH) {
+    double g[CH][3], lap[CH], yc[CH];
+    y_chunk_grad<CH, false>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int s = s0 + j;
+        if (s < S) hd[k] += hai[s * C + c] * (rhoD[s * C + c] * g[j][k] - yc[j] * se[k]);
+      }
+    each_slot(m, tyY, c, [&](int b, int t) {
+      if (bc_coupled(t)) return;
+      double bg[CH][3];
+      y_chunk_bgrad<CH>(m, t, b, S, s0, c, Y, bY, g, bg);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double bse = bsumE[k * B + b];
+        double a = s0 == 0 ? 0.0 : bhD[k * B + b];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int s = s0 + j;
+          if (s < S) a += bhai[s * B + b] * (brhoD[s * B + b] * bg[j][k] - bY[s * B + b] * bse);
+        }
+        bhD[k * B + b] = a;
+      }
+    });
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) hD[k * C + c] = hd[k];
+}
+
+// YEqn matrices, chunked over species (LDU form: the dfmi_assemble("Y") inspection path)
+template <int CH>
+__global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const int8_t* __restrict__ tyY, int inert,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
+    double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
+    double* __restrict__ bc) {
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  const double vol = m.V[c];
+  for (int s0 = 0; s0 < S; s0 += CH) {
+    double d1 = 0.0, d2 = 0.0;
+    double dL[CH], rc[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) { dL[j] = 0.0; rc[j] = s0 + j < S ? rhoD[(s0 + j) * C + c] : 0.0; }
+    each_face(m, c, [&](int f, int o2, bool own) {
+      const double ph = phi[f], pu = phiUc[f];
+      const double wu = ph >= 0 ? 1.0 : 0.0;
+      const double L1 = -wu * ph, U1 = L1 + ph;
+      const double L2 = -wu * pu, U2 = L2 + pu;
+      if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+      const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
+      const double Ls = L1 + L2, Us = U1 + U2;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int s = s0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const double rn = rhoD[s * C + o2];
+        const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
+        dL[j] -= UL;
+        if (own) { lower[s * F + f] = Ls - UL; upper[s * F + f] = Us - UL; }
+      }
+    });
+    const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+    const double ro = m.rdt * rho_old[c];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int s = s0 + j;
+      if (s >= S) break;
+      if (s == inert) continue;
+      diag[s * C + c] = dd - dL[j];
+      src[s * C + c] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
+    }
+    each_slot(m, tyY, c, [&](int b, int t) {
+      const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int s = s0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
+        const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+        const double gam = bc_coupled(t) ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+        const double pG = gam * m.bmagSf[b];
+        ic[s * B + b] = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+        bc[s * B + b] = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+      }
+    });
+  }
+}
+
+// YEqn in the solver's ELL rows, chunked over species (production path for S > 16)
+template <int CH>
+__global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, const int8_t* __restrict__ tyY, int inert,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
+    double* __restrict__ dS, double* __restrict__ rhs) {
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= m.C) return;
+  const long C = m.C, B = m.B;
+  const double vol = m.V[c];
+  for (int s0 = 0; s0 < S; s0 += CH) {
+    double d1 = 0.0, d2 = 0.0;
+    double dL[CH], rc[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) { dL[j] = 0.0; rc[j] = s0 + j < S ? rhoD[(s0 + j) * C + c] : 0.0; }
+    int k = 0;
+    each_face(m, c, [&](int f, int o2, bool own) {
+      const double ph = phi[f], pu = phiUc[f];
+      const double wu = ph >= 0 ? 1.0 : 0.0;
+      const double L1 = -wu * ph, U1 = L1 + ph;
+      const double L2 = -wu * pu, U2 = L2 + pu;
+      if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+      const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
+      const double Ls = L1 + L2, Us = U1 + U2;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int s = s0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const double rn = rhoD[s * C + o2];
+        const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
+        dL[j] -= UL;
+        val[((long)ss * W + k) * C + c] = own ? Us - UL : Ls - UL;
+      }
+      ++k;
+    });
+    const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+    const double ro = m.rdt * rho_old[c];
+    double dg[CH], sr[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int s = s0 + j;
+      dg[j] = dd - dL[j];
+      sr[j] = s < S ? ro * Y[s * C + c] * vol + vol * RR[s * C + c] : 0.0;
+    }
+    each_slot(m, tyY, c, [&](int b, int t) {
+      const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+      const bool cp = bc_coupled(t);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int s = s0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
+        const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+        const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+        const double pG = gam * m.bmagSf[b];
+        const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+        const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+        dg[j] += icv;
+        if (cp) val[((long)ss * W + k) * C + c] = -bcv;
+        else sr[j] += bcv;
+      }
+      if (cp) ++k;
+    });
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int s = s0 + j;
+      if (s >= S) break;
+      if (s == inert) continue;
+      const int ss = s < inert ? s : s - 1;
+      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + c] = 0.0;
+      dS[ss * Ce + c] = dg[j];
+      rhs[ss * Ce + c] = sr[j];
+    }
+  }
+}
+
+__global__ void k_y_inert_gen(int C, int S, int inert, double* __restrict__ Y) {
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sum = 0;
+  for (int s = 0; s < S; ++s) {
+    if (s == inert) continue;
+    double yi = Y[(long)s * C + c];
+    yi = yi > 0 ? yi : 0;
+    Y[(long)s * C + c] = yi;
+    sum += yi;
+  }
+  sum = 1 - sum;
+  Y[(long)inert * C + c] = sum > 0 ? sum : 0;
+}
+
 // ------------------------------------------------------------------ EEqn (EEqn.H:12-45; dfEEqn.cu:108-264)
 __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __restrict__ tyH, const int8_t* __restrict__ tyK,
     const double* __restrict__ he, const double* __restrict__ bhe, const double* __restrict__ rho,
@@ -812,6 +1151,28 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
     ic[b] = bphi[b] * qc.vic - pG * ql.gic;
     bc[b] = -bphi[b] * qc.vbc - (-pG * ql.gbc);
   });
+}
+
+// ------------------------------------------------------------------ df0DFoam species update
+// YEqn.H of df0DFoam (applications/solvers/df0DFoam/YEqn.H): fvm::ddt(rho, Yi) == RR_i per cell (no
+// transport), solved exactly: Y_i = (rdt rho_old Y_i V + V RR_i) / (rdt rho V); Yi.max(0); inert = 1 - sum.
+__global__ void k_zero_d_species(int C, int S, int inert, double rdt, const double* __restrict__ V,
+                                 const double* __restrict__ rho_old, const double* __restrict__ rho,
+                                 const double* __restrict__ RR, double* __restrict__ Y) {
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double vol = V[c];
+  const double dg = rdt * rho[c] * vol, ro = rdt * rho_old[c];
+  double sum = 0.0;
+  for (int s = 0; s < S; ++s) {
+    if (s == inert) continue;
+    double y = (ro * Y[(long)s * C + c] * vol + vol * RR[(long)s * C + c]) / dg;
+    y = y > 0 ? y : 0;
+    Y[(long)s * C + c] = y;
+    sum += y;
+  }
+  sum = 1 - sum;
+  Y[(long)inert * C + c] = sum > 0 ? sum : 0;
 }
 
 // ------------------------------------------------------------------ elementwise thermo bookkeeping
@@ -923,14 +1284,20 @@ void p_post_solve(Ctx& x) {
   LAUNCH(k_kinetic_slots, x.B, x.B, x.f("boundary_U"), x.f("boundary_K"));
 }
 
-#define DFMI_SWITCH_S(S, CALL)                                                                   \
-  switch (S) {                                                                                   \
+// species count: register-resident templates for 2..16 species, the chunked kernels above otherwise
+// (or always, with DFMI_SPECIES_GENERIC=1 -- the parity tests run both on the same mechanisms)
+bool species_generic(int S) {
+  const char* e = std::getenv("DFMI_SPECIES_GENERIC");
+  return S > 16 || (e && std::atoi(e) != 0);
+}
+#define DFMI_SWITCH_S(S, CALL, GEN)                                                              \
+  if (species_generic(S)) { GEN; } else switch (S) {                                             \
     case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break; \
     case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break; \
     case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break;                  \
     case 13: CALL(13); break; case 14: CALL(14); break; case 15: CALL(15); break;                  \
     case 16: CALL(16); break;                                                                      \
-    default: throw Error("dfmi: species count " + std::to_string(S) + " not instantiated (2..16)"); \
+    default: throw Error("dfmi: species count " + std::to_string(S) + " not supported");          \
   }
 
 void y_prep(Ctx& x) {
@@ -940,7 +1307,11 @@ void y_prep(Ctx& x) {
                         x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),    \
                         x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"),         \
                         x.f("diffAlphaD"), gout)
-  DFMI_SWITCH_S(x.S, CALL)
+  DFMI_SWITCH_S(x.S, CALL,
+                LAUNCH(k_y_prep_gen<YCH>, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
+                       x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"),
+                       x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),
+                       x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout))
 #undef CALL
   halo_fields(x, {"sumYDiffError", "hDiffCorrFlux"});
   LAUNCH(k_phiuc_face, x.F, m, x.f("sumYDiffError"), x.f("phiUc"));
@@ -953,7 +1324,10 @@ void y_assemble(Ctx& x) {
 #define CALL(NS) LAUNCH(k_y_assemble<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
                         x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p)
-  DFMI_SWITCH_S(x.S, CALL)
+  DFMI_SWITCH_S(x.S, CALL,
+                LAUNCH(k_y_assemble_gen<YCH>, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
+                       x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"),
+                       x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p))
 #undef CALL
 }
 
@@ -962,13 +1336,16 @@ void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs
 #define CALL(NS) LAUNCH(k_y_assemble_ell<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
                         x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs)
-  DFMI_SWITCH_S(x.S, CALL)
+  DFMI_SWITCH_S(x.S, CALL,
+                LAUNCH(k_y_assemble_ell_gen<YCH>, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"),
+                       x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),
+                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs))
 #undef CALL
 }
 
 void y_post_solve(Ctx& x) {
 #define CALL(NS) LAUNCH(k_y_inert<NS>, x.C, x.C, x.inert, x.f("Y"))
-  DFMI_SWITCH_S(x.S, CALL)
+  DFMI_SWITCH_S(x.S, CALL, LAUNCH(k_y_inert_gen, x.C, x.C, x.S, x.inert, x.f("Y")))
 #undef CALL
   k_bc_correct(x, "Y", x.f("Y"), x.f("boundary_Y"), x.S);
   halo_fields(x, {"Y"});
@@ -989,6 +1366,20 @@ void e_assemble(Ctx& x) {
 void e_post_solve(Ctx& x) {
   k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
   halo_fields(x, {"he"});
+}
+
+// one df0DFoam time step (df0DFoam.C:99-113, constantProperty pressure): chemistry.solve(deltaT) on
+// every cell (a closed isothermal reactor from setState_TPY, RR scaled by the thermo rho), YEqn
+// (ddt(rho, Yi) == RR), EEqn (he held: constant pressure) -> correctThermo (T from he), rho = thermo.rho()
+void zero_d_step(Ctx& x, double dt) {
+  DFMI_CHECK(x.chem.mode == 1 || x.chem.mode == 2, "0D step: chemistry mode must be 1 (ODE) or 2 (DNN)");
+  DFMI_HIP(hipMemcpyAsync(x.f("rho_old"), x.f("rho"), sizeof(double) * x.C, hipMemcpyDeviceToDevice, x.stream));
+  if (x.chem.mode == 1) chem_solve(x, dt, "rho");
+  else dnn_solve(x, "rho");
+  LAUNCH(k_zero_d_species, x.C, x.C, x.S, x.inert, 1.0 / dt, x.V.p, x.f("rho_old"), x.f("rho"), x.f("RR"), x.f("Y"));
+  k_bc_correct(x, "Y", x.f("Y"), x.f("boundary_Y"), x.S);
+  thermo_correct(x, false);
+  thermo_rho_from_psi(x);
 }
 
 void thermo_rho_from_psi(Ctx& x) {   // dfThermo::updateRho (dfThermo.cu:673-679)

@@ -565,6 +565,44 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   *val = x.ws.buf.p + BCG_VECS * N;
 }
 
+// the YEqn rows the production path writes straight from the assembly (y_assemble_ell), rebuilt here
+// from the LDU matrices by the generic fold (k_ell_build) -- the inspection path the parity tests
+// compare the fused kernel against
+void bicg_rows_from_ldu_Y(Ctx& x) {
+  std::vector<int> map;
+  for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
+  const int nsys = (int)map.size();
+  double *val, *dS, *rhs;
+  bicg_layout(x, nsys, &val, &dS, &rhs);
+  const long C = x.C, Ce = (long)x.C + x.H;
+  x.ws.sysmap.upload(map.data(), nsys, x.stream);
+  Matrix& A = x.mY;
+  Sys q{A.lower, A.upper, A.diag, A.source, A.ic, A.bc, x.F, x.F, C, C, x.B, x.f("Y"), C};
+  const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
+  hipLaunchKernelGGL(k_ell_build, dim3(nblk, nsys), dim3(TPB), 0, x.stream, x.view(), x.st("Y"), q,
+                     (const int*)x.ws.sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs);
+  DFMI_HIP(hipGetLastError());
+}
+
+// copy part ("val" [nsys][W][C], "dS" / "rhs" [nsys][C]) of the BiCGStab rows of nsys systems to the host
+void bicg_rows_get(Ctx& x, int nsys, const std::string& part, double* host, long count) {
+  double *val, *dS, *rhs;
+  bicg_layout(x, nsys, &val, &dS, &rhs);
+  const long C = x.C, Ce = (long)x.C + x.H;
+  const int W = x.ell.W;
+  if (part == "val") {
+    DFMI_CHECK(count == (long)nsys * W * C, "solver rows: 'val' holds nsys * W * C values");
+    DFMI_HIP(hipMemcpyAsync(host, val, count * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  } else {
+    DFMI_CHECK(part == "dS" || part == "rhs", "solver rows: part is 'val', 'dS' or 'rhs'");
+    DFMI_CHECK(count == (long)nsys * C, "solver rows: 'dS' / 'rhs' hold nsys * C values");
+    const double* src = part == "dS" ? dS : rhs;
+    for (int s = 0; s < nsys; ++s)
+      DFMI_HIP(hipMemcpyAsync(host + (long)s * C, src + s * Ce, C * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  }
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+}
+
 double solver_work(Ctx& x, const std::string& eqn, bool reset) {
   const int k = work_slot(eqn);
   if (x.work.n == 0) return 0.0;

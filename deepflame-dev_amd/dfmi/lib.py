@@ -54,6 +54,7 @@ SIGNATURES = {
     "dfmi_time_step": [_P, C.c_int], "dfmi_sync": [_P],
     "dfmi_assemble": [_P, C.c_char_p],
     "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
+    "dfmi_get_solver_rows": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
     "dfmi_set_solver": [_P, C.c_char_p, C.c_int, C.c_double, C.c_double],
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
     "dfmi_solver_work": [_P, C.c_char_p, _DP, C.c_int],
@@ -66,6 +67,8 @@ SIGNATURES = {
     "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
     "dfmi_chem_set_options": [_P, C.c_int, C.c_double, C.c_double, C.c_double],
     "dfmi_chem_solve": [_P, C.c_double],
+    "dfmi_chem_set_max_steps": [_P, C.c_int],
+    "dfmi_zero_d_step": [_P, C.c_double, C.c_int],
     "dfmi_chem_info": [_P, _IP],
     "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
                            C.c_double],
@@ -210,6 +213,11 @@ class Context:
         self._call("dfmi_get_matrix", self.h, eqn.encode(), part.encode(), _dp(out), int(n))
         return out
 
+    def get_solver_rows(self, eqn, part, n):
+        out = np.empty(n, dtype=np.float64)
+        self._call("dfmi_get_solver_rows", self.h, eqn.encode(), part.encode(), _dp(out), int(n))
+        return out
+
     # --- processes
     def call(self, name, *args):
         self._call("dfmi_" + name, self.h, *args)
@@ -236,6 +244,13 @@ class Context:
 
     def chem_solve(self, dt):
         self._call("dfmi_chem_solve", self.h, float(dt))
+
+    def zero_d_step(self, dt, n_steps=1):
+        """df0DFoam time steps on every cell (include/dfmi.h dfmi_zero_d_step)"""
+        self._call("dfmi_zero_d_step", self.h, float(dt), int(n_steps))
+
+    def chem_set_max_steps(self, n):
+        self._call("dfmi_chem_set_max_steps", self.h, int(n))
 
     def chem_info(self):
         g = C.c_int()

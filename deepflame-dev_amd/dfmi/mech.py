@@ -74,7 +74,10 @@ def read_yaml_mechanism(path: str) -> dict:
         out["W"].append(sum(ATOMIC_W[e] * c for e, c in comp.items()))
         th = s["thermo"]
         tr = th["temperature-ranges"]
-        lo, hi = th["data"]
+        if len(th["data"]) == 1:        # one range (e.g. AR in gri30): same block on both sides of T_mid
+            lo = hi = th["data"][0]
+        else:
+            lo, hi = th["data"]
         row = [float(tr[1])] + [float(x) for x in hi] + [float(x) for x in lo]
         out["nasa"].append(row)
         out["trange"].append((float(tr[0]), float(tr[-1])))

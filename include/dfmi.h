@@ -108,17 +108,23 @@ int dfmi_U_get_HbyA(dfmi_ctx* ctx);             /* dfUEqn::getHbyA (dfUEqn.cu:82
 int dfmi_p_process(dfmi_ctx* ctx);              /* dfpEqn::process (dfpEqn.cu:379-546) */
 int dfmi_post_time_step(dfmi_ctx* ctx);         /* dfMatrixDataBase::postTimeStep (:519) */
 /* the whole loop body above with n_corr pressure correctors */
-int dfmi_time_step(dfmi_ctx* ctx, int n_corr);
+int dfmi_time_step(dfmi_ctx* ctx, int n_corr);   /* non-zero also when chemistry hit its step limit */
 int dfmi_sync(dfmi_ctx* ctx);
 /* correct_boundary_conditions_{scalar,vector} (dfMatrixOpBase.cu:2402-2491) for field in
  * {"U","p","he","T","rho","K","Y"} using that field's patch types */
 int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field);
 
 /* ---- matrix inspection (the reference DEBUG_CHECK_LDU / compareResult path, dfYEqn.cu:566-572) */
-/* eqn in {"rho","U","Y","E","p"}: run that equation's assembly only (no solve) */
+/* eqn in {"rho","U","Y","E","p","HbyA","Y_ell","Y_ell_ref"}: run that equation's assembly only (no solve) */
 int dfmi_assemble(dfmi_ctx* ctx, const char* eqn);
 /* part in {"lower","upper","diag","source","source_solve","internal_coeffs","boundary_coeffs"} */
 int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count);
+/* the solver's rows of the YEqn batch after dfmi_assemble("Y_ell") (the production path: assembly
+ * written straight into the rows) or dfmi_assemble("Y_ell_ref") (LDU assembly + the generic
+ * fvMatrix::addBoundaryDiag/Source fold, the role of ldu_to_csr, dfMatrixOpBase.cu:2276-2336):
+ * part "val" [S-1][W][C] (W = coupling entries per row), "dS" (diag + internalCoeffs) or "rhs"
+ * [S-1][C]. eqn must be "Y". */
+int dfmi_get_solver_rows(dfmi_ctx* ctx, const char* eqn, const char* part, double* host, long count);
 /* solver controls (amgxUOptions / amgxpOptions): eqn in {"U","Y","E","p"} */
 int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, double abs_tol);
 /* preconditioner: "jacobi" (all) or "amg" (p; aggregation AMG V-cycle, the amgxpOptions
@@ -144,9 +150,21 @@ int dfmi_chem_set_mechanism(dfmi_ctx* ctx, int n_reactions, const int* idata, co
 /* mode 0 off, 1 stiff ODE integration each YEqn (chemistry->solve(deltaT)), 2 DNN surrogate;
  * tolerances on mass fractions (reference CVODE: relTol 1e-6, absTol 1e-10); cells below T_min get RR = 0 */
 int dfmi_chem_set_options(dfmi_ctx* ctx, int mode, double rtol, double atol, double T_min);
-/* integrate every cell over dt at fixed T, rho -> field "RR" = (Y(dt) - Y) rho / dt; field
- * "chem_stats" [2][C] = accepted / rejected steps (-1: step limit hit) */
+/* integrate every cell over dt as a closed constant-volume reactor at fixed T whose state is
+ * Cantera's setState_TPY(T, p, Y) (Y clipped at 0 and normalised, density p W/(R T);
+ * dfChemistryModel.C:755) -> field "RR" = (Y(dt) - Y) rho / dt with rho the field "rho" (the thermo
+ * density, problem.rhoi; inside dfmi_time_step / dfmi_Y_process: "rho_old", the thermo density before
+ * this step's rhoEqn). Field "chem_stats" [3][C] = accepted steps (-1: step limit hit), rejected steps,
+ * the step size the integration ended with (the next solve's first step). Returns non-zero when any
+ * cell hit the step limit (its RR is then not a completed integration). */
 int dfmi_chem_solve(dfmi_ctx* ctx, double dt);
+/* n_steps df0DFoam time steps (applications/solvers/df0DFoam/df0DFoam.C:99-113, YEqn.H, EEqn.H;
+ * zeroDReactor constantProperty pressure): per step chemistry.solve(dt) on every cell, YEqn
+ * ddt(rho, Yi) == RR_i (Yi.max(0), inert = 1 - sum), he held, correctThermo (T from he), rho = p psi.
+ * Every cell is an independent 0D reactor (BASELINE config 1). */
+int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps);
+/* integrator step budget per cell and solve (default 100000); exceeding it is an error of the call */
+int dfmi_chem_set_max_steps(dfmi_ctx* ctx, int max_steps);
 /* which integrator the last solve used: 0 data-driven generic kernel, > 0 a mechanism compiled in
  * by dfmi/chem_codegen.py (1 Burke2012_s9r23, 2 ES80_H2-7-16) */
 int dfmi_chem_info(dfmi_ctx* ctx, int* generated);
@@ -162,7 +180,8 @@ int dfmi_chem_info(dfmi_ctx* ctx, int* generated);
 int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* dims, const float* params,
                        const double* x_mu, const double* x_std, const double* y_mu, const double* y_std,
                        double T_react, double dt_infer);
-/* run the surrogate on the current T, p, rho, Y -> field "RR" (0 for non-reacting cells) */
+/* run the surrogate on the current T, p, Y -> field "RR" (0 for non-reacting cells), scaled by field
+ * "rho" (inside dfmi_time_step: "rho_old", as the reference passes d_rho_old, dfYEqn.cu:449) */
 int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting);
 /* reacting cells of the last inference; algorithmic hidden-layer GEMM flops since the last call */
 int dfmi_dnn_stats(dfmi_ctx* ctx, int* n_reacting, double* gemm_flops);

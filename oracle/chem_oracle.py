@@ -100,8 +100,15 @@ class Kinetics:
                     w[m.prod[r, j]] += m.nu_p[r, j] * q[r]
         return w
 
+    def reactor_state(self, T, p, Y):
+        """Cantera setState_TPY(T, p, Y) (dfChemistryModel.C:755): Phase::setMassFractions clips at 0 and
+        normalises; density = p * meanW / (R T). Returns (density, normalised Y)."""
+        y = np.maximum(np.asarray(Y, dtype=np.float64), 0.0)
+        y = y / y.sum()
+        return p / ((y / self.W).sum() * RU * T), y
+
     def integrate_cell(self, T, rho, Y, dt, rtol=1e-11, atol=1e-22):
-        """Constant T, rho reactor over dt -> Y(dt)."""
+        """Closed constant-volume reactor at fixed T and density rho over dt -> Y(dt)."""
         C0 = rho * np.asarray(Y) / self.W
         consts = self.rate_constants(T)
         f = lambda t, C: self.production_rates(T, C, consts)
@@ -111,10 +118,16 @@ class Kinetics:
         return sol.y[:, -1] * self.W / rho
 
     def reaction_rates(self, T, p, rho, Y, dt, **kw):
-        """RR [S, n] = (Y(dt) - Y) rho / dt for each cell (columns of Y)."""
+        """RR [S, n] = (Y(dt) - Y) rho / dt for each cell (columns of Y), dfChemistryModel::solveSingle
+        (:737-780): the reactor state is setState_TPY(T, p, Y); `rho` is the thermo density the
+        difference is scaled by (problem.rhoi = rho_[celli], :807). p = None: the reactor runs at `rho`."""
         Y = np.asarray(Y)
         out = np.zeros_like(Y)
         for c in range(Y.shape[1]):
-            Yn = self.integrate_cell(float(T[c]), float(rho[c]), Y[:, c], dt, **kw)
+            if p is None:
+                rc, y0 = float(rho[c]), Y[:, c]
+            else:
+                rc, y0 = self.reactor_state(float(T[c]), float(p[c]), Y[:, c])
+            Yn = self.integrate_cell(float(T[c]), rc, y0, dt, **kw)
             out[:, c] = (Yn - Y[:, c]) * rho[c] / dt
         return out

@@ -293,3 +293,51 @@ class Oracle:
             self.rho_eqn()
         a["rho"][...] = a["p"] * a["psi"]
         a["boundary_rho"][...] = a["boundary_p"] * a["boundary_psi"]
+
+
+def thermo_points(table, T, he, p, Y, fixT):
+    """oracle thermo_point over n states (Y [S, n]): returns dict T, he, psi, rho, mu, alpha, rhoD, hai"""
+    L = lib()
+    L.orc_set_thermo(table.S, _dp(np.ascontiguousarray(table.W)), _dp(np.ascontiguousarray(table.nasa)),
+                     _dp(np.ascontiguousarray(table.visc)), _dp(np.ascontiguousarray(table.cond)),
+                     _dp(np.ascontiguousarray(table.bdiff)))
+    n = np.size(T)
+    o = {"T": np.array(T, dtype=np.float64).ravel().copy(), "he": np.array(he, dtype=np.float64).ravel().copy(),
+         "p": np.array(p, dtype=np.float64).ravel().copy(), "Y": np.ascontiguousarray(Y, dtype=np.float64).reshape(table.S, n)}
+    for k in ("psi", "rho", "mu", "alpha"):
+        o[k] = np.zeros(n)
+    o["rhoD"] = np.zeros((table.S, n)); o["hai"] = np.zeros((table.S, n))
+    rc = L.orc_thermo_points(n, 1 if fixT else 0, _dp(o["T"]), _dp(o["he"]), _dp(o["p"]), _dp(o["Y"]), _dp(o["psi"]),
+                             _dp(o["rho"]), _dp(o["mu"]), _dp(o["alpha"]), _dp(o["rhoD"]), _dp(o["hai"]))
+    if rc != 0:
+        raise RuntimeError("orc_thermo_points failed")
+    return o
+
+
+def zero_d_trajectory(table, kin, T0, p0, Y0, dt, n_steps, rtol=1e-12, atol=1e-22, inert=None):
+    """df0DFoam (applications/solvers/df0DFoam/df0DFoam.C:99-113, YEqn.H, EEqn.H; constantProperty
+    pressure) for one cell: per step chemistry.solve(dt) -- isothermal closed reactor from
+    setState_TPY(T, p, Y), RR scaled by the thermo rho --, YEqn ddt(rho, Yi) == RR_i (Yi.max(0),
+    inert = 1 - sum), he held, correctThermo (T from he), rho = thermo.rho(). Returns T [n+1], Y [n+1, S]."""
+    S = table.S
+    inert = S - 1 if inert is None else inert
+    st = thermo_points(table, [T0], [0.0], [p0], np.asarray(Y0, dtype=np.float64).reshape(S, 1), True)
+    T, he, rho, Y = st["T"][0], st["he"][0], st["rho"][0], np.asarray(Y0, dtype=np.float64).copy()
+    Ts, Ys = [T], [Y.copy()]
+    for _ in range(n_steps):
+        rho_old = rho
+        RR = kin.reaction_rates(np.array([T]), np.array([p0]), np.array([rho]), Y.reshape(S, 1), dt,
+                                rtol=rtol, atol=atol)[:, 0]
+        rdt = 1.0 / dt
+        Yn = (rdt * rho_old * Y * 1.0 + 1.0 * RR) / (rdt * rho * 1.0)
+        Yn = np.maximum(Yn, 0.0)
+        tot = 0.0
+        for s_ in range(S):
+            if s_ != inert:
+                tot += Yn[s_]
+        Yn[inert] = max(1.0 - tot, 0.0)
+        Y = Yn
+        st = thermo_points(table, [T], [he], [p0], Y.reshape(S, 1), False)
+        T, rho = st["T"][0], st["rho"][0]
+        Ts.append(T); Ys.append(Y.copy())
+    return np.array(Ts), np.array(Ys)

@@ -32,7 +32,18 @@ def ulp_diff(a, b):
     return int(np.abs(ia - ib).max()) if a.size else 0
 
 
-def rel_err(a, b):
+def rel_err(a, b, floor=1e-12):
+    """max |a - b| relative to the reference's own magnitude, per component: a [k, n] field (vector
+    components, species) is judged row by row against max |b_row|, so trace species (H2O2, HO2 at
+    1e-6 of the major ones) are held to the same relative bar as the major ones. Rows whose magnitude
+    is below `floor` x the field's maximum (identically-zero species) are judged against that floor."""
     a = np.asarray(a, dtype=np.float64); b = np.asarray(b, dtype=np.float64)
-    scale = max(np.abs(b).max(), 1e-300)
-    return float(np.abs(a - b).max() / scale)
+    if a.size == 0:
+        return 0.0
+    if b.ndim == 1:
+        scale = max(np.abs(b).max(), 1e-300)
+        return float(np.abs(a - b).max() / scale)
+    a2 = a.reshape(a.shape[0], -1); b2 = b.reshape(b.shape[0], -1)
+    top = max(np.abs(b2).max(), 1e-300)
+    scale = np.maximum(np.abs(b2).max(axis=1), floor * top)
+    return float((np.abs(a2 - b2).max(axis=1) / scale).max())

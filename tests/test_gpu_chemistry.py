@@ -1,5 +1,9 @@
 """GPU stiff-chemistry integrator (A10) vs the CPU oracle (SciPy BDF, tight tolerances).
 
+Semantics (dfChemistryModel::solveSingle, dfChemistryModel.C:737-780): the reactor starts from
+setState_TPY(T, p, Y) -- its density is p W/(R T), not the solver's rho -- and RR is scaled by the
+thermo density (problem.rhoi). The tests set rho != p W/(R T) so both roles are pinned.
+
 RR = (Y(dt) - Y) rho / dt is a difference of nearly equal numbers, so integrator tolerances show up
 amplified: with tight GPU tolerances (rtol 1e-8) RR agrees to 1e-5 of its per-species scale; with
 the reference's CVODE tolerances (rtol 1e-6, atol 1e-10) to 2e-3."""
@@ -41,8 +45,9 @@ def _states(ym, n, seed=0):
     Y /= Y.sum(axis=0)
     T = 300.0 + 2200.0 * rng.random(n)
     Wm = 1.0 / (Y / ym["W"][:, None]).sum(axis=0)
-    rho = 101325.0 * Wm / (8314.46261815324 * T)
-    return T, rho, Y
+    p = 101325.0 * (1.0 + 0.05 * rng.standard_normal(n))
+    rho = p * Wm / (8314.46261815324 * T) * (1.0 + 0.02 * rng.standard_normal(n))   # thermo rho != reactor rho
+    return T, p, rho, Y
 
 
 @pytest.mark.parametrize("method", ["ros3", "ros3-generic", "extrap"])
@@ -55,12 +60,12 @@ def test_chem_rr_matches_oracle(mech, method, monkeypatch):
         monkeypatch.setenv("DFMI_CHEM_GENERIC", "1")
     ctx, m, ym, mc = _setup(*mech)
     C = m.n_cells
-    T, rho, Y = _states(ym, C)
-    ctx.set_field("T", T); ctx.set_field("rho", rho); ctx.set_field("Y", Y)
+    T, p, rho, Y = _states(ym, C)
+    ctx.set_field("T", T); ctx.set_field("p", p); ctx.set_field("rho", rho); ctx.set_field("Y", Y)
     dt = 1e-6
     kin = Kinetics(mc, ym["nasa"], ym["W"])
     idx = np.arange(0, C, 7)                     # oracle on a subset (BDF is slow in Python)
-    ref = kin.reaction_rates(T[idx], None, rho[idx], Y[:, idx], dt)
+    ref = kin.reaction_rates(T[idx], p[idx], rho[idx], Y[:, idx], dt)
     # per-species scale, floored for species that do not react (N2: rounding-level RR)
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
@@ -106,8 +111,8 @@ def test_chem_cost_binning_bitwise(mech, generic, monkeypatch):
         monkeypatch.setenv("DFMI_CHEM_GENERIC", "1")
     ctx, m, ym, mc = _setup(*mech, n=(16, 16, 8))
     C = m.n_cells
-    T, rho, Y = _states(ym, C, seed=3)
-    ctx.set_field("T", T); ctx.set_field("rho", rho); ctx.set_field("Y", Y)
+    T, p, rho, Y = _states(ym, C, seed=3)
+    ctx.set_field("T", T); ctx.set_field("p", p); ctx.set_field("rho", rho); ctx.set_field("Y", Y)
     ctx.chem_set_options(1)
     out = {}
     for flag in ("0", "1"):
@@ -121,3 +126,39 @@ def test_chem_cost_binning_bitwise(mech, generic, monkeypatch):
     assert st[0].min() >= 1 and (st[0] + st[1]).max() > (st[0] + st[1]).min()   # costs really differ
     assert np.array_equal(out["0"][0], out["1"][0])
     assert np.array_equal(out["0"][1], out["1"][1])
+
+
+def test_chem_density_roles():
+    """The reactor density comes from (T, p, Y) -- scaling the solver rho leaves the integration alone
+    -- and RR scales linearly with the thermo density it is handed."""
+    ctx, m, ym, mc = _setup("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt")
+    C = m.n_cells
+    T, p, rho, Y = _states(ym, C, seed=5)
+    ctx.set_field("T", T); ctx.set_field("p", p); ctx.set_field("Y", Y)
+    ctx.chem_set_options(1)
+    out = []
+    for f in (1.0, 1.25):
+        ctx.set_field("rho", rho * f)
+        ctx.set_field("chem_stats", np.zeros((3, C)))
+        ctx.chem_solve(1e-6)
+        out.append(ctx.get_field("RR", (mc.S, C)))
+    np.testing.assert_allclose(out[1], 1.25 * out[0], rtol=1e-14, atol=0)
+
+
+def test_chem_step_limit_is_an_error():
+    """A cell that runs out of integrator steps makes dfmi_chem_solve (and dfmi_time_step) fail
+    instead of leaving a partly integrated RR behind (chem.hip: failure counter)."""
+    from dfmi.lib import DfmiError
+    ctx, m, ym, mc = _setup("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt")
+    C = m.n_cells
+    T, p, rho, Y = _states(ym, C, seed=9)
+    ctx.set_field("T", T); ctx.set_field("p", p); ctx.set_field("rho", rho); ctx.set_field("Y", Y)
+    ctx.chem_set_options(1, rtol=1e-10, atol=1e-16)
+    ctx.chem_set_max_steps(1)
+    ctx.set_field("chem_stats", np.zeros((3, C)))
+    with pytest.raises(DfmiError, match="step limit"):
+        ctx.chem_solve(1e-6)
+    assert (ctx.get_field("chem_stats", (3, C))[0] < 0).any()
+    ctx.chem_set_max_steps(100000)
+    ctx.set_field("chem_stats", np.zeros((3, C)))
+    ctx.chem_solve(1e-6)                      # a sufficient budget clears the error

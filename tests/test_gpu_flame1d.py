@@ -75,6 +75,7 @@ def test_flame1d_front_chemistry_matches_oracle():
         ctx.time_step(2)
     T = ctx.get_field("T", (m.n_cells,))
     rho = ctx.get_field("rho", (m.n_cells,))
+    p = ctx.get_field("p", (m.n_cells,))
     Y = ctx.get_field("Y", (t.S, m.n_cells))
     front = np.flatnonzero((T > 700.0) & (T < 2300.0))
     assert front.size >= 3, "no reaction zone"
@@ -82,7 +83,7 @@ def test_flame1d_front_chemistry_matches_oracle():
     ctx.chem_set_options(1, rtol=1e-8, atol=1e-14)
     ctx.chem_solve(dt)
     rr = ctx.get_field("RR", (t.S, m.n_cells))[:, idx]
-    ref = Kinetics(mech, ym["nasa"], ym["W"]).reaction_rates(T[idx], None, rho[idx], Y[:, idx], dt)
+    ref = Kinetics(mech, ym["nasa"], ym["W"]).reaction_rates(T[idx], p[idx], rho[idx], Y[:, idx], dt)
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     assert (np.abs(rr - ref) / scale).max() < 1e-4
 

@@ -7,6 +7,7 @@ refuses two ranks on one device; it is exercised by `bench.py --gpus N` under to
 
 Tolerance: one outer iteration with tight solver tolerances; processor faces turn internal faces into
 coupled boundary slots (different summation order), so fields agree to ~1e-10 relative, not bitwise.
+The decomposed run is also checked against the oracle (exact solves on the undecomposed mesh).
 """
 import os
 import threading
@@ -47,6 +48,13 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True)
     ctx = _setup(mg, t, ym, dt)
     case.init_state(ctx, mg, t.S, f["T"], f["p"], f["U"], f["Y"])
     ctx.call("pre_time_step")
+    orc = None
+    if n_steps == 1:   # the oracle (sequential restatement + exact solves) on the same initial state
+        import oracle as O
+        st = case.pull_state(ctx, mg, t.S)
+        orc = O.Oracle(mg, t, {k: v.copy() for k, v in st.items()}, case.default_patch_types(mg),
+                       ym["species"].index("N2"), 1.0 / dt)
+        orc.time_step(2)
     for _ in range(n_steps):
         ctx.time_step(2)
     ref = {n: ctx.get_field(n, (mg.n_cells,)) for n in ("T", "p", "rho", "he")}
@@ -104,6 +112,8 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True)
     # all ranks agree on solver iteration counts (rank-ordered global reductions)
     for r in range(1, nr):
         assert out[r]["stats"]["p"][0] == out[0]["stats"]["p"][0]
+    if orc is not None:
+        ref["oracle"] = {n: orc[n] for n in ("T", "p", "rho", "he", "U", "Y")}
     return ref, glob
 
 
@@ -113,6 +123,8 @@ def test_decomposed_step_matches_single_domain(decomp):
     for n in ("T", "p", "rho", "he", "U", "Y"):
         e = rel_err(glob[n], ref[n])
         assert e < 1e-9, (n, e)
+        e = rel_err(glob[n], ref["oracle"][n])      # decomposed GPU run vs the oracle itself
+        assert e < 1e-9, ("oracle", n, e)
 
 
 def test_decomposed_walls_two_steps():

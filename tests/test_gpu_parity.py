@@ -16,7 +16,19 @@ pytestmark = pytest.mark.gpu
 
 
 MECHS = {"es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt"),
-         "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt")}
+         "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
+         # BASELINE config 4's 53-species table (gri30's 36 species cycled to 53, N2 last)
+         "gri53": ("gri30.yaml", "thermo_gri53_synthetic.txt")}
+
+
+def _mech(mech):
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    if mech == "gri53":
+        from dfmi.synthetic import gri53_species
+        sp = gri53_species(os.path.join(GOLDEN, "gri30.yaml"))
+        return {"species": sp}, read_thermo_table(os.path.join(GOLDEN, MECHS[mech][1]), sp)
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, MECHS[mech][0]))
+    return ym, read_thermo_table(os.path.join(GOLDEN, MECHS[mech][1]), ym["species"])
 
 
 def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
@@ -36,11 +48,9 @@ def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
 
 def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
-    from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi.lib import Context
     from dfmi import case
-    ym = read_yaml_mechanism(os.path.join(GOLDEN, MECHS[mech][0]))
-    t = read_thermo_table(os.path.join(GOLDEN, MECHS[mech][1]), ym["species"])
+    ym, t = _mech(mech)
     L = 1e-3
     if distorted:
         m = _distorted_mesh(nx, ny, nz, (2 * np.pi * L,) * 3)
@@ -54,6 +64,9 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
     dt = 1e-6
     case.setup_context(ctx, m, t, inert, dt, pt)
     f = case.tgv_fields(m, ym["species"], kernel_radius=1.2e-3)
+    if mech == "gri53":   # every one of the 53 species present (Dirichlet-like draws)
+        from dfmi.synthetic import gri53_mass_fractions
+        f["Y"] = gri53_mass_fractions(m.n_cells, seed=1)
     case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"])
     ctx.call("pre_time_step")
     rng = np.random.default_rng(7)
@@ -75,9 +88,19 @@ def _oracle(m, t, st, pt, inert, dt):
     return O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt)
 
 
-@pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted"])
+# es80 / burke9: register-resident species templates; "-generic": the same cases through the
+# species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
+# (BASELINE config 4) -- every variant bitwise against the same oracle
+@pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
+                                        "gri53", "gri53-walls"])
 def periodic(request):
-    if request.param in ("walls", "distorted"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
+    generic = request.param.endswith("-generic")
+    if generic:
+        os.environ["DFMI_SPECIES_GENERIC"] = "1"
+        request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
+    param = request.param.replace("-generic", "")
+    mech = "gri53" if param.startswith("gri53") else "burke9"
+    if param in ("walls", "distorted", "gri53-walls"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
         from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY
 
         def walls(m):
@@ -93,8 +116,8 @@ def periodic(request):
             fv["he"] = t
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
-        return _case(periodic=False, walls=walls, mech="burke9", distorted=request.param == "distorted")
-    return _case(mech=request.param)
+        return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted")
+    return _case(mech=param if param != "gri53" else "gri53")
 
 
 def _cmp_matrix(ctx, eqn, o, parts, B, nsys=1):
@@ -171,6 +194,30 @@ def test_y_eqn_assembly_bitwise(periodic):
     assert not bad, bad
 
 
+def _ell_width(m):
+    """coupling entries per solver row: internal faces + coupled boundary slots of the busiest cell"""
+    n = np.bincount(m.owner, minlength=m.n_cells) + np.bincount(m.neighbour, minlength=m.n_cells)
+    for p in m.patches:
+        if p.kind in ("cyclic", "processor", "processorCyclic"):
+            n = n + np.bincount(p.face_cells, minlength=m.n_cells)
+    return int(n.max())
+
+
+def test_y_ell_rows_bitwise(periodic):
+    """The production YEqn kernel (assembly written straight into the BiCGStab rows) equals the LDU
+    assembly folded by the generic gather (the ldu_to_csr + addBoundaryDiag/Source role), bit for bit."""
+    ctx, m, t, st, pt, inert, dt = periodic
+    W = _ell_width(m)
+    n = t.S - 1
+    ctx.assemble("Y_ell")
+    got = {p: ctx.get_solver_rows("Y", p, n * (W if p == "val" else 1) * m.n_cells) for p in ("val", "dS", "rhs")}
+    ctx.assemble("Y_ell_ref")
+    for p in ("val", "dS", "rhs"):
+        ref = ctx.get_solver_rows("Y", p, got[p].size)
+        assert ulp_diff(got[p], ref) == 0, p
+        assert np.abs(ref).max() > 0, p
+
+
 def test_e_eqn_assembly_bitwise(periodic):
     ctx, m, t, st, pt, inert, dt = periodic
     # species on gradientEnergy walls off their cell values, so the energy gradient is non-trivial
@@ -216,6 +263,7 @@ def test_thermo_correct(periodic):
         assert rel_err(ctx.get_field("boundary_" + n, (m.n_boundary_slots,)), o["boundary_" + n]) < 1e-12, n
     for n in ("rhoD", "hai"):
         assert rel_err(ctx.get_field(n, (t.S, m.n_cells)), o[n]) < 1e-12, n
+        assert rel_err(ctx.get_field("boundary_" + n, (t.S, m.n_boundary_slots)), o["boundary_" + n]) < 1e-12, n
     case.push_state(ctx, st)
 
 
@@ -237,7 +285,7 @@ def test_full_outer_iteration(periodic):
     U = ctx.get_field("U", (3, m.n_cells))
     assert rel_err(U, o["U"]) < 1e-9
     Y = ctx.get_field("Y", (t.S, m.n_cells))
-    assert rel_err(Y, o["Y"]) < 1e-9
+    assert rel_err(Y, o["Y"]) < 1e-9            # per species (trace species included)
     phi = ctx.get_field("phi", (m.n_faces,))
     assert rel_err(phi, o["phi"]) < 1e-9
     for e in ("U", "Y", "E"):
