@@ -105,6 +105,8 @@ def parse():
     ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
                     help="chemistry source: stiff ODE integration per cell (BASELINE config 3), the DF-ODENet "
                          "surrogate (MFMA fp16, config 4's path on the H2 nets) or off")
+    ap.add_argument("--renumber", default="morton", choices=["morton", "rcm", "none"],
+                    help="cell order (dfmi_renumber_cells): Morton bricks (default), reverse Cuthill-McKee, or blockMesh order")
     ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -399,6 +401,9 @@ def main():
     L = 6.283185307179586e-3
     m = hex_box(n * decomp[0], n * decomp[1], n * decomp[2], lengths=(L * decomp[0], L * decomp[1], L * decomp[2]),
                 decomp=decomp, rank=rank)
+    if args.renumber != "none":   # renumberMesh's role: cells in Morton bricks, faces re-sorted
+        from dfmi.renumber import renumber_mesh
+        m, _ = renumber_mesh(m, args.renumber)
     ctx = Context(local)
     comm = None
     if world > 1:
@@ -523,7 +528,7 @@ def main():
         "config": {"workload": f"dfLowMachFoam 3D periodic box {n * decomp[0]}x{n * decomp[1]}x{n * decomp[2]} = "
                                f"{cells_total} hex cells ({m.n_cells} per GPU), H2/air {table.S} species "
                                f"({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
-                   "cells_per_gpu": m.n_cells, "species": table.S,
+                   "cells_per_gpu": m.n_cells, "species": table.S, "cell_order": args.renumber,
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
         "roofline": dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "

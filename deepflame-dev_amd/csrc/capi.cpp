@@ -738,4 +738,18 @@ int dfmi_set_comm_local(dfmi_ctx* ctx, int hub_id, int nranks, int rank, const i
 
 int dfmi_get_unique_id(void* out) { return guard([&] { rccl_unique_id(out); }); }
 
+int dfmi_renumber_cells(int num_cells, const double* cell_centres, int num_faces, const int* owner,
+                        const int* neighbour, const char* method, int* new_to_old) {
+  return guard([&] { renumber_cells(num_cells, cell_centres, num_faces, owner, neighbour, method, new_to_old); });
+}
+
+int dfmi_renumber_faces(int num_cells, int num_faces, const int* owner, const int* neighbour,
+                        const int* cell_new_to_old, int* face_new_to_old, int* new_owner, int* new_neighbour,
+                        int* flipped) {
+  return guard([&] {
+    renumber_faces(num_cells, num_faces, owner, neighbour, cell_new_to_old, face_new_to_old, new_owner, new_neighbour,
+                   flipped);
+  });
+}
+
 }  // extern "C"

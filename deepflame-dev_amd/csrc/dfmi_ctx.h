@@ -215,6 +215,12 @@ struct KScope {
   ~KScope() noexcept(false) { if (idx >= 0) DFMI_HIP(hipEventRecord(x.ktimer.next(), x.stream)); }
 };
 
+// ---- renumber.cpp (host): cell order for cache-local gathers, faces re-sorted upper-triangular
+void renumber_cells(int num_cells, const double* cell_centres, int num_faces, const int* owner, const int* neighbour,
+                    const char* method, int* new_to_old);
+void renumber_faces(int num_cells, int num_faces, const int* owner, const int* neighbour, const int* cell_new_to_old,
+                    int* face_new_to_old, int* new_owner, int* new_neighbour, int* flipped);
+
 // ---- launchers (fv_kernels.hip)
 void k_bc_correct(Ctx& x, const char* type_field, double* vf, double* bvf, int ncomp);
 void rho_process(Ctx& x, bool write_matrix);

@@ -69,6 +69,8 @@ SIGNATURES = {
     "dfmi_chem_solve": [_P, C.c_double],
     "dfmi_chem_set_max_steps": [_P, C.c_int],
     "dfmi_zero_d_step": [_P, C.c_double, C.c_int],
+    "dfmi_renumber_cells": [C.c_int, _DP, C.c_int, _IP, _IP, C.c_char_p, _IP],
+    "dfmi_renumber_faces": [C.c_int, C.c_int, _IP, _IP, _IP, _IP, _IP, _IP, _IP],
     "dfmi_chem_info": [_P, _IP],
     "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
                            C.c_double],
@@ -94,6 +96,37 @@ def exported_symbols() -> list:
 
 class DfmiError(RuntimeError):
     pass
+
+
+def _check(rc, name):
+    if rc != 0:
+        buf = C.create_string_buffer(4096)
+        load().dfmi_last_error(buf, 4096)
+        raise DfmiError(f"{name}: {buf.value.decode()}")
+
+
+def renumber_cells(n_cells, cell_centres, owner, neighbour, method="morton"):
+    """new -> old cell map (include/dfmi.h dfmi_renumber_cells)"""
+    lib = load()
+    cc = np.ascontiguousarray(cell_centres, dtype=np.float64).reshape(-1)
+    o = np.ascontiguousarray(owner, dtype=np.int32); nb = np.ascontiguousarray(neighbour, dtype=np.int32)
+    out = np.empty(n_cells, np.int32)
+    _check(lib.dfmi_renumber_cells(int(n_cells), cc.ctypes.data_as(_DP), int(o.size), o.ctypes.data_as(_IP),
+                                   nb.ctypes.data_as(_IP), method.encode(), out.ctypes.data_as(_IP)), "dfmi_renumber_cells")
+    return out
+
+
+def renumber_faces(n_cells, owner, neighbour, cell_new_to_old):
+    """(face new -> old, new owner, new neighbour, flipped) (include/dfmi.h dfmi_renumber_faces)"""
+    lib = load()
+    o = np.ascontiguousarray(owner, dtype=np.int32); nb = np.ascontiguousarray(neighbour, dtype=np.int32)
+    p = np.ascontiguousarray(cell_new_to_old, dtype=np.int32)
+    F = o.size
+    fo, no, nn, fl = (np.empty(F, np.int32) for _ in range(4))
+    _check(lib.dfmi_renumber_faces(int(n_cells), int(F), o.ctypes.data_as(_IP), nb.ctypes.data_as(_IP),
+                                   p.ctypes.data_as(_IP), fo.ctypes.data_as(_IP), no.ctypes.data_as(_IP),
+                                   nn.ctypes.data_as(_IP), fl.ctypes.data_as(_IP)), "dfmi_renumber_faces")
+    return fo, no, nn, fl.astype(bool)
 
 
 def _dp(a):

@@ -70,6 +70,21 @@ int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* boundary_sf,
                                        const int* boundary_face_cell, const int* patch_type_calculated,
                                        const int* patch_type_extrapolated);
 
+/* ---- cell renumbering (the role of OpenFOAM's renumberMesh; run once on the host before
+ * dfmi_set_constant_indexes, then permute the mesh and field data with the returned maps) -------- */
+/* new_to_old[num_cells]: method "morton" (Z-order of the cell centres [C][3]: aligned runs of 2^k cells
+ * are compact bricks -- the order the gathers are tuned for), "rcm" (reverse Cuthill-McKee of the face
+ * graph, no geometry) or "none" */
+int dfmi_renumber_cells(int num_cells, const double* cell_centres, int num_faces, const int* owner,
+                        const int* neighbour, const char* method, int* new_to_old);
+/* faces of the renumbered mesh in upper-triangular order: face_new_to_old[F], new owner/neighbour
+ * (owner < neighbour), flipped[F] = 1 where owner and neighbour swapped (negate Sf and face fluxes,
+ * w -> 1 - w, reverse the centre-to-centre vector); boundary faces keep their order (faceCells map
+ * through the cell permutation) */
+int dfmi_renumber_faces(int num_cells, int num_faces, const int* owner, const int* neighbour,
+                        const int* cell_new_to_old, int* face_new_to_old, int* new_owner, int* new_neighbour,
+                        int* flipped);
+
 /* ---- per-equation patch types ------------------------------------------------------------ */
 /* dfUEqn/dfYEqn/dfEEqn/dfpEqn/dfRhoEqn/dfThermo::setConstantFields (e.g. dfUEqn.cu:364-379,
  * dfEEqn.cu setConstantFields, dfThermo.cu setConstantFields). field in

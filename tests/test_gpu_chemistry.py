@@ -160,5 +160,6 @@ def test_chem_step_limit_is_an_error():
         ctx.chem_solve(1e-6)
     assert (ctx.get_field("chem_stats", (3, C))[0] < 0).any()
     ctx.chem_set_max_steps(100000)
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
     ctx.set_field("chem_stats", np.zeros((3, C)))
     ctx.chem_solve(1e-6)                      # a sufficient budget clears the error

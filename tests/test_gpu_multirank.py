@@ -34,7 +34,7 @@ def _setup(m, t, ym, dt, comm=None):
     return ctx
 
 
-def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True):
+def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True, renumber=None):
     from dfmi.mesh import hex_box, global_cell_ids
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
@@ -65,6 +65,9 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True)
     nr = int(np.prod(decomp))
     meshes = [hex_box(nx, ny, nz, lengths=L, gradings=gradings, periodic=(periodic,) * 3, decomp=decomp, rank=r)
               for r in range(nr)]
+    if renumber:      # every rank block renumbered (procCols follow the peers' new local ids)
+        from dfmi.renumber import renumber_mesh
+        meshes = [renumber_mesh(mm, renumber)[0] for mm in meshes]
     gids = [global_cell_ids(mm, nx, ny) for mm in meshes]
     out = [None] * nr
     err = [None] * nr
@@ -124,6 +127,13 @@ def test_decomposed_step_matches_single_domain(decomp):
         e = rel_err(glob[n], ref[n])
         assert e < 1e-9, (n, e)
         e = rel_err(glob[n], ref["oracle"][n])      # decomposed GPU run vs the oracle itself
+        assert e < 1e-9, ("oracle", n, e)
+
+
+def test_decomposed_renumbered_step_matches_single_domain():
+    ref, glob = _run(8, 8, 4, (2, 2, 1), renumber="morton")
+    for n in ("T", "p", "rho", "he", "U", "Y"):
+        e = rel_err(glob[n], ref["oracle"][n])
         assert e < 1e-9, ("oracle", n, e)
 
 

@@ -46,7 +46,8 @@ def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
         return read_polymesh(d)
 
 
-def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False):
+def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False,
+          renumber=None):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.lib import Context
     from dfmi import case
@@ -56,6 +57,9 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
         m = _distorted_mesh(nx, ny, nz, (2 * np.pi * L,) * 3)
     else:
         m = hex_box(nx, ny, nz, lengths=(2 * np.pi * L,) * 3, periodic=(periodic,) * 3, gradings=gradings)
+    if renumber:      # the production cell order (dfmi_renumber_cells): oracle and GPU both on it
+        from dfmi.renumber import renumber_mesh
+        m, _ = renumber_mesh(m, renumber)
     ctx = Context(0)
     pt = case.default_patch_types(m)
     if walls:
@@ -92,13 +96,17 @@ def _oracle(m, t, st, pt, inert, dt):
 # species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
-                                        "gri53", "gri53-walls"])
+                                        "gri53", "gri53-walls", "burke9-morton", "distorted-rcm"])
 def periodic(request):
     generic = request.param.endswith("-generic")
     if generic:
         os.environ["DFMI_SPECIES_GENERIC"] = "1"
         request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
     param = request.param.replace("-generic", "")
+    renumber = None
+    for meth in ("morton", "rcm"):
+        if param.endswith("-" + meth):
+            renumber, param = meth, param[: -len(meth) - 1]
     mech = "gri53" if param.startswith("gri53") else "burke9"
     if param in ("walls", "distorted", "gri53-walls"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
         from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY
@@ -116,8 +124,8 @@ def periodic(request):
             fv["he"] = t
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
-        return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted")
-    return _case(mech=param if param != "gri53" else "gri53")
+        return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber)
+    return _case(mech=param, renumber=renumber, nx=8 if renumber else 6, ny=8 if renumber else 5)
 
 
 def _cmp_matrix(ctx, eqn, o, parts, B, nsys=1):
