@@ -327,11 +327,13 @@ def zero_d_line(n_steps=1000):
 def config4_line(m, T, U, p, steps=3, warmup=1):
     """BASELINE config 4 as a full dfLowMachFoam step: the 2M-cell box with 53 species (SURVEY 8d synthetic
     table: gri30's 36 species fitted by dfmi.transport_fit, cycled to 53, N2 last; Dirichlet-like mass
-    fractions) and the DF-ODENet surrogate (52 seeded nets [55,1600,800,400,1]) as the chemistry source."""
+    fractions blended by the hot kernel's progress) and the DF-ODENet surrogate (52 seeded nets
+    [55,1600,800,400,1]) as the chemistry source."""
+    import numpy as np
     from dfmi.mech import read_thermo_table
     from dfmi.lib import Context
     from dfmi import case
-    from dfmi.synthetic import gri53_species, gri53_mass_fractions, gri53_dnn
+    from dfmi.synthetic import gri53_species, gri53_smooth_fractions, gri53_dnn
     golden = os.path.join(ROOT, "tests", "golden")
     sp = gri53_species(os.path.join(golden, "gri30.yaml"))
     t = read_thermo_table(os.path.join(golden, "thermo_gri53_synthetic.txt"), sp)
@@ -339,7 +341,7 @@ def config4_line(m, T, U, p, steps=3, warmup=1):
     case.setup_context(ctx, m, t, sp.index("N2"), 1e-6)
     gri53_dnn(ctx)
     ctx.chem_set_options(2)
-    case.init_state(ctx, m, t.S, T, p, U, gri53_mass_fractions(m.n_cells))
+    case.init_state(ctx, m, t.S, T, p, U, gri53_smooth_fractions((T - T.min()) / max(np.ptp(T), 1.0)))
     for _ in range(warmup):
         ctx.time_step(2)
     ctx.sync()

@@ -51,6 +51,20 @@ def gri53_mass_fractions(n: int, seed: int = 0, alpha: float = 0.3) -> np.ndarra
     return Y / Y.sum(axis=0)
 
 
+def gri53_smooth_fractions(prog: np.ndarray, seed: int = 0) -> np.ndarray:
+    """[53, n] mass fractions varying smoothly in space: two Dirichlet-like compositions (30 % of the mass
+    spread over the 52 non-inert species by gamma(0.3) draws, 70 % N2) blended by prog in [0, 1] -- the
+    hot kernel's progress variable -- so that enthalpy and density stay smooth fields (a per-cell random
+    composition makes the flow solution itself noise)"""
+    rng = np.random.default_rng(seed)
+    comp = []
+    for _ in range(2):
+        b = rng.gamma(0.3, 1.0, S53 - 1)
+        comp.append(np.concatenate([0.3 * b / b.sum(), [0.7]]))
+    prog = np.clip(np.asarray(prog, dtype=np.float64), 0.0, 1.0)
+    return (1 - prog)[None, :] * comp[0][:, None] + prog[None, :] * comp[1][:, None]
+
+
 def gri53_dnn(ctx, seed: int = 0):
     """52 DF-ODENet nets [55, 1600, 800, 400, 1] (inference.py:12-25 widths) with seeded N(0, 1/fan_in)
     weights; input normalisation in the H2 nets' pattern (T ~ 1300 +- 400 K, p ~ 1 atm, Box-Cox(Y) ~ -5

@@ -243,6 +243,26 @@ class Oracle:
                            (np.concatenate(rows + [np.arange(C_), np.array(cr, dtype=np.int64)]),
                             np.concatenate(cols + [np.arange(C_), np.array(cc, dtype=np.int64)]))),
                           shape=(C_, C_)).tocsc()
+        if C_ <= 5000:
+            return spla.spsolve(A, b)
+        # large meshes: a direct factorisation of a 3-D operator fills in badly; a Jacobi-preconditioned
+        # Krylov solve to 1e-15 of the right-hand side is exact to the comparison tolerances (1e-9)
+        Dinv = sp.diags(1.0 / A.diagonal())
+        nb = max(np.abs(b).max(), 1e-300)
+        sym = abs(A - A.T).max() <= 1e-14 * abs(A).max()
+        solvers = ([lambda: spla.cg(A, b, rtol=1e-15, atol=0.0, maxiter=5000, M=Dinv)] if sym else []) + \
+                  [lambda: spla.bicgstab(A, b, rtol=1e-15, atol=0.0, maxiter=3000, M=Dinv),
+                   lambda: spla.gmres(A, b, rtol=1e-15, atol=0.0, restart=60, maxiter=40, M=Dinv)]
+        best = None
+        for solver in solvers:
+            x, info = solver()
+            res = np.abs(A @ x - b).max() / nb if np.isfinite(x).all() else np.inf
+            if best is None or res < best[1]:
+                best = (x, res)
+            if res < 1e-12:
+                return x
+        if best[1] < 1e-11:
+            return best[0]
         return spla.spsolve(A, b)
 
     # ---- one full outer iteration (dfLowMachFoam.C:284-531, nOuter = 1)

@@ -7,7 +7,7 @@ from dfmi.mesh import hex_box
 from dfmi.mech import read_thermo_table
 from dfmi.lib import Context
 from dfmi import case
-from dfmi.synthetic import gri53_species, gri53_mass_fractions, gri53_dnn
+from dfmi.synthetic import gri53_species, gri53_smooth_fractions, gri53_dnn
 
 golden = os.path.join(ROOT, "tests", "golden")
 sp = gri53_species(os.path.join(golden, "gri30.yaml"))
@@ -22,7 +22,7 @@ if mode == "dnn":
     ctx.chem_set_options(2)
 f = case.tgv_fields(m, ["H2", "O2", "N2", "H2O"], kernel_radius=1.5e-3)
 C = m.n_cells
-case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], gri53_mass_fractions(C, seed=0))
+case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], gri53_smooth_fractions((f["T"] - 300.0) / np.ptp(f["T"])))
 
 
 def stats(tag):

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -v -s --timeout 240 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/gpu_tests.log; ok $rc || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc

@@ -17,7 +17,7 @@ def test_gri53_dnn_time_steps():
     from dfmi.mech import read_thermo_table
     from dfmi.lib import Context
     from dfmi import case
-    from dfmi.synthetic import gri53_species, gri53_mass_fractions, gri53_dnn
+    from dfmi.synthetic import gri53_species, gri53_smooth_fractions, gri53_dnn
     sp = gri53_species(os.path.join(GOLDEN, "gri30.yaml"))
     t = read_thermo_table(os.path.join(GOLDEN, "thermo_gri53_synthetic.txt"), sp)
     m = hex_box(12, 10, 8)
@@ -27,7 +27,8 @@ def test_gri53_dnn_time_steps():
     ctx.chem_set_options(2)
     f = case.tgv_fields(m, ["H2", "O2", "N2", "H2O"], kernel_radius=1.5e-3)
     C = m.n_cells
-    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], gri53_mass_fractions(C, seed=2))
+    prog = (f["T"] - f["T"].min()) / np.ptp(f["T"])
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], gri53_smooth_fractions(prog, seed=2))
     ctx.call("pre_time_step")
     for _ in range(3):
         ctx.time_step(2)
@@ -36,6 +37,10 @@ def test_gri53_dnn_time_steps():
     RR = ctx.get_field("RR", (t.S, C))
     rho_old = ctx.get_field("rho_old", (C,))
     assert np.isfinite(T).all() and np.isfinite(Y).all() and np.isfinite(RR).all()
+    assert T.min() > 290.0 and T.max() < 1900.0                # a smooth state stays bounded
+    for e in ("U", "Y", "E"):
+        assert ctx.solver_stats(e)[0] < 20, e                  # every solve converged
+    assert ctx.solver_stats("p")[0] < 1000
     assert np.abs(Y.sum(axis=0) - 1).max() < 1e-10
     hot = ctx.get_field("T", (C,)) >= 610.0
     assert np.abs(RR[:, hot]).max() > 0                   # reacting cells carry the surrogate's source
