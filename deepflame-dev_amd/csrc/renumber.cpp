@@ -63,6 +63,31 @@ void morton_order(int C, const double* cc, std::vector<int>& order) {
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
 }
 
+// Morton order of 8 x 8 x 4 bricks, lexicographic (x fastest) inside a brick: one 64-lane wave is an
+// 8 x 8 layer of a brick, so its own-cell reads, its -x/-y neighbours (c-1, c-8) and its -z neighbours
+// (the layer below, contiguous even across a brick boundary) coalesce, while the bricks themselves
+// follow a Z-order curve, so a brick's neighbour bricks are a few bricks away at every level (and each
+// XCD's contiguous eighth of the cells is a compact octant). Needs integer (i, j, k) cell coordinates
+// (structured blocks); monotone in each coordinate, so no face flips.
+void brick_order(int C, const double* ijk, std::vector<int>& order) {
+  constexpr int BX = 8, BY = 8, BZ = 4;
+  std::vector<uint64_t> key(C);
+  for (int c = 0; c < C; ++c) {
+    long v[3];
+    for (int k = 0; k < 3; ++k) {
+      const double d = ijk[3L * c + k];
+      v[k] = std::lround(d);
+      if (std::fabs(d - (double)v[k]) > 1e-9 || v[k] < 0) throw std::runtime_error("dfmi: renumber: bricks needs integer (i, j, k) cell coordinates >= 0");
+    }
+    const uint64_t b = spread3((uint64_t)(v[0] / BX)) | spread3((uint64_t)(v[1] / BY)) << 1 | spread3((uint64_t)(v[2] / BZ)) << 2;
+    const uint64_t in = (uint64_t)(v[0] % BX) + BX * ((uint64_t)(v[1] % BY) + BY * (uint64_t)(v[2] % BZ));
+    key[c] = b << 8 | in;
+  }
+  order.resize(C);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key[a] < key[b]; });
+}
+
 // reverse Cuthill-McKee on the face graph (renumberMesh's default CuthillMcKee, reversed): needs no
 // geometry; bandwidth-reducing rather than brick-forming
 void rcm_order(int C, int F, const int* own, const int* nei, std::vector<int>& order) {
@@ -105,6 +130,9 @@ void renumber_cells(int num_cells, const double* cell_centres, int num_faces, co
   if (m == "morton") {
     if (!cell_centres) throw std::runtime_error("dfmi: renumber: morton needs the cell centres");
     morton_order(num_cells, cell_centres, order);
+  } else if (m == "bricks") {
+    if (!cell_centres) throw std::runtime_error("dfmi: renumber: bricks needs (i, j, k) cell coordinates");
+    brick_order(num_cells, cell_centres, order);
   } else if (m == "rcm") {
     if (num_faces < 0 || (num_faces > 0 && (!owner || !neighbour))) throw std::runtime_error("dfmi: renumber: rcm needs owner/neighbour");
     rcm_order(num_cells, num_faces, owner, neighbour, order);
@@ -112,7 +140,7 @@ void renumber_cells(int num_cells, const double* cell_centres, int num_faces, co
     order.resize(num_cells);
     std::iota(order.begin(), order.end(), 0);
   } else {
-    throw std::runtime_error("dfmi: renumber: method must be 'morton', 'rcm' or 'none'");
+    throw std::runtime_error("dfmi: renumber: method must be 'bricks', 'morton', 'rcm' or 'none'");
   }
   std::memcpy(new_to_old, order.data(), sizeof(int) * num_cells);
 }

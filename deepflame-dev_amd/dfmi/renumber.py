@@ -39,10 +39,12 @@ class Renumbering:
         return v
 
 
-def renumber_mesh(m: Mesh, method: str = "morton", peer_perm=None):
+def renumber_mesh(m: Mesh, method: str = "bricks", peer_perm=None):
     """(renumbered mesh, Renumbering). Geometry is permuted, never recomputed."""
     # structured boxes order by their integer (i, j, k) -- the same permutation on every rank block of
     # a decomposition, whatever the grading; other meshes by their cell centres
+    if method == "bricks" and not hasattr(m, "local_index"):
+        method = "morton"             # unstructured: no (i, j, k) -- Z-order of the centres
     key = np.stack(m.local_index, axis=1).astype(np.float64) if hasattr(m, "local_index") else m.cell_centres
     perm = renumber_cells(m.n_cells, key, m.owner, m.neighbour, method)
     fo, no, nn, fl = renumber_faces(m.n_cells, m.owner, m.neighbour, perm)

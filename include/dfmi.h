@@ -72,9 +72,10 @@ int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* boundary_sf,
 
 /* ---- cell renumbering (the role of OpenFOAM's renumberMesh; run once on the host before
  * dfmi_set_constant_indexes, then permute the mesh and field data with the returned maps) -------- */
-/* new_to_old[num_cells]: method "morton" (Z-order of the cell centres [C][3]: aligned runs of 2^k cells
- * are compact bricks -- the order the gathers are tuned for), "rcm" (reverse Cuthill-McKee of the face
- * graph, no geometry) or "none" */
+/* new_to_old[num_cells]: method "bricks" (structured blocks: cell_centres holds the integer (i, j, k) of
+ * each cell; 8x8x4 bricks along a Z-order curve, lexicographic inside a brick -- the order the gathers
+ * are tuned for), "morton" (Z-order of the cell centres [C][3], any mesh), "rcm" (reverse Cuthill-McKee
+ * of the face graph, no geometry) or "none" */
 int dfmi_renumber_cells(int num_cells, const double* cell_centres, int num_faces, const int* owner,
                         const int* neighbour, const char* method, int* new_to_old);
 /* faces of the renumbered mesh in upper-triangular order: face_new_to_old[F], new owner/neighbour

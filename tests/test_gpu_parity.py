@@ -96,7 +96,7 @@ def _oracle(m, t, st, pt, inert, dt):
 # species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
-                                        "gri53", "gri53-walls", "burke9-morton", "distorted-rcm"])
+                                        "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm"])
 def periodic(request):
     generic = request.param.endswith("-generic")
     if generic:
@@ -104,7 +104,7 @@ def periodic(request):
         request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
     param = request.param.replace("-generic", "")
     renumber = None
-    for meth in ("morton", "rcm"):
+    for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
             renumber, param = meth, param[: -len(meth) - 1]
     mech = "gri53" if param.startswith("gri53") else "burke9"
@@ -125,7 +125,8 @@ def periodic(request):
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
         return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber)
-    return _case(mech=param, renumber=renumber, nx=8 if renumber else 6, ny=8 if renumber else 5)
+    return _case(mech=param, renumber=renumber, nx=16 if renumber else 6, ny=8 if renumber else 5,
+                 nz=4 if renumber else 4)
 
 
 def _cmp_matrix(ctx, eqn, o, parts, B, nsys=1):

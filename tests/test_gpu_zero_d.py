@@ -45,7 +45,7 @@ def test_zero_d_trajectory_matches_oracle():
     for k in range(1, n + 1):
         ctx.zero_d_step(ref["dt"], 1)
         Tc = ctx.get_field("T", (C,))
-        assert np.ptp(Tc) == 0.0                  # identical reactors stay identical
+        assert np.ptp(Tc) <= 1e-12 * Tc[0]        # identical reactors stay identical
         T[k] = Tc[0]
         Y[k] = ctx.get_field("Y", (t.S, C))[:, 0]
     assert Tref[-1] > 2000.0                      # the oracle trajectory ignites inside the 1 ms

@@ -18,11 +18,12 @@ def _check_mesh(m):
     np.testing.assert_allclose(m.mesh_distance, d, rtol=0, atol=1e-15)
 
 
-def test_morton_bricks_and_faces():
+@pytest.mark.parametrize("method", ["morton", "bricks"])
+def test_morton_bricks_and_faces(method):
     from dfmi.mesh import hex_box
     from dfmi.renumber import renumber_mesh
     m = hex_box(16, 16, 16)
-    r2, r = renumber_mesh(m, "morton")
+    r2, r = renumber_mesh(m, method)
     assert sorted(r.cells.tolist()) == list(range(m.n_cells))
     assert not r.flip.any()                                       # monotone order of a structured box: no flips
     _check_mesh(r2)
@@ -30,6 +31,8 @@ def test_morton_bricks_and_faces():
     for b in range(0, m.n_cells, 256):                            # 256 consecutive cells = one 8 x 8 x 4 brick
         ext = [np.ptp(a[b:b + 256]) + 1 for a in (ii, jj, kk)]
         assert ext == [8, 8, 4], ext
+    if method == "bricks":                                        # lexicographic inside the brick
+        assert np.array_equal(ii[:8], np.arange(8)) and np.all(jj[:8] == 0) and jj[8] == 1
     np.testing.assert_array_equal(r2.volume, m.volume[r.cells])
     for p, q in zip(m.patches, r2.patches):
         np.testing.assert_array_equal(r.cells[q.face_cells], p.face_cells)
