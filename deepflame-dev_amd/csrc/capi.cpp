@@ -154,6 +154,7 @@ void copy_field(Ctx& x, const std::string& name, const double* host, long count,
 
 void require_ready(Ctx& x) {
   DFMI_CHECK(x.have_sizes && x.have_topo && x.have_geom && x.have_bgeom, "mesh not fully initialised");
+  if (!x.ell.ready) build_ell(x);   // gather rows (face lists of the assembly kernels, solver columns)
 }
 
 void maybe_setup_halo(Ctx& x);

@@ -24,6 +24,8 @@ struct MeshView {
   const int *own, *nei, *ownStart, *nbrStart, *nbrFace, *cbStart, *cbSlot, *bfc, *partner;
   const int8_t* sprim;   // 1 = primary slot (owner side), 0 = processor [internal n] slot
   const double *Sf, *magSf, *w, *dc, *V, *bSf, *bmagSf, *bw, *bdc;
+  const int *ecol, *esrc;   // solver gather rows [W][C] (linsolve.hip build_ell): the face loops read them
+  int W;
   double rdt;
 };
 
@@ -177,6 +179,7 @@ struct Ctx {
     m.own = own; m.nei = nei; m.ownStart = ownStart; m.nbrStart = nbrStart; m.nbrFace = nbrFace;
     m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
+    m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
     m.rdt = rdt;
     return m;
   }
@@ -203,6 +206,7 @@ struct KScope {
   int idx;
   static int match(const std::vector<std::string>& ts, const char* name) {   // template arguments ignored
     if (ts.empty()) return -1;
+    while (*name == '(') ++name;
     size_t n = 0;
     while (name[n] && name[n] != '<') ++n;
     for (size_t i = 0; i < ts.size(); ++i)
@@ -251,6 +255,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
                           long sstride, const double* ic, const double* bc, long bstride, const char* type_field,
                           double* xsol, long xstride, const SolverCfg& cfg, bool prebuilt = false);
 void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs);
+void build_ell(Ctx& x);   // solver gather rows; also the face lists of the assembly kernels
 void bicg_rows_from_ldu_Y(Ctx& x);
 void bicg_rows_get(Ctx& x, int nsys, const std::string& part, double* host, long count);
 bool species_generic(int S);   // fv_kernels.hip: chunked kernels for S > 16 (or DFMI_SPECIES_GENERIC=1)

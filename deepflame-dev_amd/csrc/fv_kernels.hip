@@ -41,12 +41,27 @@ __device__ __forceinline__ double bface(const MeshView& m, int t, const double* 
   return bc_coupled(t) ? interp_b(m.bw[b], vf[c], nbrv(m, vf, bvf, b)) : bvf[b];
 }
 
-// visit faces of cell c in sequential order: fn(face, other_cell, is_owner)
-template <class FN> __device__ __forceinline__ void each_face(const MeshView& m, int c, FN&& fn) {
-  const int e1 = m.nbrStart[c + 1];
-  for (int k = m.nbrStart[c]; k < e1; ++k) { const int f = m.nbrFace[k]; fn(f, m.own[f], false); }
-  const int e2 = m.ownStart[c + 1];
-  for (int f = m.ownStart[c]; f < e2; ++f) fn(f, m.nei[f], true);
+// visit faces of cell c in sequential order: fn(face, other_cell, is_owner).
+// WT > 0 (meshes whose busiest cell has WT couplings, hex meshes: 6): read the cell's row of the solver
+// gather (ELL [W][C], built once: neighbour faces ascending, owned faces ascending, then coupled slots)
+// -- coalesced index loads, one indirection, all WT entries loaded up front and the loop unrolled, so
+// every face's gathers are in flight together instead of one face's latency after another's.
+// WT = 0: the CSR walk (nbrStart/nbrFace, ownStart), same order, any mesh.
+template <int WT, class FN> __device__ __forceinline__ void each_face(const MeshView& m, int c, FN&& fn) {
+  if constexpr (WT > 0) {
+    const long C = m.C;
+    int es[WT], cs[WT];
+#pragma unroll
+    for (int k = 0; k < WT; ++k) { es[k] = m.esrc[k * C + c]; cs[k] = m.ecol[k * C + c]; }
+#pragma unroll
+    for (int k = 0; k < WT; ++k)
+      if (es[k] >= 0) fn(es[k] >> 1, cs[k], (es[k] & 1) != 0);   // slots (< 0) and padding skipped
+  } else {
+    const int e1 = m.nbrStart[c + 1];
+    for (int k = m.nbrStart[c]; k < e1; ++k) { const int f = m.nbrFace[k]; fn(f, m.own[f], false); }
+    const int e2 = m.ownStart[c + 1];
+    for (int f = m.ownStart[c]; f < e2; ++f) fn(f, m.nei[f], true);
+  }
 }
 // visit primary, non-empty boundary slots of c in slot order: fn(slot, type)
 template <class FN> __device__ __forceinline__ void each_slot(const MeshView& m, const int8_t* ty, int c, FN&& fn) {
@@ -91,13 +106,14 @@ __global__ void k_copy_multi(CopyList L) {
 }
 
 // ------------------------------------------------------------------ rhoEqn (dfRhoEqn.cu:41-92)
+template <int WT>
 __global__ void k_rho(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ rho_old,
                       const double* __restrict__ phi, const double* __restrict__ bphi, double* __restrict__ rho,
                       double* __restrict__ odiag, double* __restrict__ osrc) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   double div = 0.0;
-  each_face(m, c, [&](int f, int, bool own) { if (own) div += phi[f]; else div -= phi[f]; });
+  each_face<WT>(m, c, [&](int f, int, bool own) { if (own) div += phi[f]; else div -= phi[f]; });
   each_slot(m, ty, c, [&](int b, int) { div += bphi[b]; });
   const double diag = m.rdt * m.V[c];
   double src = m.rdt * rho_old[c] * m.V[c];
@@ -116,6 +132,7 @@ __device__ __forceinline__ void dev2T(double sc, const double* v, double* o) {
   o[6] = sc * v[2]; o[7] = sc * v[5]; o[8] = sc * (v[8] - tr);
 }
 
+template <int WT>
 __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
                          const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
                          double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
@@ -125,7 +142,7 @@ __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __rest
   double s[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) s[k] = 0.0;
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const int o = own ? c : o2, n = own ? o2 : c;
     const double w = m.w[f];
     double uf[3], sf[3];
@@ -178,6 +195,7 @@ __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __rest
 
 // UEqn matrix (UEqn.H:3-20): ddt(rho,U) + div(phi,U) - laplacian(mu,U) - div(mu dev2 T(gradU)),
 // plus source_solve = source - grad(p) and rAU (dfUEqn.cu:721-738).
+template <int WT>
 __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
     const double* __restrict__ rho, const double* __restrict__ rho_old, const double* __restrict__ U_old,
     const double* __restrict__ bU, const double* __restrict__ phi, const double* __restrict__ bphi,
@@ -190,7 +208,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
   double dT[3] = {0.0, 0.0, 0.0}, gp[3] = {0.0, 0.0, 0.0};
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const int o = own ? c : o2, n = own ? o2 : c;
     const double w = m.w[f], ph = phi[f];
     const double L1 = -w * ph;
@@ -265,6 +283,7 @@ __global__ void k_kinetic(int C, const double* __restrict__ U, double* __restric
 }
 
 // HbyA: fvMatrix::H() / V (dfUEqn.cu:753-822), unscaled; rAU scaling and constrainHbyA follow.
+template <int WT>
 __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __restrict__ tyU, const double* __restrict__ U,
     const double* __restrict__ bU, const double* __restrict__ lower, const double* __restrict__ upper,
     const double* __restrict__ src, const double* __restrict__ ic, const double* __restrict__ bc,
@@ -280,7 +299,7 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
     bd = -bd;
     each_slot(m, tyU, c, [&](int b, int) { bd += (ic[b] + ic[B + b] + ic[2 * B + b]) / 3; });
     double Hl = 0.0;
-    each_face(m, c, [&](int f, int oc, bool own) {
+    each_face<WT>(m, c, [&](int f, int oc, bool own) {
       if (own) Hl -= upper[f] * Uk[oc]; else Hl -= lower[f] * Uk[oc];
     });
     double h = bd * Uk[c] + (Hl + src[k * C + c]);
@@ -380,6 +399,7 @@ __global__ void k_p_slot(MeshView m, const int8_t* __restrict__ tyP, const int8_
   bc[b] = -(-pG * q.gbc);
 }
 
+template <int WT>
 __global__ void k_p_cell(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ lower,
                          const double* __restrict__ ph, const double* __restrict__ bph, const double* __restrict__ p,
                          const double* __restrict__ p_old, const double* __restrict__ psi, const double* __restrict__ rho,
@@ -387,7 +407,7 @@ __global__ void k_p_cell(MeshView m, const int8_t* __restrict__ tyP, const doubl
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   double dL = 0.0, div = 0.0;
-  each_face(m, c, [&](int f, int, bool own) {
+  each_face<WT>(m, c, [&](int f, int, bool own) {
     dL -= -lower[f];
     if (own) div += ph[f]; else div -= ph[f];
   });
@@ -425,6 +445,7 @@ __global__ void k_p_flux_slot(MeshView m, const int8_t* __restrict__ tyP, const 
   bphi[b] = bph[b] + fl;
 }
 // U = HbyA - rAU*grad(p); K; dpdt
+template <int WT>
 __global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ p,
                               const double* __restrict__ bp, const double* __restrict__ p_old,
                               const double* __restrict__ H, const double* __restrict__ rAU, double* __restrict__ U,
@@ -433,7 +454,7 @@ __global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const 
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double g[3] = {0.0, 0.0, 0.0};
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const int o = own ? c : o2, n = own ? o2 : c;
     const double pf = interp_f(m.w[f], p[o], p[n]);
 #pragma unroll
@@ -461,7 +482,7 @@ __global__ void k_kinetic_slots(int B, const double* __restrict__ bU, double* __
 // ------------------------------------------------------------------ YEqn preparation (YEqn.H:24-118)
 // per cell: grad(Y_s), sumYDiffError, hDiffCorrFlux, diffAlphaD; per non-coupled slot of the cell:
 // corrected boundary gradients -> boundary sumYDiffError / hDiffCorrFlux.
-template <int S>
+template <int S, int WT>
 __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
     const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
     const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
@@ -482,7 +503,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
     yc[s] = Y[s * C + c];
     ahc[s] = ac * hai[s * C + c];
   }
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     const double ms = m.magSf[f], dcf = m.dc[f];
     const double an = alpha[o2];
@@ -611,7 +632,7 @@ __global__ void k_phiuc_slot(MeshView m, const int8_t* __restrict__ tyY, const d
 
 // Y species matrices, all non-inert species in one pass (dfYEqn.cu:571-638 fused and batched):
 // fvm::ddt(rho,Yi) + div(phi,Yi) + div(phiUc,Yi) == laplacian(rhoD_i,Yi) + RR_i
-template <int S>
+template <int S, int WT>
 __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
@@ -626,7 +647,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
   double dL[S], rc[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double ph = phi[f], pu = phiUc[f];
     const double wu = ph >= 0 ? 1.0 : 0.0;
     const double L1 = -wu * ph, U1 = L1 + ph;
@@ -672,7 +693,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
 // faces, coupled slots), dS = diag + sum internalCoeffs and rhs = source + non-coupled
 // boundaryCoeffs in slot order -- bitwise what k_ell_build makes from the LDU arrays, without writing
 // and re-reading lower/upper/internalCoeffs/boundaryCoeffs.
-template <int S>
+template <int S, int WT>
 __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
@@ -687,7 +708,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
 #pragma unroll
   for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
   int k = 0;
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double ph = phi[f], pu = phiUc[f];
     const double wu = ph >= 0 ? 1.0 : 0.0;
     const double L1 = -wu * ph, U1 = L1 + ph;
@@ -774,7 +795,7 @@ __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
 constexpr int YCH = 8;
 
 // gradient (and, with LAP, the diffAlphaD laplacian) of species s0 .. s0+CH-1 at cell c, divided by V
-template <int CH, bool LAP>
+template <int CH, bool LAP, int WT>
 __device__ __forceinline__ void y_chunk_grad(const MeshView& m, const int8_t* __restrict__ tyY, int S, int s0, int c,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ hai,
     const double* __restrict__ bhai, const double* __restrict__ alpha, const double* __restrict__ balpha, double ac,
@@ -788,7 +809,7 @@ __device__ __forceinline__ void y_chunk_grad(const MeshView& m, const int8_t* __
     yc[j] = s < S ? Y[s * C + c] : 0.0;
     ahc[j] = (LAP && s < S) ? ac * hai[s * C + c] : 0.0;
   }
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     const double ms = m.magSf[f], dcf = m.dc[f];
     const double an = LAP ? alpha[o2] : 0.0;
@@ -857,7 +878,7 @@ __device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, i
   }
 }
 
-template <int CH>
+template <int CH, int WT>
 __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int8_t* __restrict__ tyY,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ hai, const double* __restrict__ bhai,
@@ -872,7 +893,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
   // pass 1: gradients + laplacians -> sumYDiffError, diffAlphaD; boundary sumYDiffError summed in place
   for (int s0 = 0; s0 < S; s0 += CH) {
     double g[CH][3], lap[CH], yc[CH];
-    y_chunk_grad<CH, true>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
+    y_chunk_grad<CH, true, WT>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
     if (gout) {
 #pragma unroll
       for (int j = 0; j < CH; ++j)
@@ -909,7 +930,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
   double hd[3] = {0.0, 0.0, 0.0};
   for (int s0 = 0; s0 < S; s0 += CH) {
     double g[CH][3], lap[CH], yc[CH];
-    y_chunk_grad<CH, false>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
+    y_chunk_grad<CH, false, WT>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -939,7 +960,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
 }
 
 // YEqn matrices, chunked over species (LDU form: the dfmi_assemble("Y") inspection path)
-template <int CH>
+template <int CH, int WT>
 __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
@@ -956,7 +977,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
     double dL[CH], rc[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) { dL[j] = 0.0; rc[j] = s0 + j < S ? rhoD[(s0 + j) * C + c] : 0.0; }
-    each_face(m, c, [&](int f, int o2, bool own) {
+    each_face<WT>(m, c, [&](int f, int o2, bool own) {
       const double ph = phi[f], pu = phiUc[f];
       const double wu = ph >= 0 ? 1.0 : 0.0;
       const double L1 = -wu * ph, U1 = L1 + ph;
@@ -1004,7 +1025,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
 }
 
 // YEqn in the solver's ELL rows, chunked over species (production path for S > 16)
-template <int CH>
+template <int CH, int WT>
 __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
@@ -1021,7 +1042,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
 #pragma unroll
     for (int j = 0; j < CH; ++j) { dL[j] = 0.0; rc[j] = s0 + j < S ? rhoD[(s0 + j) * C + c] : 0.0; }
     int k = 0;
-    each_face(m, c, [&](int f, int o2, bool own) {
+    each_face<WT>(m, c, [&](int f, int o2, bool own) {
       const double ph = phi[f], pu = phiUc[f];
       const double wu = ph >= 0 ? 1.0 : 0.0;
       const double L1 = -wu * ph, U1 = L1 + ph;
@@ -1101,6 +1122,7 @@ __global__ void k_y_inert_gen(int C, int S, int inert, double* __restrict__ Y) {
 }
 
 // ------------------------------------------------------------------ EEqn (EEqn.H:12-45; dfEEqn.cu:108-264)
+template <int WT>
 __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __restrict__ tyH, const int8_t* __restrict__ tyK,
     const double* __restrict__ he, const double* __restrict__ bhe, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ K, const double* __restrict__ K_old,
@@ -1113,7 +1135,7 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0, divK = 0.0, divh = 0.0;
-  each_face(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const int o = own ? c : o2, n = own ? o2 : c;
     const double ph = phi[f], w = m.w[f];
     const double wu = ph >= 0 ? 1.0 : 0.0;
@@ -1195,6 +1217,17 @@ template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim
   do { KScope _ks(x, #kernel); if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
        DFMI_HIP(hipGetLastError()); } while (0)
 
+// kernels templated on the ELL width: the unrolled path for hex meshes (W = 6), the CSR walk otherwise
+// (DFMI_FACE_CSR=1 forces the CSR walk everywhere: A/B measurement and parity of both paths)
+bool face_rows(const Ctx& x) {
+  const char* e = std::getenv("DFMI_FACE_CSR");
+  return x.ell.W == 6 && !(e && std::atoi(e) != 0);
+}
+#define LAUNCH_W(kern, n, ...) \
+  do { if (face_rows(x)) LAUNCH(kern<6>, n, __VA_ARGS__); else LAUNCH(kern<0>, n, __VA_ARGS__); } while (0)
+#define LAUNCH_SW(kern, NS, n, ...) \
+  do { if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
+
 void k_bc_correct(Ctx& x, const char* tf, double* vf, double* bvf, int ncomp) {
   const double* eg = std::string(tf) == "he" ? x.f("boundary_heGradient") : nullptr;
   LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp, eg);
@@ -1220,7 +1253,7 @@ void copy_old(Ctx& x) {   // dfMatrixDataBase::preTimeStep (dfMatrixDataBase.cu:
 void rho_process(Ctx& x, bool write_matrix) {
   double* od = write_matrix ? x.f("dbg_rho_diag") : nullptr;
   double* os = write_matrix ? x.f("dbg_rho_source") : nullptr;
-  LAUNCH(k_rho, x.C, x.view(), x.st("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("rho"), od, os);
+  LAUNCH_W(k_rho, x.C, x.view(), x.st("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("rho"), od, os);
   k_bc_correct(x, "rho", x.f("rho"), x.f("boundary_rho"), 1);
   halo_fields(x, {"rho"});
 }
@@ -1228,10 +1261,10 @@ void rho_process(Ctx& x, bool write_matrix) {
 void u_assemble(Ctx& x) {
   Matrix& A = x.mU;
   double* gout = x.fields.count("dbg_gradU") ? x.f("dbg_gradU") : nullptr;
-  LAUNCH(k_u_grad, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), x.f("mu"), x.f("boundary_mu"),
+  LAUNCH_W(k_u_grad, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), x.f("mu"), x.f("boundary_mu"),
          x.f("tauU"), x.f("boundary_tauU"), gout);
   halo_fields(x, {"tauU"});   // fvc_grad_vector_correctBC_processor (dfMatrixOpBase.cu:1366-1389)
-  LAUNCH(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
+  LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
          x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
          x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
          A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"));
@@ -1248,7 +1281,7 @@ void u_post_solve(Ctx& x) {
 
 void u_hbya(Ctx& x) {
   Matrix& A = x.mU;
-  LAUNCH(k_u_hbya, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), A.lower.p, A.upper.p, A.source.p,
+  LAUNCH_W(k_u_hbya, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), A.lower.p, A.upper.p, A.source.p,
          A.ic.p, A.bc.p, x.f("HbyA"));
   k_bc_correct(x, "extrapolated", x.f("HbyA"), x.f("boundary_HbyA"), 3);
   LAUNCH(k_hbya_scale_cells, x.C, x.C, x.f("rAU"), x.f("HbyA"));
@@ -1265,7 +1298,7 @@ void p_assemble(Ctx& x) {
          x.f("rho_old"), x.f("boundary_rho_old"), x.f("U_old"), x.f("boundary_U_old"), x.f("boundary_phi_old"),
          x.f("HbyA"), x.f("boundary_HbyA"), x.f("boundary_p"), x.f("boundary_rhorAUf"), x.f("boundary_phiHbyA"),
          A.ic.p, A.bc.p);
-  LAUNCH(k_p_cell, x.C, m, x.st("p"), A.lower.p, x.f("phiHbyA"), x.f("boundary_phiHbyA"), x.f("p"), x.f("p_old"),
+  LAUNCH_W(k_p_cell, x.C, m, x.st("p"), A.lower.p, x.f("phiHbyA"), x.f("boundary_phiHbyA"), x.f("p"), x.f("p_old"),
          x.f("psi"), x.f("rho"), x.f("rho_old"), A.diag.p, A.source.p);
 }
 
@@ -1277,7 +1310,7 @@ void p_post_solve(Ctx& x) {
   LAUNCH(k_p_flux_face, x.F, m, x.f("phiHbyA"), A.lower.p, A.upper.p, x.f("p"), x.f("phi"));
   LAUNCH(k_p_flux_slot, x.B, m, x.st("p"), x.f("boundary_phiHbyA"), A.ic.p, A.bc.p, x.f("p"), x.f("boundary_p"),
          x.f("boundary_phi"));
-  LAUNCH(k_p_cell_post, x.C, m, x.st("p"), x.f("p"), x.f("boundary_p"), x.f("p_old"), x.f("HbyA"), x.f("rAU"),
+  LAUNCH_W(k_p_cell_post, x.C, m, x.st("p"), x.f("p"), x.f("boundary_p"), x.f("p_old"), x.f("HbyA"), x.f("rAU"),
          x.f("U"), x.f("K"), x.f("dpdt"));
   k_bc_correct(x, "U", x.f("U"), x.f("boundary_U"), 3);
   halo_fields(x, {"U"});
@@ -1303,12 +1336,12 @@ bool species_generic(int S) {
 void y_prep(Ctx& x) {
   MeshView m = x.view();
   double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
-#define CALL(NS) LAUNCH(k_y_prep<NS>, x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
+#define CALL(NS) LAUNCH_SW(k_y_prep, NS, x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
                         x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),    \
                         x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"),         \
                         x.f("diffAlphaD"), gout)
   DFMI_SWITCH_S(x.S, CALL,
-                LAUNCH(k_y_prep_gen<YCH>, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
+                LAUNCH_SW(k_y_prep_gen, YCH, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
                        x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"),
                        x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),
                        x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout))
@@ -1321,11 +1354,11 @@ void y_prep(Ctx& x) {
 void y_assemble(Ctx& x) {
   Matrix& A = x.mY;
   MeshView m = x.view();
-#define CALL(NS) LAUNCH(k_y_assemble<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
+#define CALL(NS) LAUNCH_SW(k_y_assemble, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
                         x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p)
   DFMI_SWITCH_S(x.S, CALL,
-                LAUNCH(k_y_assemble_gen<YCH>, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
+                LAUNCH_SW(k_y_assemble_gen, YCH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"),
                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p))
 #undef CALL
@@ -1333,11 +1366,11 @@ void y_assemble(Ctx& x) {
 
 void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs) {
   MeshView m = x.view();
-#define CALL(NS) LAUNCH(k_y_assemble_ell<NS>, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
+#define CALL(NS) LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
                         x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs)
   DFMI_SWITCH_S(x.S, CALL,
-                LAUNCH(k_y_assemble_ell_gen<YCH>, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"),
+                LAUNCH_SW(k_y_assemble_ell_gen, YCH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"),
                        x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),
                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs))
 #undef CALL
@@ -1357,7 +1390,7 @@ void e_assemble(Ctx& x) {
   thermo_energy_gradient(x);   // eeqn_calculate_energy_gradient (dfEEqn.cu:148, :266-287)
   k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
   const double* eg = x.f("boundary_heGradient");
-  LAUNCH(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
+  LAUNCH_W(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
          x.f("K"), x.f("K_old"), x.f("boundary_K"), x.f("phi"), x.f("boundary_phi"), x.f("alpha"),
          x.f("boundary_alpha"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("dpdt"), x.f("diffAlphaD"),
          eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p);

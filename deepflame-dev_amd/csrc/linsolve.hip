@@ -405,53 +405,6 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
 }
 
 // ------------------------------------------------------------------ host side
-void build_ell(Ctx& x) {
-  const int C = x.C;
-  std::vector<int> own = x.h_own, nei = x.h_nei;
-  std::vector<std::vector<std::pair<int, int>>> ent(C);   // (col, src)
-  std::vector<std::vector<int>> nbrf(C);
-  for (int f = 0; f < x.F; ++f) nbrf[nei[f]].push_back(f);
-  for (int c = 0; c < C; ++c) for (int f : nbrf[c]) ent[c].push_back({own[f], 2 * f});
-  for (int f = 0; f < x.F; ++f) ent[own[f]].push_back({nei[f], 2 * f + 1});
-  // owned faces were appended in ascending face order after the neighbour faces: matches each_face
-  std::vector<int> partner(x.B, -1);
-  for (int p = 0; p < x.P; ++p) {
-    if (x.pkind[p] != 1) continue;
-    const int q = x.cyc_nbr[p];
-    for (int i = 0; i < x.psize[p]; ++i) partner[x.poff[p] + i] = x.h_bfc[x.poff[q] + i];
-  }
-  for (int p = 0; p < x.P; ++p) {   // coupled primary slots in slot order (= cbSlot order per cell)
-    if (x.pkind[p] == 0) continue;
-    for (int i = 0; i < x.psize[p]; ++i) {
-      const int b = x.poff[p] + i;
-      const int c = x.h_bfc[b];
-      int colv;
-      if (x.pkind[p] == 1) colv = partner[b];
-      else {
-        DFMI_CHECK(halo_active(x) && b < (int)x.h_hidx.size() && x.h_hidx[b] >= 0,
-                   "processor patches need dfmi_set_comm_info before the first solve");
-        colv = C + x.h_hidx[b];
-      }
-      ent[c].push_back({colv, -(b + 1)});
-    }
-  }
-  int W = 0;
-  for (auto& e : ent) W = std::max(W, (int)e.size());
-  W = std::max(W, 1);
-  std::vector<int> col((size_t)W * C), src((size_t)W * C);
-  for (int c = 0; c < C; ++c)
-    for (int k = 0; k < W; ++k) {
-      const bool have = k < (int)ent[c].size();
-      col[(size_t)k * C + c] = have ? ent[c][k].first : c;
-      src[(size_t)k * C + c] = have ? ent[c][k].second : PAD;
-    }
-  x.ell.W = W;
-  x.ell.col.upload(col, x.stream);
-  x.ell.src.upload(src, x.stream);
-  DFMI_HIP(hipStreamSynchronize(x.stream));
-  x.ell.ready = true;
-}
-
 struct Launch {
   Ctx& x;
   int nblk, nsys;
@@ -549,6 +502,54 @@ void record_stats(Ctx& x, const char* eqn, const double* scal, int nsys) {
 }
 
 }  // namespace
+
+void build_ell(Ctx& x) {
+  const int C = x.C;
+  std::vector<int> own = x.h_own, nei = x.h_nei;
+  std::vector<std::vector<std::pair<int, int>>> ent(C);   // (col, src)
+  std::vector<std::vector<int>> nbrf(C);
+  for (int f = 0; f < x.F; ++f) nbrf[nei[f]].push_back(f);
+  for (int c = 0; c < C; ++c) for (int f : nbrf[c]) ent[c].push_back({own[f], 2 * f});
+  for (int f = 0; f < x.F; ++f) ent[own[f]].push_back({nei[f], 2 * f + 1});
+  // owned faces were appended in ascending face order after the neighbour faces: matches each_face
+  std::vector<int> partner(x.B, -1);
+  for (int p = 0; p < x.P; ++p) {
+    if (x.pkind[p] != 1) continue;
+    const int q = x.cyc_nbr[p];
+    for (int i = 0; i < x.psize[p]; ++i) partner[x.poff[p] + i] = x.h_bfc[x.poff[q] + i];
+  }
+  for (int p = 0; p < x.P; ++p) {   // coupled primary slots in slot order (= cbSlot order per cell)
+    if (x.pkind[p] == 0) continue;
+    for (int i = 0; i < x.psize[p]; ++i) {
+      const int b = x.poff[p] + i;
+      const int c = x.h_bfc[b];
+      int colv;
+      if (x.pkind[p] == 1) colv = partner[b];
+      else {
+        DFMI_CHECK(halo_active(x) && b < (int)x.h_hidx.size() && x.h_hidx[b] >= 0,
+                   "processor patches need dfmi_set_comm_info before the first solve");
+        colv = C + x.h_hidx[b];
+      }
+      ent[c].push_back({colv, -(b + 1)});
+    }
+  }
+  int W = 0;
+  for (auto& e : ent) W = std::max(W, (int)e.size());
+  W = std::max(W, 1);
+  std::vector<int> col((size_t)W * C), src((size_t)W * C);
+  for (int c = 0; c < C; ++c)
+    for (int k = 0; k < W; ++k) {
+      const bool have = k < (int)ent[c].size();
+      col[(size_t)k * C + c] = have ? ent[c][k].first : c;
+      src[(size_t)k * C + c] = have ? ent[c][k].second : PAD;
+    }
+  x.ell.W = W;
+  x.ell.col.upload(col, x.stream);
+  x.ell.src.upload(src, x.stream);
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  x.ell.ready = true;
+}
+
 
 // BiCGStab workspace: BCG_VECS vectors of nsys * (C + H), then the ELL values [nsys][W][C], then partials.
 // Assembly kernels that emit the ELL form directly (y_assemble_ell) write into it before the solve.

@@ -96,13 +96,16 @@ def _oracle(m, t, st, pt, inert, dt):
 # species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
-                                        "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm"])
+                                        "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr"])
 def periodic(request):
     generic = request.param.endswith("-generic")
     if generic:
         os.environ["DFMI_SPECIES_GENERIC"] = "1"
         request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
-    param = request.param.replace("-generic", "")
+    if request.param.endswith("-csr"):     # face loops by the CSR walk instead of the gather rows
+        os.environ["DFMI_FACE_CSR"] = "1"
+        request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
+    param = request.param.replace("-generic", "").replace("-csr", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
