@@ -343,10 +343,10 @@ void amg_setup(Ctx& x) {
   std::vector<int> col((size_t)x.ell.W * C);
   DFMI_HIP(hipMemcpy(col.data(), x.ell.col.p, col.size() * sizeof(int), hipMemcpyDeviceToHost));
   // geometric strength |Sf| * deltaCoeffs per coupling (faces and cyclic slots)
-  std::vector<double> mag(x.F), dcf(x.F), bmag(x.B), bdc(x.B);
-  if (x.F) {
-    DFMI_HIP(hipMemcpy(mag.data(), x.magSf.p, x.F * sizeof(double), hipMemcpyDeviceToHost));
-    DFMI_HIP(hipMemcpy(dcf.data(), x.dc.p, x.F * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<double> mag(x.Fs), dcf(x.Fs), bmag(x.B), bdc(x.B);   // face storage order
+  if (x.Fs) {
+    DFMI_HIP(hipMemcpy(mag.data(), x.magSf.p, x.Fs * sizeof(double), hipMemcpyDeviceToHost));
+    DFMI_HIP(hipMemcpy(dcf.data(), x.dc.p, x.Fs * sizeof(double), hipMemcpyDeviceToHost));
   }
   if (x.B) {
     DFMI_HIP(hipMemcpy(bmag.data(), x.bmagSf.p, x.B * sizeof(double), hipMemcpyDeviceToHost));
@@ -357,7 +357,7 @@ void amg_setup(Ctx& x) {
   {
     std::vector<std::vector<std::pair<int, double>>> e(C);
     for (int f = 0; f < x.F; ++f) {
-      const double s = mag[f] * dcf[f];
+      const double s = mag[x.h_fst[f]] * dcf[x.h_fst[f]];
       e[x.h_own[f]].push_back({x.h_nei[f], s});
       e[x.h_nei[f]].push_back({x.h_own[f], s});
     }

@@ -25,15 +25,15 @@ template <class FN> int guard(FN&& fn) {
 
 using namespace dfmi;
 
-void alloc_field(Ctx& x, const std::string& name, long n, int ncomp, bool boundary) {
+void alloc_field(Ctx& x, const std::string& name, long n, int ncomp, bool boundary, bool face = false) {
   Field& f = x.fields[name];
-  f.n = n; f.ncomp = ncomp; f.boundary = boundary;
+  f.n = n; f.ncomp = ncomp; f.boundary = boundary; f.face = face;
   f.buf.alloc((size_t)n * ncomp);
   f.buf.zero(x.stream);
 }
 
 void allocate_fields(Ctx& x) {
-  const long C = x.C, F = x.F, B = x.B;
+  const long C = x.C, B = x.B;
   const int S = x.S;
   for (auto n : {"rho", "rho_old", "p", "p_old", "he", "T", "K", "K_old", "psi", "mu", "alpha", "dpdt", "rAU",
                  "diffAlphaD", "psip0"}) {
@@ -53,12 +53,13 @@ void allocate_fields(Ctx& x) {
     alloc_field(x, std::string("boundary_") + n, B, S, true);
   }
   for (auto n : {"phi", "phi_old", "phiUc", "rhorAUf", "phiHbyA"}) {
-    alloc_field(x, n, F, 1, false);
+    alloc_field(x, n, x.Fs, 1, false, true);
     alloc_field(x, std::string("boundary_") + n, B, 1, true);
   }
+  const long Fs = x.Fs;
   auto mk = [&](Matrix& A, int ns, int nsrc, int nb) {
     A.nsys = ns;
-    A.lower.alloc((size_t)ns * F); A.upper.alloc((size_t)ns * F); A.diag.alloc((size_t)ns * C);
+    A.lower.alloc((size_t)ns * Fs); A.upper.alloc((size_t)ns * Fs); A.diag.alloc((size_t)ns * C);
     A.source.alloc((size_t)nsrc * C); A.ic.alloc((size_t)nb * B); A.bc.alloc((size_t)nb * B);
     A.lower.zero(x.stream); A.upper.zero(x.stream); A.diag.zero(x.stream); A.source.zero(x.stream);
     A.ic.zero(x.stream); A.bc.zero(x.stream);
@@ -126,6 +127,21 @@ void copy_field(Ctx& x, const std::string& name, const double* host, long count,
   auto it = x.fields.find(name);
   DFMI_CHECK(it != x.fields.end(), "unknown field '" + name + "'");
   Field& f = it->second;
+  if (f.face) {   // OpenFOAM face order on the host, owner-slot storage on the device
+    DFMI_CHECK(count == x.F, "field '" + name + "': expected " + std::to_string(x.F) + " values, got " + std::to_string(count));
+    std::vector<double> st(f.n, 0.0);
+    if (to_dev) {
+      for (long i = 0; i < x.F; ++i) st[x.h_fst[i]] = host[i];
+      DFMI_HIP(hipMemcpyAsync(f.buf.p, st.data(), f.n * sizeof(double), hipMemcpyHostToDevice, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+    } else {
+      DFMI_HIP(hipMemcpyAsync(st.data(), f.buf.p, f.n * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      double* out = const_cast<double*>(host);
+      for (long i = 0; i < x.F; ++i) out[i] = st[x.h_fst[i]];
+    }
+    return;
+  }
   DFMI_CHECK(count == f.n, "field '" + name + "': expected " + std::to_string(f.n) + " values per component, got " +
                                std::to_string(count));
   const size_t tot = (size_t)f.n * f.ncomp;
@@ -181,7 +197,7 @@ void do_Y(Ctx& x) {
   double *val, *dS, *rhs;
   bicg_layout(x, (int)map.size(), &val, &dS, &rhs);
   y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
-  solve_bicgstab(x, "Y", (int)map.size(), map.data(), A.lower, x.F, A.upper, x.F, A.diag, x.C, A.source, x.C, A.ic,
+  solve_bicgstab(x, "Y", (int)map.size(), map.data(), A.lower, x.Fs, A.upper, x.Fs, A.diag, x.C, A.source, x.C, A.ic,
                  A.bc, x.B, "Y", x.f("Y"), x.C, x.solver["Y"], true);
   y_post_solve(x);
 }
@@ -284,10 +300,20 @@ int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighb
       nbrCnt[n + 1]++;
     }
     for (int c = 0; c < C; ++c) { ownStart[c + 1] += ownStart[c]; nbrCnt[c + 1] += nbrCnt[c]; }
+    // face storage: owner-slot order (k-th owned face of c at k*C + c) when at most 3 faces per cell
+    // are owned or the padding stays small; OpenFOAM order otherwise
+    int kmax = 0;
+    for (int c = 0; c < C; ++c) kmax = std::max(kmax, ownStart[c + 1] - ownStart[c]);
+    x.fslot = F > 0 && (kmax <= 3 || (long)kmax * C <= (long)F + F / 4);
+    x.Fs = x.fslot ? kmax * C : F;
+    x.h_fst.resize(F);
+    for (int f = 0; f < F; ++f) x.h_fst[f] = x.fslot ? (f - ownStart[owner[f]]) * C + owner[f] : f;
+    std::vector<int> own_s(std::max(x.Fs, 1), -1), nei_s(std::max(x.Fs, 1), -1);
+    for (int f = 0; f < F; ++f) { own_s[x.h_fst[f]] = owner[f]; nei_s[x.h_fst[f]] = neighbour[f]; }
     std::vector<int> nbrFace(std::max(F, 1)), pos(nbrCnt.begin(), nbrCnt.end() - 1);
-    for (int f = 0; f < F; ++f) nbrFace[pos[neighbour[f]]++] = f;   // ascending face order per cell
-    x.own.upload(x.h_own.empty() ? std::vector<int>{0} : x.h_own, x.stream);
-    x.nei.upload(x.h_nei.empty() ? std::vector<int>{0} : x.h_nei, x.stream);
+    for (int f = 0; f < F; ++f) nbrFace[pos[neighbour[f]]++] = x.h_fst[f];   // ascending face order per cell
+    x.own.upload(own_s, x.stream);
+    x.nei.upload(nei_s, x.stream);
     x.ownStart.upload(ownStart, x.stream);
     x.nbrStart.upload(nbrCnt, x.stream);
     x.nbrFace.upload(nbrFace, x.stream);
@@ -302,13 +328,18 @@ int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const do
   return guard([&] {
     Ctx& x = ctx->x;
     DFMI_CHECK(x.have_topo, "call dfmi_set_constant_indexes first");
-    const long F = x.F;
-    std::vector<double> soa(3 * F);
-    for (long f = 0; f < F; ++f) for (int k = 0; k < 3; ++k) soa[k * F + f] = sf[f * 3 + k];   // AoS -> SoA
+    const long F = x.F, Fs = x.Fs;
+    std::vector<double> soa(3 * std::max(Fs, 1L), 0.0), ms(std::max(Fs, 1L), 0.0), ww(std::max(Fs, 1L), 0.0),
+        dd(std::max(Fs, 1L), 0.0);
+    for (long f = 0; f < F; ++f) {   // AoS -> SoA, OpenFOAM face order -> face storage
+      const long s = x.h_fst[f];
+      for (int k = 0; k < 3; ++k) soa[k * Fs + s] = sf[f * 3 + k];
+      ms[s] = mag_sf[f]; ww[s] = weight[f]; dd[s] = delta_coeffs[f];
+    }
     x.Sf.upload(soa, x.stream);
-    x.magSf.upload(mag_sf, F, x.stream);
-    x.w.upload(weight, F, x.stream);
-    x.dc.upload(delta_coeffs, F, x.stream);
+    x.magSf.upload(ms, x.stream);
+    x.w.upload(ww, x.stream);
+    x.dc.upload(dd, x.stream);
     x.V.upload(volume, x.C, x.stream);
     DFMI_HIP(hipStreamSynchronize(x.stream));
     x.have_geom = true;
@@ -564,6 +595,16 @@ int dfmi_get_matrix(dfmi_ctx* ctx, const char* eqn, const char* part, double* ho
                         p == "source" ? &A->source : p == "source_solve" ? &A->source_solve :
                         p == "internal_coeffs" ? &A->ic : p == "boundary_coeffs" ? &A->bc : nullptr;
     DFMI_CHECK(b && b->p, "unknown matrix part '" + p + "'");
+    if (p == "lower" || p == "upper") {   // face storage -> OpenFOAM face order, per system
+      const long ns = (long)(b->n / std::max(x.Fs, 1));
+      DFMI_CHECK(count == ns * x.F, "matrix part size mismatch: expected " + std::to_string(ns * x.F));
+      std::vector<double> st(b->n);
+      DFMI_HIP(hipMemcpyAsync(st.data(), b->p, b->n * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      for (long s = 0; s < ns; ++s)
+        for (long f = 0; f < x.F; ++f) host[s * x.F + f] = st[s * x.Fs + x.h_fst[f]];
+      return;
+    }
     DFMI_CHECK((size_t)count == b->n, "matrix part size mismatch: expected " + std::to_string(b->n));
     DFMI_HIP(hipMemcpyAsync(host, b->p, count * sizeof(double), hipMemcpyDeviceToHost, x.stream));
     DFMI_HIP(hipStreamSynchronize(x.stream));

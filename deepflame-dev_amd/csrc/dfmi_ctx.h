@@ -9,6 +9,13 @@
 // Topology for deterministic cell gathers (no FP atomics anywhere):
 //   ownStart[C+1]           faces owned by c are [ownStart[c], ownStart[c+1]) (upper-triangular order)
 //   nbrStart[C+1], nbrFace  faces whose neighbour is c, ascending face index (losort)
+// Face STORAGE: every face array lives in "owner-slot" order when the mesh allows it (at most a few
+// faces owned per cell, e.g. hex meshes: 3): the k-th face owned by cell c at k*C + c. A wavefront of
+// consecutive cells then reads and writes its k-th owned faces as one contiguous run (OpenFOAM order
+// interleaves each cell's 3 faces: stride-3 partial lines that the L2 evicts between the three
+// visits), and a cell's neighbour-side faces are the owned faces of consecutive cells too. Padding
+// slots have own = -1. The API keeps OpenFOAM face order: face fields and lower/upper are mapped
+// through h_fst (face -> storage) at the boundary. Meshes with many owned faces per cell keep face order.
 //   cbStart[C+1], cbSlot    primary boundary slots of c, ascending slot index
 // Visiting nbrFace, then own faces, then cbSlot is exactly OpenFOAM's sequential face order.
 #pragma once
@@ -22,6 +29,7 @@ namespace dfmi {
 struct MeshView {
   int C, F, B, S;
   const int *own, *nei, *ownStart, *nbrStart, *nbrFace, *cbStart, *cbSlot, *bfc, *partner;
+  int fslot;                // face storage in owner-slot order (k*C + c) rather than OpenFOAM order
   const int8_t* sprim;   // 1 = primary slot (owner side), 0 = processor [internal n] slot
   const double *Sf, *magSf, *w, *dc, *V, *bSf, *bmagSf, *bw, *bdc;
   const int *ecol, *esrc;   // solver gather rows [W][C] (linsolve.hip build_ell): the face loops read them
@@ -31,9 +39,10 @@ struct MeshView {
 
 struct Field {
   DevBuf<double> buf;
-  long n = 0;       // values per component
+  long n = 0;       // values per component (device storage; faces: Fs)
   int ncomp = 1;
   bool boundary = false;
+  bool face = false;  // internal-face field: API order F, device storage Fs (Ctx::h_fst)
 };
 
 // one assembled fvMatrix (LDU + boundary coefficients), reference storage convention
@@ -121,6 +130,9 @@ struct Ctx {
   hipStream_t stream = nullptr;
   // sizes (dfMatrixDataBase::setConstantValues, dfMatrixDataBase.cu:114-147)
   int C = 0, Ctot = 0, F = 0, B = 0, P = 0, S = 0, nproc_faces = 0;
+  int Fs = 0;                    // face storage size (owner-slot layout: kmax * C; otherwise F)
+  bool fslot = false;
+  std::vector<int> h_fst;        // OpenFOAM face -> storage index
   double rdt = 0;
   int inert = -1;
   bool have_sizes = false, have_topo = false, have_geom = false, have_bgeom = false;
@@ -175,7 +187,7 @@ struct Ctx {
 
   MeshView view() const {
     MeshView m;
-    m.C = C; m.F = F; m.B = B; m.S = S;
+    m.C = C; m.F = Fs; m.B = B; m.S = S; m.fslot = fslot ? 1 : 0;
     m.own = own; m.nei = nei; m.ownStart = ownStart; m.nbrStart = nbrStart; m.nbrFace = nbrFace;
     m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;

@@ -59,8 +59,11 @@ template <int WT, class FN> __device__ __forceinline__ void each_face(const Mesh
   } else {
     const int e1 = m.nbrStart[c + 1];
     for (int k = m.nbrStart[c]; k < e1; ++k) { const int f = m.nbrFace[k]; fn(f, m.own[f], false); }
-    const int e2 = m.ownStart[c + 1];
-    for (int f = m.ownStart[c]; f < e2; ++f) fn(f, m.nei[f], true);
+    const int o0 = m.ownStart[c], no = m.ownStart[c + 1] - o0;
+    for (int k = 0; k < no; ++k) {
+      const int f = m.fslot ? k * m.C + c : o0 + k;   // storage index of the k-th owned face
+      fn(f, m.nei[f], true);
+    }
   }
 }
 // visit primary, non-empty boundary slots of c in slot order: fn(slot, type)
@@ -340,6 +343,7 @@ __global__ void k_p_face(MeshView m, const double* __restrict__ rho, const doubl
   if (f >= m.F) return;
   const long C = m.C, F = m.F;
   const int o = m.own[f], n = m.nei[f];
+  if (o < 0) return;   // padding slot of the owner-slot face storage
   const double w = m.w[f];
   const double r = interp_f(w, rho[o] * rAU[o], rho[n] * rAU[n]);
   rf[f] = r;
@@ -430,7 +434,9 @@ __global__ void k_p_flux_face(MeshView m, const double* __restrict__ ph, const d
                               const double* __restrict__ upper, const double* __restrict__ p, double* __restrict__ phi) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= m.F) return;
-  phi[f] = ph[f] + (upper[f] * p[m.nei[f]] - lower[f] * p[m.own[f]]);
+  const int o = m.own[f];
+  if (o < 0) return;
+  phi[f] = ph[f] + (upper[f] * p[m.nei[f]] - lower[f] * p[o]);
 }
 __global__ void k_p_flux_slot(MeshView m, const int8_t* __restrict__ tyP, const double* __restrict__ bph,
                               const double* __restrict__ ic, const double* __restrict__ bc, const double* __restrict__ p,
@@ -611,6 +617,7 @@ __global__ void k_phiuc_face(MeshView m, const double* __restrict__ sumE, double
   if (f >= m.F) return;
   const long C = m.C, F = m.F;
   const int o = m.own[f], n = m.nei[f];
+  if (o < 0) return;
   const double w = m.w[f];
   phiUc[f] = m.Sf[f] * interp_f(w, sumE[o], sumE[n]) + m.Sf[F + f] * interp_f(w, sumE[C + o], sumE[C + n]) +
              m.Sf[2 * F + f] * interp_f(w, sumE[2 * C + o], sumE[2 * C + n]);
@@ -1292,7 +1299,7 @@ void u_hbya(Ctx& x) {
 void p_assemble(Ctx& x) {
   Matrix& A = x.mP;
   MeshView m = x.view();
-  LAUNCH(k_p_face, x.F, m, x.f("rho"), x.f("rAU"), x.f("rho_old"), x.f("U_old"), x.f("phi_old"), x.f("HbyA"),
+  LAUNCH(k_p_face, x.Fs, m, x.f("rho"), x.f("rAU"), x.f("rho_old"), x.f("U_old"), x.f("phi_old"), x.f("HbyA"),
          x.f("rhorAUf"), x.f("phiHbyA"), A.lower.p, A.upper.p);
   LAUNCH(k_p_slot, x.B, m, x.st("p"), x.st("U"), x.f("rho"), x.f("boundary_rho"), x.f("rAU"), x.f("boundary_rAU"),
          x.f("rho_old"), x.f("boundary_rho_old"), x.f("U_old"), x.f("boundary_U_old"), x.f("boundary_phi_old"),
@@ -1307,7 +1314,7 @@ void p_post_solve(Ctx& x) {
   MeshView m = x.view();
   k_bc_correct(x, "p", x.f("p"), x.f("boundary_p"), 1);
   halo_fields(x, {"p"});
-  LAUNCH(k_p_flux_face, x.F, m, x.f("phiHbyA"), A.lower.p, A.upper.p, x.f("p"), x.f("phi"));
+  LAUNCH(k_p_flux_face, x.Fs, m, x.f("phiHbyA"), A.lower.p, A.upper.p, x.f("p"), x.f("phi"));
   LAUNCH(k_p_flux_slot, x.B, m, x.st("p"), x.f("boundary_phiHbyA"), A.ic.p, A.bc.p, x.f("p"), x.f("boundary_p"),
          x.f("boundary_phi"));
   LAUNCH_W(k_p_cell_post, x.C, m, x.st("p"), x.f("p"), x.f("boundary_p"), x.f("p_old"), x.f("HbyA"), x.f("rAU"),
@@ -1347,7 +1354,7 @@ void y_prep(Ctx& x) {
                        x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout))
 #undef CALL
   halo_fields(x, {"sumYDiffError", "hDiffCorrFlux"});
-  LAUNCH(k_phiuc_face, x.F, m, x.f("sumYDiffError"), x.f("phiUc"));
+  LAUNCH(k_phiuc_face, x.Fs, m, x.f("sumYDiffError"), x.f("phiUc"));
   LAUNCH(k_phiuc_slot, x.B, m, x.st("Y"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("boundary_phiUc"));
 }
 

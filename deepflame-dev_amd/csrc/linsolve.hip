@@ -509,8 +509,9 @@ void build_ell(Ctx& x) {
   std::vector<std::vector<std::pair<int, int>>> ent(C);   // (col, src)
   std::vector<std::vector<int>> nbrf(C);
   for (int f = 0; f < x.F; ++f) nbrf[nei[f]].push_back(f);
-  for (int c = 0; c < C; ++c) for (int f : nbrf[c]) ent[c].push_back({own[f], 2 * f});
-  for (int f = 0; f < x.F; ++f) ent[own[f]].push_back({nei[f], 2 * f + 1});
+  // coefficient sources by face STORAGE index (lower/upper live in the owner-slot layout)
+  for (int c = 0; c < C; ++c) for (int f : nbrf[c]) ent[c].push_back({own[f], 2 * x.h_fst[f]});
+  for (int f = 0; f < x.F; ++f) ent[own[f]].push_back({nei[f], 2 * x.h_fst[f] + 1});
   // owned faces were appended in ascending face order after the neighbour faces: matches each_face
   std::vector<int> partner(x.B, -1);
   for (int p = 0; p < x.P; ++p) {
@@ -578,7 +579,7 @@ void bicg_rows_from_ldu_Y(Ctx& x) {
   const long C = x.C, Ce = (long)x.C + x.H;
   x.ws.sysmap.upload(map.data(), nsys, x.stream);
   Matrix& A = x.mY;
-  Sys q{A.lower, A.upper, A.diag, A.source, A.ic, A.bc, x.F, x.F, C, C, x.B, x.f("Y"), C};
+  Sys q{A.lower, A.upper, A.diag, A.source, A.ic, A.bc, x.Fs, x.Fs, C, C, x.B, x.f("Y"), C};
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   hipLaunchKernelGGL(k_ell_build, dim3(nblk, nsys), dim3(TPB), 0, x.stream, x.view(), x.st("Y"), q,
                      (const int*)x.ws.sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs);
