@@ -105,9 +105,10 @@ def parse():
     ap.add_argument("--chem", default="ode", choices=["ode", "dnn", "off"],
                     help="chemistry source: stiff ODE integration per cell (BASELINE config 3), the DF-ODENet "
                          "surrogate (MFMA fp16, config 4's path on the H2 nets) or off")
-    ap.add_argument("--renumber", default="bricks", choices=["bricks", "morton", "rcm", "none"],
-                    help="cell order (dfmi_renumber_cells): 8x8x4 bricks on a Z-order curve (default), plain "
-                         "Morton, reverse Cuthill-McKee, or blockMesh order")
+    ap.add_argument("--renumber", default="none", choices=["bricks", "morton", "rcm", "none"],
+                    help="cell order (dfmi_renumber_cells): blockMesh order (default: with the owner-slot face "
+                         "storage its gathers are contiguous runs and it measured fastest), 8x8x4 bricks on a Z-order "
+                         "curve, plain Morton, or reverse Cuthill-McKee")
     ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
     ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
