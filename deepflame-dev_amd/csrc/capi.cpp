@@ -48,6 +48,14 @@ void allocate_fields(Ctx& x) {
   alloc_field(x, "chem_stats", C, 3, false);   // per cell: accepted / rejected integrator steps, next step size
   alloc_field(x, "boundary_tauU", B, 9, true);
   alloc_field(x, "boundary_heGradient", B, 1, true);   // gradientEnergy patches (dfEEqn.cu:266-287)
+  // mixed conditions: p's waveTransmissive valueFraction (set at each pEqn assembly) and gamma; the
+  // inletValue of every field that may use inletOutlet
+  alloc_field(x, "boundary_p_vf", B, 1, true);
+  alloc_field(x, "boundary_p_gamma", B, 1, true);
+  alloc_field(x, "boundary_U_ref", B, 3, true);
+  alloc_field(x, "boundary_p_ref", B, 1, true);
+  alloc_field(x, "boundary_Y_ref", B, S, true);
+  alloc_field(x, "boundary_K_ref", B, 1, true);
   for (auto n : {"Y", "rhoD", "hai", "RR"}) {
     alloc_field(x, n, C, S, false);
     alloc_field(x, std::string("boundary_") + n, B, S, true);
@@ -384,7 +392,10 @@ int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type
                "unknown patch-type field '" + f + "'");
     for (int p = 0; p < x.P; ++p) {
       const int t = patch_type[p];
-      DFMI_CHECK(t >= 0 && t <= 10 && t != COUPLED, "patch " + std::to_string(p) + ": unsupported boundary condition code " + std::to_string(t));
+      DFMI_CHECK(t >= 0 && t <= 12 && t != COUPLED, "patch " + std::to_string(p) + ": unsupported boundary condition code " + std::to_string(t));
+      DFMI_CHECK(t != WAVE_TRANSMISSIVE || f == "p", "waveTransmissive is supported for p (the 1D flame's outlet)");
+      DFMI_CHECK(t != INLET_OUTLET || f == "U" || f == "p" || f == "Y" || f == "K",
+                 "inletOutlet is supported for U, p, Y and K (energy needs its own mixed form)");
       DFMI_CHECK((x.pkind[p] == 1) == (t == CYCLIC) && (x.pkind[p] == 2) == bc_proc(t),
                  "patch " + std::to_string(p) + ": field '" + f + "' type disagrees with the mesh patch kind");
       DFMI_CHECK(t != GRADIENT_ENERGY || f == "he", "gradientEnergy is an energy boundary condition (field 'he')");
@@ -392,6 +403,20 @@ int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type
     }
     set_ptype(x, f, patch_type);
     DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_set_patch_param(dfmi_ctx* ctx, const char* field, int patch, const char* name, double value) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_bgeom, "call dfmi_init_constant_fields_boundary first");
+    DFMI_CHECK(patch >= 0 && patch < x.P, "patch index out of range");
+    const std::string f(field), n(name);
+    DFMI_CHECK(f == "p" && n == "gamma", "patch parameters: ('p', 'gamma') of waveTransmissive");
+    std::vector<double> g(x.B);
+    DFMI_HIP(hipMemcpy(g.data(), x.f("boundary_p_gamma"), x.B * sizeof(double), hipMemcpyDeviceToHost));
+    for (int i = 0; i < x.psize[patch]; ++i) g[x.poff[patch] + i] = value;
+    DFMI_HIP(hipMemcpy(x.f("boundary_p_gamma"), g.data(), x.B * sizeof(double), hipMemcpyHostToDevice));
   });
 }
 

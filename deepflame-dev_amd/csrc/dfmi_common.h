@@ -22,14 +22,19 @@ __device__ __forceinline__ int xcd_block() {
 
 
 // Boundary-condition codes, identical to the reference enum (src_gpu/dfMatrixDataBase.H:81-93)
+// plus two mixed conditions the reference GPU path rejects (dfMatrixDataBase.cu:22-27) but its CPU
+// cases use: waveTransmissive (test/Tu500K-Phi1/0/p:34) and inletOutlet
 enum BC : int8_t {
   ZERO_GRADIENT = 0, FIXED_VALUE = 1, COUPLED = 2, EMPTY = 3, GRADIENT_ENERGY = 4, CALCULATED = 5,
-  CYCLIC = 6, PROCESSOR = 7, EXTRAPOLATED = 8, FIXED_ENERGY = 9, PROCESSOR_CYCLIC = 10
+  CYCLIC = 6, PROCESSOR = 7, EXTRAPOLATED = 8, FIXED_ENERGY = 9, PROCESSOR_CYCLIC = 10,
+  WAVE_TRANSMISSIVE = 11, INLET_OUTLET = 12
 };
 
 __host__ __device__ inline bool bc_coupled(int t) { return t == CYCLIC || t == PROCESSOR || t == PROCESSOR_CYCLIC || t == COUPLED; }
 __host__ __device__ inline bool bc_proc(int t) { return t == PROCESSOR || t == PROCESSOR_CYCLIC; }
 __host__ __device__ inline bool bc_fixes_value(int t) { return t == FIXED_VALUE || t == FIXED_ENERGY; }
+// mixedFvPatchField: value = f ref + (1 - f) cell (refGrad = 0)
+__host__ __device__ inline bool bc_mixed(int t) { return t == WAVE_TRANSMISSIVE || t == INLET_OUTLET; }
 
 struct Error : std::runtime_error { using std::runtime_error::runtime_error; };
 

@@ -23,6 +23,22 @@ __device__ __forceinline__ double interp_f(double w, double vo, double vn) { ret
 __device__ __forceinline__ double interp_b(double w, double vo, double vn) { return w * vo + (1.0 - w) * vn; }
 
 struct BCoef { double vic, vbc, gic, gbc; };
+// per-slot data of the mixed conditions of one field: waveTransmissive (advectiveFvPatchField, Euler ddt:
+// refValue = the old-time boundary value, valueFraction = 1 / (1 + w dt deltaCoeffs) set at the pEqn
+// assembly) and inletOutlet (refValue = inletValue, valueFraction = 1 - pos0(phi))
+struct MixBC {
+  const double* wvf;    // waveTransmissive valueFraction [B]
+  const double* wref;   // waveTransmissive refValue (old-time boundary field) [B]
+  const double* bphi;   // boundary flux (inletOutlet switch) [B]
+  const double* ioref;  // inletValue [ncomp][B]
+};
+__device__ __forceinline__ void mix_vf_ref(int t, const MixBC& x, int b, long B, int comp, double& vf, double& ref) {
+  if (t == WAVE_TRANSMISSIVE) { vf = x.wvf[b]; ref = x.wref[b]; }
+  else { vf = x.bphi[b] >= 0.0 ? 0.0 : 1.0; ref = x.ioref[comp * B + b]; }
+}
+__device__ __forceinline__ BCoef bcoef_mixed(double vf, double ref, double bdc) {
+  return {1.0 - vf, vf * ref, -vf * bdc, vf * bdc * ref};
+}
 __device__ __forceinline__ BCoef bcoef(int t, double bval, double w, double bdc, double egrad = 0.0) {
   switch (t) {
     case ZERO_GRADIENT: case EXTRAPOLATED: return {1., 0., 0., 0.};
@@ -30,6 +46,16 @@ __device__ __forceinline__ BCoef bcoef(int t, double bval, double w, double bdc,
     case GRADIENT_ENERGY: return {1., egrad / bdc, 0., egrad};
     default: return {w, 1.0 - w, -1 * bdc, bdc};
   }
+}
+
+__device__ __forceinline__ BCoef bcoef_f(int t, double bval, double w, double bdc, const MixBC& mx, int b, long B, int comp,
+                                        double egrad = 0.0) {
+  if (bc_mixed(t)) {
+    double vf, ref;
+    mix_vf_ref(t, mx, b, B, comp, vf, ref);
+    return bcoef_mixed(vf, ref, bdc);
+  }
+  return bcoef(t, bval, w, bdc, egrad);
 }
 
 // coupled neighbour-side cell value: cyclic partner cell, or the processor halo value in the slot
@@ -82,7 +108,7 @@ template <class FN> __device__ __forceinline__ void each_slot(const MeshView& m,
 // gradientEnergy: cell value + gradient / deltaCoeffs (correct_boundary_conditions_gradientEnergy_scalar,
 // dfMatrixOpBase.cu:351-366)
 __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
-                             double* __restrict__ bvf, int ncomp, const double* __restrict__ egrad) {
+                             double* __restrict__ bvf, int ncomp, const double* __restrict__ egrad, MixBC mx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= m.B) return;
   const int t = ty[b];
@@ -90,7 +116,11 @@ __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const do
   for (int k = 0; k < ncomp; ++k) {
     const double* v = vf + (long)k * m.C;
     double* bv = bvf + (long)k * m.B;
-    if (t == ZERO_GRADIENT || t == EXTRAPOLATED) bv[b] = v[c];
+    if (bc_mixed(t)) {   // mixedFvPatchField::evaluate
+      double f, ref;
+      mix_vf_ref(t, mx, b, m.B, k, f, ref);
+      bv[b] = f * ref + (1.0 - f) * v[c];
+    } else if (t == ZERO_GRADIENT || t == EXTRAPOLATED) bv[b] = v[c];
     else if (t == CYCLIC) bv[b] = interp_b(m.bw[b], v[c], v[m.partner[b]]);
     else if (bc_proc(t) && !m.sprim[b]) bv[b] = v[c];
     else if (t == GRADIENT_ENERGY && egrad) bv[b] = v[c] + egrad[b] / m.bdc[b];
@@ -185,7 +215,7 @@ __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __rest
     double bg[9], bo[9];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const double sn = (t == FIXED_VALUE) ? m.bdc[b] * (bU[j * B + b] - U[j * C + c]) : 0.0;
+      const double sn = (t == FIXED_VALUE || bc_mixed(t)) ? m.bdc[b] * (bU[j * B + b] - U[j * C + c]) : 0.0;
       const double corr = sn - (nv[0] * g[0 * 3 + j] + nv[1] * g[1 * 3 + j] + nv[2] * g[2 * 3 + j]);
 #pragma unroll
       for (int i = 0; i < 3; ++i) bg[i * 3 + j] = g[i * 3 + j] + nv[i] * corr;
@@ -205,7 +235,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
     const double* __restrict__ mu, const double* __restrict__ bmu, const double* __restrict__ p,
     const double* __restrict__ bp, const double* __restrict__ T, const double* __restrict__ bT,
     double* __restrict__ lower, double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src,
-    double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU) {
+    double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU, MixBC mxU) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -267,7 +297,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
     double icv[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const BCoef q = bcoef(t, bU[k * B + b], m.bw[b], m.bdc[b]);
+      const BCoef q = bcoef_f(t, bU[k * B + b], m.bw[b], m.bdc[b], mxU, b, B, k);
       icv[k] = bphi[b] * q.vic + (-(pG * q.gic));
       ic[k * B + b] = icv[k];
       bc[k * B + b] = -bphi[b] * q.vbc + (-(-pG * q.gbc));
@@ -369,7 +399,8 @@ __global__ void k_p_slot(MeshView m, const int8_t* __restrict__ tyP, const int8_
                          const double* __restrict__ bU_old, const double* __restrict__ bphi_old,
                          const double* __restrict__ H, const double* __restrict__ bH, const double* __restrict__ bp,
                          double* __restrict__ brf, double* __restrict__ bph, double* __restrict__ ic,
-                         double* __restrict__ bc) {
+                         double* __restrict__ bc, MixBC mxP, const double* __restrict__ bphi,
+                         const double* __restrict__ bpsi, const double* __restrict__ gamma, double* __restrict__ wvf) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= m.B) return;
   const long C = m.C, B = m.B;
@@ -397,7 +428,16 @@ __global__ void k_p_slot(MeshView m, const int8_t* __restrict__ tyP, const int8_
   const double coeff = bc_fixes_value(tu) ? 0.0 : 1.0 - fmin(fabs(phiCorr) / (fabs(bphi_old[b]) + 1e-15), 1.0);
   const double fl = s0 * Hb[0] + s1 * Hb[1] + s2 * Hb[2];
   bph[b] = rb * fl + r * (coeff * m.rdt * phiCorr);
-  const BCoef q = bcoef(t, bp[b], bw, m.bdc[b]);
+  BCoef q;
+  if (t == WAVE_TRANSMISSIVE) {
+    // waveTransmissiveFvPatchField::advectionSpeed = phi_p / (rho_p |Sf|) + sqrt(gamma / psi_p);
+    // advectiveFvPatchField::updateCoeffs (Euler): valueFraction = 1 / (1 + w dt deltaCoeffs),
+    // refValue = p.oldTime() on the patch
+    const double wsp = fmax(bphi[b] / (brho[b] * m.bmagSf[b]) + sqrt(gamma[b] / bpsi[b]), 0.0);
+    const double vf = 1.0 / (1.0 + wsp * (1.0 / m.rdt) * m.bdc[b]);
+    wvf[b] = vf;
+    q = bcoef_mixed(vf, mxP.wref[b], m.bdc[b]);
+  } else q = bcoef_f(t, bp[b], bw, m.bdc[b], mxP, b, m.B, 0);
   const double pG = r * m.bmagSf[b];
   ic[b] = -(pG * q.gic);
   bc[b] = -(-pG * q.gbc);
@@ -538,7 +578,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
         const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
         v = interp_b(m.bw[b], ahc[s], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[s]));
       } else {
-        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
+        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
         v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
       }
       lap[s] += v;
@@ -586,7 +626,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
     double bg[S][3];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
+      const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
       const double corr = sn - (nv[0] * g[s][0] + nv[1] * g[s][1] + nv[2] * g[s][2]);
 #pragma unroll
       for (int k = 0; k < 3; ++k) bg[s][k] = g[s][k] + nv[k] * corr;
@@ -646,7 +686,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
-    double* __restrict__ bc) {
+    double* __restrict__ bc, MixBC mxY) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -685,8 +725,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       if (s == inert) continue;
-      const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
-      const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+      const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+      const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
       const double gam = bc_coupled(t) ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
       const double pG = gam * m.bmagSf[b];
       ic[s * B + b] = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
@@ -706,7 +746,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
-    double* __restrict__ dS, double* __restrict__ rhs) {
+    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
@@ -750,8 +790,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     for (int s = 0; s < S; ++s) {
       if (s == inert) continue;
       const int ss = s < inert ? s : s - 1;
-      const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
-      const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+      const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+      const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
       const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
       const double pG = gam * m.bmagSf[b];
       const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
@@ -852,7 +892,7 @@ __device__ __forceinline__ void y_chunk_grad(const MeshView& m, const int8_t* __
           const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
           v = interp_b(m.bw[b], ahc[j], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[j]));
         } else {
-          const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - yc[j]) : 0.0;
+          const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc[j]) : 0.0;
           v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
         }
         lap[j] += v;
@@ -878,7 +918,7 @@ __device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, i
   for (int j = 0; j < CH; ++j) {
     const int s = s0 + j;
     if (s >= S) break;
-    const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
+    const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
     const double corr = sn - (nv[0] * g[j][0] + nv[1] * g[j][1] + nv[2] * g[j][2]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) bg[j][k] = g[j][k] + nv[k] * corr;
@@ -974,7 +1014,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
-    double* __restrict__ bc) {
+    double* __restrict__ bc, MixBC mxY) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -1020,8 +1060,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
         const int s = s0 + j;
         if (s >= S) break;
         if (s == inert) continue;
-        const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
-        const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+        const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+        const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
         const double gam = bc_coupled(t) ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
         const double pG = gam * m.bmagSf[b];
         ic[s * B + b] = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
@@ -1038,7 +1078,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
-    double* __restrict__ dS, double* __restrict__ rhs) {
+    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
@@ -1088,8 +1128,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
         if (s >= S) break;
         if (s == inert) continue;
         const int ss = s < inert ? s : s - 1;
-        const BCoef qc = bcoef(t, bY[s * B + b], wu, m.bdc[b]);
-        const BCoef ql = bcoef(t, bY[s * B + b], m.bw[b], m.bdc[b]);
+        const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+        const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
         const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
         const double pG = gam * m.bmagSf[b];
         const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
@@ -1235,9 +1275,18 @@ bool face_rows(const Ctx& x) {
 #define LAUNCH_SW(kern, NS, n, ...) \
   do { if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
 
+// the mixed-condition data of a field (MixBC): p's waveTransmissive state, every field's inletValue
+MixBC mixbc(Ctx& x, const std::string& field) {
+  MixBC m{nullptr, nullptr, x.f("boundary_phi"), nullptr};
+  if (field == "p") { m.wvf = x.f("boundary_p_vf"); m.wref = x.f("boundary_p_old"); }
+  auto it = x.fields.find("boundary_" + field + "_ref");
+  if (it != x.fields.end()) m.ioref = it->second.buf.p;
+  return m;
+}
+
 void k_bc_correct(Ctx& x, const char* tf, double* vf, double* bvf, int ncomp) {
   const double* eg = std::string(tf) == "he" ? x.f("boundary_heGradient") : nullptr;
-  LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp, eg);
+  LAUNCH(k_bc_correct, x.B, x.view(), x.st(tf), vf, bvf, ncomp, eg, mixbc(x, tf));
 }
 
 void copy_old(Ctx& x) {   // dfMatrixDataBase::preTimeStep (dfMatrixDataBase.cu:503-517)
@@ -1274,7 +1323,7 @@ void u_assemble(Ctx& x) {
   LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
          x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
          x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
-         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"));
+         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"));
   k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
   halo_fields(x, {"rAU"});
 }
@@ -1304,7 +1353,8 @@ void p_assemble(Ctx& x) {
   LAUNCH(k_p_slot, x.B, m, x.st("p"), x.st("U"), x.f("rho"), x.f("boundary_rho"), x.f("rAU"), x.f("boundary_rAU"),
          x.f("rho_old"), x.f("boundary_rho_old"), x.f("U_old"), x.f("boundary_U_old"), x.f("boundary_phi_old"),
          x.f("HbyA"), x.f("boundary_HbyA"), x.f("boundary_p"), x.f("boundary_rhorAUf"), x.f("boundary_phiHbyA"),
-         A.ic.p, A.bc.p);
+         A.ic.p, A.bc.p, mixbc(x, "p"), x.f("boundary_phi"), x.f("boundary_psi"), x.f("boundary_p_gamma"),
+         x.f("boundary_p_vf"));
   LAUNCH_W(k_p_cell, x.C, m, x.st("p"), A.lower.p, x.f("phiHbyA"), x.f("boundary_phiHbyA"), x.f("p"), x.f("p_old"),
          x.f("psi"), x.f("rho"), x.f("rho_old"), A.diag.p, A.source.p);
 }
@@ -1365,11 +1415,11 @@ void y_assemble(Ctx& x) {
   MeshView m = x.view();
 #define CALL(NS) LAUNCH_SW(k_y_assemble, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
-                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p)
+                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y"))
   DFMI_SWITCH_S(x.S, CALL,
                 LAUNCH_SW(k_y_assemble_gen, YCH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"),
-                       x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p))
+                       x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y")))
 #undef CALL
 }
 
@@ -1377,11 +1427,11 @@ void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs
   MeshView m = x.view();
 #define CALL(NS) LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
-                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs)
+                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"))
   DFMI_SWITCH_S(x.S, CALL,
                 LAUNCH_SW(k_y_assemble_ell_gen, YCH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"),
                        x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),
-                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs))
+                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y")))
 #undef CALL
 }
 

@@ -43,6 +43,7 @@ SIGNATURES = {
     "dfmi_init_constant_fields_boundary": [_P, _DP, _DP, _DP, _DP, _IP, _IP, _IP],
     "dfmi_set_patch_types": [_P, C.c_char_p, _IP],
     "dfmi_set_inert_index": [_P, C.c_int],
+    "dfmi_set_patch_param": [_P, C.c_char_p, C.c_int, C.c_char_p, C.c_double],
     "dfmi_thermo_set_coeffs": [_P, C.c_int, _DP, _DP, _DP, _DP, _DP],
     "dfmi_thermo_load": [_P, C.c_char_p],
     "dfmi_set_field": [_P, C.c_char_p, _DP, C.c_long, C.c_int],
@@ -221,6 +222,9 @@ class Context:
 
     def set_patch_types(self, field, types):
         a = _i32(types); self._call("dfmi_set_patch_types", self.h, field.encode(), _ip(a))
+
+    def set_patch_param(self, field, patch, name, value):
+        self._call("dfmi_set_patch_param", self.h, field.encode(), int(patch), name.encode(), float(value))
 
     def set_inert_index(self, i):
         self._call("dfmi_set_inert_index", self.h, int(i))

@@ -36,12 +36,15 @@ PROCESSOR = 7
 EXTRAPOLATED = 8
 FIXED_ENERGY = 9
 PROCESSOR_CYCLIC = 10
+WAVE_TRANSMISSIVE = 11   # mixed conditions beyond the reference GPU enum (include/dfmi.h)
+INLET_OUTLET = 12
 
 BC_NAMES = {
     "zeroGradient": ZERO_GRADIENT, "fixedValue": FIXED_VALUE, "coupled": COUPLED,
     "empty": EMPTY, "gradientEnergy": GRADIENT_ENERGY, "calculated": CALCULATED,
     "cyclic": CYCLIC, "processor": PROCESSOR, "extrapolated": EXTRAPOLATED,
     "fixedEnergy": FIXED_ENERGY, "processorCyclic": PROCESSOR_CYCLIC,
+    "waveTransmissive": WAVE_TRANSMISSIVE, "inletOutlet": INLET_OUTLET,
 }
 
 

@@ -13,7 +13,10 @@
  *    takes 2n slots [neighbour values | patch-internal values] (createGPUSolver.H:118-123);
  *  - patch type codes: zeroGradient 0, fixedValue 1, coupled 2, empty 3, gradientEnergy 4,
  *    calculated 5, cyclic 6, processor 7, extrapolated 8, fixedEnergy 9, processorCyclic 10
- *    (dfMatrixDataBase.H:81-93);
+ *    (dfMatrixDataBase.H:81-93), plus waveTransmissive 11 (p only; gamma via dfmi_set_patch_param,
+ *    OpenFOAM-7 advectiveFvPatchField semantics with Euler ddt) and inletOutlet 12 (U, p, Y, K;
+ *    inletValue in the field "boundary_<field>_ref") -- the mixed conditions the reference GPU path
+ *    rejects (dfMatrixDataBase.cu:22-27) though its own 1D-flame case uses one (test/Tu500K-Phi1/0/p);
  *  - every call returns 0 on success, non-zero on error, and never exits the process
  *    (the reference exit()s, dfMatrixDataBase.H:40-50); dfmi_last_error() gives the message.
  */
@@ -91,6 +94,8 @@ int dfmi_renumber_faces(int num_cells, int num_faces, const int* owner, const in
  * dfEEqn.cu setConstantFields, dfThermo.cu setConstantFields). field in
  * {"U","p","he","K","Y","T","rho"}; patch_type[num_patches] */
 int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type);
+/* a patch parameter of a mixed condition: (field "p", name "gamma") of waveTransmissive */
+int dfmi_set_patch_param(dfmi_ctx* ctx, const char* field, int patch, const char* name, double value);
 /* dfYEqn inertIndex (YEqn.H:119-131) */
 int dfmi_set_inert_index(dfmi_ctx* ctx, int inert_index);
 
@@ -105,7 +110,9 @@ int dfmi_thermo_load(dfmi_ctx* ctx, const char* thermo_coeff_file);
 /* names: cells  rho rho_old p p_old he T K K_old psi mu alpha dpdt rAU diffAlphaD psip0
  *        vector U U_old HbyA hDiffCorrFlux sumYDiffError     species Y rhoD hai RR
  *        faces  phi phi_old phiUc rhorAUf phiHbyA
- *        boundary_<name> for the boundary counterparts. count = values per component. */
+ *        boundary_<name> for the boundary counterparts; boundary-only: boundary_heGradient,
+ *        boundary_{U,p,Y,K}_ref (inletOutlet inletValue), boundary_p_vf (waveTransmissive valueFraction),
+ *        boundary_p_gamma, chem_stats [3][C]. count = values per component. */
 int dfmi_set_field(dfmi_ctx* ctx, const char* name, const double* host, long count, int layout);
 int dfmi_get_field(dfmi_ctx* ctx, const char* name, double* host, long count, int layout);
 

@@ -36,7 +36,10 @@
 namespace {
 
 enum BC { ZG = 0, FV = 1, COUPLED = 2, EMPTY = 3, GRAD_E = 4, CALC = 5, CYCLIC = 6, PROC = 7, EXTRAP = 8,
-          FIX_E = 9, PROC_CYC = 10 };
+          FIX_E = 9, PROC_CYC = 10, WAVE = 11, IN_OUT = 12 };
+// mixedFvPatchField family: waveTransmissive (advectiveFvPatchField, OpenFOAM-7; the 1D flame's outlet p,
+// test/Tu500K-Phi1/0/p:34) and inletOutlet; value = f ref + (1 - f) cell
+inline bool is_mixed(int t) { return t == WAVE || t == IN_OUT; }
 inline bool is_coupled(int t) { return t == CYCLIC || t == PROC || t == PROC_CYC || t == COUPLED; }
 inline bool is_proc(int t) { return t == PROC || t == PROC_CYC; }
 inline bool fixes_value(int t) { return t == FV || t == FIX_E; }
@@ -105,6 +108,23 @@ inline double nbr(const M& m, const double* vf, const double* bvf, int b) {
 inline double interp_f(double w, double vo, double vn) { return w * (vo - vn) + vn; }      // surfaceInterpolation::interpolate
 inline double interp_b(double w, double vo, double vn) { return w * vo + (1.0 - w) * vn; } // coupledFvPatchField::evaluate
 
+// per-slot data of a field's mixed conditions: waveTransmissive valueFraction (set at the pEqn
+// assembly) and refValue = old-time boundary value; inletOutlet valueFraction = 1 - pos0(phi_b),
+// refValue = inletValue
+struct Mix { const double *wvf, *wref, *bphi, *ioref; };
+Mix mix_for(const std::string& field) {
+  Mix x{nullptr, nullptr, nullptr, nullptr};
+  if (has("boundary_phi")) x.bphi = d("boundary_phi");
+  if (field == "p" && has("boundary_p_vf")) { x.wvf = d("boundary_p_vf"); x.wref = d("boundary_p_old"); }
+  std::string r = "boundary_" + field + "_ref";
+  if (has(r.c_str())) x.ioref = d(r.c_str());
+  return x;
+}
+inline void mix_vf_ref(int t, const Mix& x, int b, int B, int comp, double& vf, double& ref) {
+  if (t == WAVE) { vf = x.wvf[b]; ref = x.wref[b]; }
+  else { vf = x.bphi[b] >= 0.0 ? 0.0 : 1.0; ref = x.ioref[(long)comp * B + b]; }
+}
+
 // value/gradient coefficients (valueInternalCoeffs etc.; dfMatrixOpBase.cu:279-621)
 struct BCoef { double vic, vbc, gic, gbc; };
 inline BCoef bcoef(int t, double bval, double w, double bdc, double egrad = 0.0) {
@@ -114,6 +134,16 @@ inline BCoef bcoef(int t, double bval, double w, double bdc, double egrad = 0.0)
     case GRAD_E: return {1., egrad / bdc, 0., egrad};
     default: return {w, 1.0 - w, -1 * bdc, bdc};   // coupled
   }
+}
+
+// the same, for a field that may carry mixed conditions (mixedFvPatchField::value/gradient*Coeffs)
+inline BCoef bcoef_f(int t, double bval, double w, double bdc, const Mix& mx, int b, int B, int comp, double egrad = 0.0) {
+  if (is_mixed(t)) {
+    double vf, ref;
+    mix_vf_ref(t, mx, b, B, comp, vf, ref);
+    return {1.0 - vf, vf * ref, -vf * bdc, vf * bdc * ref};
+  }
+  return bcoef(t, bval, w, bdc, egrad);
 }
 
 template <class FN> void for_slots(const M& m, const int* type, FN fn) {
@@ -142,19 +172,25 @@ std::vector<double> neg_sum_diag(const M& m, const double* L, const double* U) {
 // ---------------------------------------------------------------- BC correction
 // correct_boundary_conditions_scalar (dfMatrixOpBase.cu:2402-2450). Processor slots refresh
 // only their [internal n] part here; the [neighbour n] part is the halo exchange's job.
-void correct_bc_scalar(const M& m, const int* type, const double* vf, double* bvf) {
+void correct_bc_scalar(const M& m, const int* type, const double* vf, double* bvf, const Mix* mx = nullptr,
+                       int comp = 0) {
   for (int b = 0; b < m.B; ++b) {
     int t = type[m.slot_patch[b]];
     int c = m.bfc[b];
-    if (t == ZG || t == EXTRAP) bvf[b] = vf[c];
+    if (is_mixed(t)) {
+      if (!mx) throw std::runtime_error("oracle: mixed boundary condition without its field data");
+      double f, ref;
+      mix_vf_ref(t, *mx, b, m.B, comp, f, ref);
+      bvf[b] = f * ref + (1.0 - f) * vf[c];
+    } else if (t == ZG || t == EXTRAP) bvf[b] = vf[c];
     else if (t == CYCLIC) bvf[b] = interp_b(m.bw[b], vf[c], vf[m.partner_cell[b]]);
     else if (is_proc(t) && !m.primary[b]) bvf[b] = vf[c];
     else if (t == GRAD_E && has("boundary_heGradient"))   // dfMatrixOpBase.cu:351-366
       bvf[b] = vf[c] + d("boundary_heGradient")[b] / m.bdc[b];
   }
 }
-void correct_bc_vec(const M& m, const int* type, const double* vf, double* bvf, int ncomp) {
-  for (int k = 0; k < ncomp; ++k) correct_bc_scalar(m, type, vf + (long)k * m.C, bvf + (long)k * m.B);
+void correct_bc_vec(const M& m, const int* type, const double* vf, double* bvf, int ncomp, const Mix* mx = nullptr) {
+  for (int k = 0; k < ncomp; ++k) correct_bc_scalar(m, type, vf + (long)k * m.C, bvf + (long)k * m.B, mx, k);
 }
 
 // face value of a scalar field on a boundary slot (linear interpolation semantics)
@@ -198,7 +234,7 @@ void grad_scalar(const M& m, const int* type, const double* vf, const double* bv
     }
     double nx = m.bsf(0, b) / m.bmagSf[b], ny = m.bsf(1, b) / m.bmagSf[b], nz = m.bsf(2, b) / m.bmagSf[b];
     double gx = g[c], gy = g[(long)m.C + c], gz = g[2L * m.C + c];
-    double sn = (t == FV || t == CALC || t == FIX_E) ? m.bdc[b] * (bvf[b] - vf[c]) : 0.0;
+    double sn = (t == FV || t == CALC || t == FIX_E || is_mixed(t)) ? m.bdc[b] * (bvf[b] - vf[c]) : 0.0;
     double corr = sn - (nx * gx + ny * gy + nz * gz);
     bg[b] = gx + nx * corr; bg[(long)m.B + b] = gy + ny * corr; bg[2L * m.B + b] = gz + nz * corr;
   }
@@ -228,11 +264,12 @@ void u_eqn_assemble(const M& m) {
   for (int f = 0; f < F; ++f) { lower[f] = L1[f] + (-UL[f]); upper[f] = U1[f] + (-UL[f]); }
   for (int c = 0; c < C; ++c) diag[c] = (m.rdt * rho[c] * m.V[c] + d1[c]) + (-dL[c]);
   std::fill(ic, ic + 3L * B, 0.0); std::fill(bc, bc + 3L * B, 0.0);
+  const Mix mxU = mix_for("U");
   for_slots(m, tU, [&](int b, int t, int c) {
     double gam = is_coupled(t) ? interp_b(m.bw[b], mu[c], nbr(m, mu, bmu, b)) : bmu[b];
     double pG = gam * m.bmagSf[b];
     for (int k = 0; k < 3; ++k) {
-      BCoef q = bcoef(t, bU[(long)k * B + b], m.bw[b], m.bdc[b]);
+      BCoef q = bcoef_f(t, bU[(long)k * B + b], m.bw[b], m.bdc[b], mxU, b, B, k);
       ic[(long)k * B + b] = bphi[b] * q.vic + (-(pG * q.gic));
       bc[(long)k * B + b] = -bphi[b] * q.vbc + (-(-pG * q.gbc));
     }
@@ -251,7 +288,7 @@ void u_eqn_assemble(const M& m) {
     int c = m.bfc[b];
     double nv[3] = {m.bsf(0, b) / m.bmagSf[b], m.bsf(1, b) / m.bmagSf[b], m.bsf(2, b) / m.bmagSf[b]};
     for (int j = 0; j < 3; ++j) {
-      double sn = (t == FV) ? m.bdc[b] * (bU[(long)j * B + b] - U[(long)j * C + c]) : 0.0;
+      double sn = (t == FV || is_mixed(t)) ? m.bdc[b] * (bU[(long)j * B + b] - U[(long)j * C + c]) : 0.0;
       double gc[3] = {g[(long)(0 * 3 + j) * C + c], g[(long)(1 * 3 + j) * C + c], g[(long)(2 * 3 + j) * C + c]};
       double corr = sn - (nv[0] * gc[0] + nv[1] * gc[1] + nv[2] * gc[2]);
       for (int i = 0; i < 3; ++i) bg[(long)(i * 3 + j) * B + b] = gc[i] + nv[i] * corr;
@@ -416,8 +453,18 @@ void p_eqn_assemble(const M& m) {
   }
   for (int f = 0; f < F; ++f) { lower[f] = -UL[f]; upper[f] = -UL[f]; }
   std::fill(ic, ic + B, 0.0); std::fill(bc, bc + B, 0.0);
+  const Mix mxP = mix_for("p");
   for_slots(m, tp, [&](int b, int t, int) {
-    BCoef q = bcoef(t, bp[b], m.bw[b], m.bdc[b]);
+    BCoef q;
+    if (t == WAVE) {   // advectiveFvPatchField::updateCoeffs (Euler), waveTransmissive::advectionSpeed
+      const double* bph_now = d("boundary_phi");
+      double wsp = bph_now[b] / (brho[b] * m.bmagSf[b]) + std::sqrt(d("boundary_p_gamma")[b] / d("boundary_psi")[b]);
+      wsp = std::fmax(wsp, 0.0);
+      double vf = 1.0 / (1.0 + wsp * (1.0 / m.rdt) * m.bdc[b]);
+      d("boundary_p_vf")[b] = vf;
+      double ref = mxP.wref[b];
+      q = {1.0 - vf, vf * ref, -vf * m.bdc[b], vf * m.bdc[b] * ref};
+    } else q = bcoef_f(t, bp[b], m.bw[b], m.bdc[b], mxP, b, B, 0);
     double pG = brf[b] * m.bmagSf[b];
     ic[b] = -(pG * q.gic);
     bc[b] = -(-pG * q.gbc);
@@ -434,7 +481,7 @@ void p_eqn_post(const M& m) {
   double *ph = d("peqn_phiHbyA"), *bph = d("peqn_boundary_phiHbyA");
   double *phi = d("phi"), *bphi = d("boundary_phi"), *U = d("U"), *bU = d("boundary_U");
   double *H = d("HbyA"), *rAU = d("rAU"), *K = d("K"), *bK = d("boundary_K"), *dpdt = d("dpdt");
-  correct_bc_scalar(m, tp, p, bp);
+  { const Mix mx = mix_for("p"); correct_bc_scalar(m, tp, p, bp, &mx); }
   for (int f = 0; f < F; ++f) phi[f] = ph[f] + (upper[f] * p[m.nei[f]] - lower[f] * p[m.own[f]]);  // lduMatrix::faceH
   for_slots(m, tp, [&](int b, int t, int c) {              // fvMatrix::flux boundary
     double fl = is_coupled(t) ? ic[b] * p[c] - bc[b] * nbr(m, p, bp, b) : ic[b] * p[c] - bc[b];
@@ -444,7 +491,7 @@ void p_eqn_post(const M& m) {
   grad_scalar(m, tp, p, bp, g.data(), nullptr);
   for (int k = 0; k < 3; ++k)
     for (int c = 0; c < C; ++c) U[(long)k * C + c] = H[(long)k * C + c] - rAU[c] * g[(long)k * C + c];
-  correct_bc_vec(m, tU, U, bU, 3);
+  { const Mix mx = mix_for("U"); correct_bc_vec(m, tU, U, bU, 3, &mx); }
   for (int c = 0; c < C; ++c) K[c] = 0.5 * (U[c] * U[c] + U[(long)C + c] * U[(long)C + c] + U[2L * C + c] * U[2L * C + c]);
   for (int b = 0; b < B; ++b) bK[b] = 0.5 * (bU[b] * bU[b] + bU[(long)B + b] * bU[(long)B + b] + bU[2L * B + b] * bU[2L * B + b]);
   for (int c = 0; c < C; ++c) dpdt[c] = m.rdt * (p[c] - p_old[c]);
@@ -498,7 +545,7 @@ void y_prep(const M& m) {
             double an = m.partner_cell[b] >= 0 ? ah[m.partner_cell[b]] : balpha[b] * bhs[b];
             return interp_b(m.bw[b], ah[c], an) * m.bmagSf[b] * (m.bdc[b] * (nbr(m, y, by, b) - y[c]));
           }
-          double sng = (t == FV || t == CALC || t == FIX_E) ? m.bdc[b] * (by[b] - y[c]) : 0.0;
+          double sng = (t == FV || t == CALC || t == FIX_E || is_mixed(t)) ? m.bdc[b] * (by[b] - y[c]) : 0.0;
           return balpha[b] * bhs[b] * m.bmagSf[b] * sng; });
     for (int c = 0; c < C; ++c) dAD[c] = dAD[c] + lap[c] / m.V[c];
   }
@@ -542,6 +589,7 @@ void y_assemble(const M& m) {
   std::fill(lo, lo + (long)S * F, 0.0); std::fill(up, up + (long)S * F, 0.0);
   std::fill(dg, dg + (long)S * C, 0.0); std::fill(sr, sr + (long)S * C, 0.0);
   std::fill(icA, icA + (long)S * B, 0.0); std::fill(bcA, bcA + (long)S * B, 0.0);
+  const Mix mxY = mix_for("Y");
   for (int s = 0; s < S; ++s) {
     if (s == inert) continue;
     const double *rd = rhoD + (long)s * C, *brd = brhoD + (long)s * B, *y = Y + (long)s * C, *by = bY + (long)s * B;
@@ -557,8 +605,8 @@ void y_assemble(const M& m) {
     }
     for_slots(m, tY, [&](int b, int t, int c) {
       double wu = bphi[b] >= 0 ? 1.0 : 0.0;
-      BCoef qc = bcoef(t, by[b], wu, m.bdc[b]);
-      BCoef ql = bcoef(t, by[b], m.bw[b], m.bdc[b]);
+      BCoef qc = bcoef_f(t, by[b], wu, m.bdc[b], mxY, b, B, s);
+      BCoef ql = bcoef_f(t, by[b], m.bw[b], m.bdc[b], mxY, b, B, s);
       double gam = is_coupled(t) ? interp_b(m.bw[b], rd[c], nbr(m, rd, brd, b)) : brd[b];
       double pG = gam * m.bmagSf[b];
       icA[(long)s * B + b] = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
@@ -584,7 +632,8 @@ void y_inert(const M& m) {
     sum = 1 - sum;
     Y[(long)inert * m.C + c] = sum > 0 ? sum : 0;
   }
-  for (int s = 0; s < m.S; ++s) correct_bc_scalar(m, tY, Y + (long)s * m.C, bY + (long)s * m.B);
+  const Mix mx = mix_for("Y");
+  for (int s = 0; s < m.S; ++s) correct_bc_scalar(m, tY, Y + (long)s * m.C, bY + (long)s * m.B, &mx, s);
 }
 
 // ---------------------------------------------------------------- EEqn (EEqn.H:12-45; dfEEqn.cu:108-264)
@@ -810,7 +859,8 @@ int orc_e_assemble() { ORC_CALL(e_assemble(m)) }
 int orc_thermo_correct(int from_T) { ORC_CALL(thermo_correct(m, from_T != 0)) }
 int orc_energy_gradient() { ORC_CALL(energy_gradient(m)) }
 int orc_correct_bc(const char* field, const char* bfield, const char* ptype, int ncomp) {
-  ORC_CALL(correct_bc_vec(m, ia(ptype), d(field), d(bfield), ncomp))
+  const Mix mx = mix_for(field);
+  ORC_CALL(correct_bc_vec(m, ia(ptype), d(field), d(bfield), ncomp, &mx))
 }
 int orc_grad_scalar(const char* field, const char* bfield, const char* ptype, const char* out, const char* bout) {
   ORC_CALL(grad_scalar(m, ia(ptype), d(field), d(bfield), d(out), bout ? d(bout) : nullptr))

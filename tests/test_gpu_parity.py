@@ -47,7 +47,7 @@ def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
 
 
 def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False,
-          renumber=None):
+          renumber=None, mixed=False):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.lib import Context
     from dfmi import case
@@ -71,7 +71,12 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
     if mech == "gri53":   # every one of the 53 species present (Dirichlet-like draws)
         from dfmi.synthetic import gri53_mass_fractions
         f["Y"] = gri53_mass_fractions(m.n_cells, seed=1)
-    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"])
+    refs = gammas = None
+    if mixed:   # inletOutlet U/Y and waveTransmissive p on "right": the TGV flow crosses it both ways
+        yu, _ = case.h2_air_compositions(ym["species"])
+        refs = {"U": {"right": np.array([0.3, -0.1, 0.2])}, "Y": {"right": yu}}
+        gammas = {"right": 1.4}
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], refs=refs, gammas=gammas)
     ctx.call("pre_time_step")
     rng = np.random.default_rng(7)
     # perturb old-time fields so ddt/ddtCorr terms are exercised
@@ -96,7 +101,8 @@ def _oracle(m, t, st, pt, inert, dt):
 # species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
-                                        "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr"])
+                                        "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
+                                        "mixed", "mixed-generic"])
 def periodic(request):
     generic = request.param.endswith("-generic")
     if generic:
@@ -111,12 +117,14 @@ def periodic(request):
         if param.endswith("-" + meth):
             renumber, param = meth, param[: -len(meth) - 1]
     mech = "gri53" if param.startswith("gri53") else "burke9"
-    if param in ("walls", "distorted", "gri53-walls"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
-        from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY
+    if param in ("walls", "distorted", "gri53-walls", "mixed"):   # zeroGradient walls (+ fixedValue T/Y/U on two sides)
+        from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY, INLET_OUTLET, WAVE_TRANSMISSIVE
+        mixed = param == "mixed"
 
         def walls(m):
             fv = {}
-            fixed = [i for i, p in enumerate(m.patches) if p.name in ("left", "right")]
+            names = ("left",) if mixed else ("left", "right")
+            fixed = [i for i, p in enumerate(m.patches) if p.name in names]
             for f in ("U", "T", "Y"):
                 t = m.patch_types(0).copy()
                 t[fixed] = FIXED_VALUE
@@ -125,9 +133,16 @@ def periodic(request):
             t = m.patch_types(GRADIENT_ENERGY).copy()
             t[fixed] = FIXED_ENERGY
             fv["he"] = t
+            if mixed:   # an open outlet: the mixed conditions of the reference's own cases (0/p, 0/U)
+                out = [i for i, p in enumerate(m.patches) if p.name == "right"]
+                fv["U"][out] = INLET_OUTLET
+                fv["Y"][out] = INLET_OUTLET
+                fv["p"] = m.patch_types(0).copy()
+                fv["p"][out] = WAVE_TRANSMISSIVE
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
-        return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber)
+        return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber,
+                     mixed=mixed)
     return _case(mech=param, renumber=renumber, nx=16 if renumber else 6, ny=8 if renumber else 5,
                  nz=4 if renumber else 4)
 
@@ -188,6 +203,8 @@ def test_p_eqn_assembly_bitwise(periodic):
     assert not bad, bad
     assert ulp_diff(ctx.get_field("phiHbyA", (m.n_faces,)), ref["phiHbyA"]) == 0
     assert ulp_diff(ctx.get_field("rhorAUf", (m.n_faces,)), ref["rhorAUf"]) == 0
+    vf = ctx.get_field("boundary_p_vf", (m.n_boundary_slots,))     # waveTransmissive valueFraction
+    assert ulp_diff(vf, o["boundary_p_vf"]) == 0
 
 
 def test_y_eqn_assembly_bitwise(periodic):
@@ -300,6 +317,14 @@ def test_full_outer_iteration(periodic):
     assert rel_err(Y, o["Y"]) < 1e-9            # per species (trace species included)
     phi = ctx.get_field("phi", (m.n_faces,))
     assert rel_err(phi, o["phi"]) < 1e-9
+    B = m.n_boundary_slots
+    for n, shp in (("boundary_U", (3, B)), ("boundary_Y", (t.S, B)), ("boundary_p", (B,)), ("boundary_phi", (B,))):
+        assert rel_err(ctx.get_field(n, shp), o[n]) < 1e-9, n
+    from dfmi.mesh import INLET_OUTLET
+    io = np.repeat(np.asarray(pt["U"]) == INLET_OUTLET, [p.slots for p in m.patches])
+    if io.any():   # inletOutlet switched per slot on the flux sign: inflow -> inletValue, outflow -> cell
+        bphi = ctx.get_field("boundary_phi", (B,))
+        assert (io & (bphi < 0)).any() and (io & (bphi >= 0)).any()
     for e in ("U", "Y", "E"):
         ctx.set_solver(e, 20, 1e-5)
     ctx.set_solver("p", 1000, 1e-5)
