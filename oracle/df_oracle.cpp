@@ -24,6 +24,11 @@
 //    surfaceInterpolation linear weights); explicit fvc terms enter the source as the
 //    face sum itself (the reference skips the /V then *V round trip);
 //  * built with -ffp-contract=off (the reference used -fmad=false, src_gpu/CMakeLists.txt:17).
+//
+// Parallelism (OpenMP): the per-face scatter "owner +=, neighbour -=" is evaluated as a per-cell
+// gather over the cell's faces in increasing face index -- the very order in which the sequential
+// loop would have added them -- so every partial sum is bitwise the sequential one. Boundary-slot
+// scatters stay sequential (several slots may share a cell).
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -60,11 +65,31 @@ int* ia(const char* k) {
   return it->second;
 }
 
+// cell -> faces, merged in increasing face index: entry f (cell owns f) or ~f (cell is f's neighbour)
+struct CellFaces {
+  const int *own = nullptr, *nei = nullptr;
+  int C = -1, F = -1;
+  std::vector<int> start, face;
+};
+CellFaces g_cf;
+const CellFaces& cell_faces(int C, int F, const int* own, const int* nei) {
+  if (g_cf.own == own && g_cf.nei == nei && g_cf.C == C && g_cf.F == F) return g_cf;
+  g_cf.own = own; g_cf.nei = nei; g_cf.C = C; g_cf.F = F;
+  g_cf.start.assign(C + 1, 0);
+  for (int f = 0; f < F; ++f) { g_cf.start[own[f] + 1]++; g_cf.start[nei[f] + 1]++; }
+  for (int c = 0; c < C; ++c) g_cf.start[c + 1] += g_cf.start[c];
+  g_cf.face.resize(2L * F);
+  std::vector<int> pos(g_cf.start.begin(), g_cf.start.end() - 1);
+  for (int f = 0; f < F; ++f) { g_cf.face[pos[own[f]]++] = f; g_cf.face[pos[nei[f]]++] = ~f; }   // f ascending
+  return g_cf;
+}
+
 struct M {
   int C, F, B, P, S;
   const int *own, *nei, *psize, *cyc_nbr, *bfc, *kind;
   const double *Sf, *magSf, *w, *dc, *V, *bSf, *bmagSf, *bw, *bdc;
   std::vector<int> poff, slot_patch, primary, partner_cell;
+  const int *cfs, *cff;   // cell_faces
   double rdt;
   double sf(int k, int f) const { return Sf[(long)k * F + f]; }
   double bsf(int k, int b) const { return bSf[(long)k * B + b]; }
@@ -80,6 +105,8 @@ M mesh() {
   m.bSf = d("boundary_sf"); m.bmagSf = d("boundary_mag_sf"); m.bw = d("boundary_weight");
   m.bdc = d("boundary_delta_coeffs");
   m.rdt = d("rdelta_t")[0];
+  const CellFaces& cf = cell_faces(m.C, m.F, m.own, m.nei);
+  m.cfs = cf.start.data(); m.cff = cf.face.data();
   m.poff.resize(m.P + 1);
   m.slot_patch.assign(m.B, -1);
   m.primary.assign(m.B, 0);
@@ -155,17 +182,32 @@ template <class FN> void for_slots(const M& m, const int* type, FN fn) {
   }
 }
 
+// per-cell gather of face terms in increasing face index: fo(f) where the cell owns f, fn(f) where
+// it is f's neighbour, folded into a sum starting from 0
+template <class FO, class FN> void gather(const M& m, double* s, FO fo, FN fn) {
+#pragma omp parallel for schedule(static)
+  for (int c = 0; c < m.C; ++c) {
+    double a = 0.0;
+    for (int e = m.cfs[c]; e < m.cfs[c + 1]; ++e) {
+      const int f = m.cff[e];
+      a = f >= 0 ? fo(a, f) : fn(a, ~f);
+    }
+    s[c] = a;
+  }
+}
 // fvc::surfaceIntegrate without the /V: owner +=, neighbour -=, then boundary +=
 template <class FF, class FB> std::vector<double> integrate(const M& m, const int* type, FF face, FB bnd) {
-  std::vector<double> s(m.C, 0.0);
-  for (int f = 0; f < m.F; ++f) { double v = face(f); s[m.own[f]] += v; s[m.nei[f]] -= v; }
+  std::vector<double> v(m.F), s(m.C);
+#pragma omp parallel for schedule(static)
+  for (int f = 0; f < m.F; ++f) v[f] = face(f);
+  gather(m, s.data(), [&](double a, int f) { return a + v[f]; }, [&](double a, int f) { return a - v[f]; });
   for_slots(m, type, [&](int b, int t, int c) { s[c] += bnd(b, t, c); });
   return s;
 }
 // lduMatrix::negSumDiag
 std::vector<double> neg_sum_diag(const M& m, const double* L, const double* U) {
-  std::vector<double> s(m.C, 0.0);
-  for (int f = 0; f < m.F; ++f) { s[m.own[f]] -= L[f]; s[m.nei[f]] -= U[f]; }
+  std::vector<double> s(m.C);
+  gather(m, s.data(), [&](double a, int f) { return a - L[f]; }, [&](double a, int f) { return a - U[f]; });
   return s;
 }
 
@@ -174,19 +216,23 @@ std::vector<double> neg_sum_diag(const M& m, const double* L, const double* U) {
 // only their [internal n] part here; the [neighbour n] part is the halo exchange's job.
 void correct_bc_scalar(const M& m, const int* type, const double* vf, double* bvf, const Mix* mx = nullptr,
                        int comp = 0) {
+  if (!mx)
+    for (int b = 0; b < m.B; ++b)
+      if (is_mixed(type[m.slot_patch[b]])) throw std::runtime_error("oracle: mixed boundary condition without its field data");
+  const double* eg = has("boundary_heGradient") ? d("boundary_heGradient") : nullptr;
+#pragma omp parallel for schedule(static)
   for (int b = 0; b < m.B; ++b) {
     int t = type[m.slot_patch[b]];
     int c = m.bfc[b];
     if (is_mixed(t)) {
-      if (!mx) throw std::runtime_error("oracle: mixed boundary condition without its field data");
       double f, ref;
       mix_vf_ref(t, *mx, b, m.B, comp, f, ref);
       bvf[b] = f * ref + (1.0 - f) * vf[c];
     } else if (t == ZG || t == EXTRAP) bvf[b] = vf[c];
     else if (t == CYCLIC) bvf[b] = interp_b(m.bw[b], vf[c], vf[m.partner_cell[b]]);
     else if (is_proc(t) && !m.primary[b]) bvf[b] = vf[c];
-    else if (t == GRAD_E && has("boundary_heGradient"))   // dfMatrixOpBase.cu:351-366
-      bvf[b] = vf[c] + d("boundary_heGradient")[b] / m.bdc[b];
+    else if (t == GRAD_E && eg)   // dfMatrixOpBase.cu:351-366
+      bvf[b] = vf[c] + eg[b] / m.bdc[b];
   }
 }
 void correct_bc_vec(const M& m, const int* type, const double* vf, double* bvf, int ncomp, const Mix* mx = nullptr) {
@@ -203,6 +249,7 @@ void rho_eqn(const M& m) {
   const int* trho = ia("ptype_rho");
   double *rho = d("rho"), *rho_old = d("rho_old"), *phi = d("phi"), *bphi = d("boundary_phi"), *brho = d("boundary_rho");
   auto div = integrate(m, trho, [&](int f) { return phi[f]; }, [&](int b, int, int) { return bphi[b]; });
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < m.C; ++c) {
     double diag = m.rdt * m.V[c];                            // EulerDdtScheme::fvmDdt(vf)
     double src = m.rdt * rho_old[c] * m.V[c];
@@ -219,9 +266,11 @@ void grad_scalar(const M& m, const int* type, const double* vf, const double* bv
   for (int k = 0; k < 3; ++k) {
     auto s = integrate(m, type, [&](int f) { return m.sf(k, f) * interp_f(m.w[f], vf[m.own[f]], vf[m.nei[f]]); },
                        [&](int b, int t, int c) { return m.bsf(k, b) * bface(m, t, vf, bvf, b, c); });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < m.C; ++c) g[(long)k * m.C + c] = s[c] / m.V[c];
   }
   if (!bg) return;
+  #pragma omp parallel for schedule(static)
   for (int b = 0; b < m.B; ++b) {
     int t = type[m.slot_patch[b]];
     if (t == EMPTY) continue;
@@ -256,12 +305,16 @@ void u_eqn_assemble(const M& m) {
   double *rAU = d("rAU"), *brAU = d("boundary_rAU");
   // fvm::div(phi,U), Gauss linear (gaussConvectionScheme::fvmDiv; dfMatrixOpBase.cu:741-781)
   std::vector<double> L1(F), U1(F), UL(F);
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { L1[f] = -m.w[f] * phi[f]; U1[f] = L1[f] + phi[f]; }
   auto d1 = neg_sum_diag(m, L1.data(), U1.data());
   // fvm::laplacian(mu,U) (gaussLaplacianScheme; :783-810); symmetric
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) UL[f] = m.dc[f] * (interp_f(m.w[f], mu[m.own[f]], mu[m.nei[f]]) * m.magSf[f]);
   auto dL = neg_sum_diag(m, UL.data(), UL.data());
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { lower[f] = L1[f] + (-UL[f]); upper[f] = U1[f] + (-UL[f]); }
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) diag[c] = (m.rdt * rho[c] * m.V[c] + d1[c]) + (-dL[c]);
   std::fill(ic, ic + 3L * B, 0.0); std::fill(bc, bc + 3L * B, 0.0);
   const Mix mxU = mix_for("U");
@@ -280,8 +333,10 @@ void u_eqn_assemble(const M& m) {
     auto s = integrate(m, tU,
         [&](int f) { return m.sf(i, f) * interp_f(m.w[f], U[(long)j * C + m.own[f]], U[(long)j * C + m.nei[f]]); },
         [&](int b, int t, int c) { return m.bsf(i, b) * bface(m, t, U + (long)j * C, bU + (long)j * B, b, c); });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) g[(long)(i * 3 + j) * C + c] = s[c] / m.V[c];
   }
+  #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) {                           // boundary gradient, non-coupled only (:1239-1327)
     int t = tU[m.slot_patch[b]];
     if (t == EMPTY || is_coupled(t)) continue;
@@ -300,12 +355,14 @@ void u_eqn_assemble(const M& m) {
     o[3] = sc * v[1]; o[4] = sc * (v[4] - tr); o[5] = sc * v[7];
     o[6] = sc * v[2]; o[7] = sc * v[5]; o[8] = sc * (v[8] - tr);
   };
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) {
     double v[9], o[9];
     for (int k = 0; k < 9; ++k) v[k] = g[(long)k * C + c];
     dev2T(mu[c], v, o);
     for (int k = 0; k < 9; ++k) T[(long)k * C + c] = o[k];
   }
+  #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) {
     double v[9], o[9];
     for (int k = 0; k < 9; ++k) v[k] = bg[(long)k * B + b];
@@ -330,16 +387,20 @@ void u_eqn_assemble(const M& m) {
   if (has("out_gradU")) std::copy(g.begin(), g.end(), d("out_gradU"));
   // source: ddt + divDevRhoReff explicit part
   for (int k = 0; k < 3; ++k)
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) src[(long)k * C + c] = m.rdt * rho_old[c] * U_old[(long)k * C + c] * m.V[c] + divT[k][c];
   // UEqn == -fvc::grad(p)
   for (int k = 0; k < 3; ++k) {
     auto gp = integrate(m, tp, [&](int f) { return m.sf(k, f) * interp_f(m.w[f], p[m.own[f]], p[m.nei[f]]); },
                         [&](int b, int t, int c) { return m.bsf(k, b) * bface(m, t, p, bp, b, c); });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) srcs[(long)k * C + c] = src[(long)k * C + c] - gp[c];
   }
   // rAU = 1/UEqn.A() (fvMatrix::D + addCmptAvBoundaryDiag; dfUEqn.cu:721-738)
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) rAU[c] = diag[c];
   for_slots(m, tU, [&](int b, int, int c) { rAU[c] += (ic[b] + ic[(long)B + b] + ic[2L * B + b]) / 3; });
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) rAU[c] = 1 / (rAU[c] / m.V[c]);
   correct_bc_scalar(m, textr, rAU, brAU);
 }
@@ -357,22 +418,25 @@ void u_hbya(const M& m) {
     const double* Uk = U + (long)k * C;
     std::vector<double> bd(C, 0.0), Hl(C, 0.0);
     for_slots(m, tU, [&](int b, int, int c) { bd[c] += ic[(long)k * B + b]; });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) bd[c] = -bd[c];
     for_slots(m, tU, [&](int b, int, int c) { bd[c] += (ic[b] + ic[(long)B + b] + ic[2L * B + b]) / 3; });
-    for (int f = 0; f < F; ++f) {                        // lduMatrix::H
-      Hl[m.nei[f]] -= lower[f] * Uk[m.own[f]];
-      Hl[m.own[f]] -= upper[f] * Uk[m.nei[f]];
-    }
+    gather(m, Hl.data(), [&](double a, int f) { return a - upper[f] * Uk[m.nei[f]]; },   // lduMatrix::H
+           [&](double a, int f) { return a - lower[f] * Uk[m.own[f]]; });
     double* Hk = H + (long)k * C;
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) Hk[c] = bd[c] * Uk[c] + (Hl[c] + src[(long)k * C + c]);
     for_slots(m, tU, [&](int b, int t, int c) {         // addBoundarySource
       Hk[c] += is_coupled(t) ? bc[(long)k * B + b] * nbr(m, Uk, bU + (long)k * B, b) : bc[(long)k * B + b];
     });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) Hk[c] = Hk[c] / m.V[c];
   }
   correct_bc_vec(m, textr, H, bH, 3);
   for (int k = 0; k < 3; ++k) {
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) H[(long)k * C + c] = rAU[c] * H[(long)k * C + c];
+    #pragma omp parallel for schedule(static)
     for (int b = 0; b < B; ++b) {
       int t = tU[m.slot_patch[b]];
       bH[(long)k * B + b] = brAU[b] * bH[(long)k * B + b];
@@ -397,8 +461,10 @@ void p_eqn_assemble(const M& m) {
   const double small_ = 1e-15;    // OpenFOAM 'small' in ddtScheme::fvcDdtPhiCoeff
   // rhorAUf = fvc::interpolate(rho*rAU)
   std::vector<double> rr(C), rUo(3L * C);
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) rr[c] = rho[c] * rAU[c];
   for (int k = 0; k < 3; ++k) for (int c = 0; c < C; ++c) rUo[(long)k * C + c] = rho_old[c] * U_old[(long)k * C + c];
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) rf[f] = interp_f(m.w[f], rr[m.own[f]], rr[m.nei[f]]);
   std::fill(brf, brf + B, 0.0); std::fill(bph, bph + B, 0.0);
   for_slots(m, tp, [&](int b, int t, int c) {
@@ -406,6 +472,7 @@ void p_eqn_assemble(const M& m) {
                            : brho[b] * brAU[b];
   });
   // phiHbyA = interpolate(rho)*flux(HbyA) + rhorAUf*ddtCorr(rho, U, phi) (EulerDdtScheme::fvcDdtPhiCorr)
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) {
     int o = m.own[f], n = m.nei[f];
     double w = m.w[f];
@@ -435,9 +502,11 @@ void p_eqn_assemble(const M& m) {
   });
   // fvm::laplacian(rhorAUf, p), symmetric
   std::vector<double> UL(F);
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) UL[f] = m.dc[f] * (rf[f] * m.magSf[f]);
   auto dL = neg_sum_diag(m, UL.data(), UL.data());
   auto div = integrate(m, tp, [&](int f) { return ph[f]; }, [&](int b, int, int) { return bph[b]; });
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) {
     // psi*correction(fvm::ddt(p)) (correct_diag_mtx_multi_tpsi_kernel, dfpEqn.cu:258)
     double dg = m.rdt * m.V[c];
@@ -451,6 +520,7 @@ void p_eqn_assemble(const M& m) {
     src[c] = sr;
     diag[c] = dg - dL[c];                                   // - fvm::laplacian
   }
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { lower[f] = -UL[f]; upper[f] = -UL[f]; }
   std::fill(ic, ic + B, 0.0); std::fill(bc, bc + B, 0.0);
   const Mix mxP = mix_for("p");
@@ -482,6 +552,7 @@ void p_eqn_post(const M& m) {
   double *phi = d("phi"), *bphi = d("boundary_phi"), *U = d("U"), *bU = d("boundary_U");
   double *H = d("HbyA"), *rAU = d("rAU"), *K = d("K"), *bK = d("boundary_K"), *dpdt = d("dpdt");
   { const Mix mx = mix_for("p"); correct_bc_scalar(m, tp, p, bp, &mx); }
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) phi[f] = ph[f] + (upper[f] * p[m.nei[f]] - lower[f] * p[m.own[f]]);  // lduMatrix::faceH
   for_slots(m, tp, [&](int b, int t, int c) {              // fvMatrix::flux boundary
     double fl = is_coupled(t) ? ic[b] * p[c] - bc[b] * nbr(m, p, bp, b) : ic[b] * p[c] - bc[b];
@@ -490,10 +561,14 @@ void p_eqn_post(const M& m) {
   std::vector<double> g(3L * C);
   grad_scalar(m, tp, p, bp, g.data(), nullptr);
   for (int k = 0; k < 3; ++k)
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) U[(long)k * C + c] = H[(long)k * C + c] - rAU[c] * g[(long)k * C + c];
   { const Mix mx = mix_for("U"); correct_bc_vec(m, tU, U, bU, 3, &mx); }
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) K[c] = 0.5 * (U[c] * U[c] + U[(long)C + c] * U[(long)C + c] + U[2L * C + c] * U[2L * C + c]);
+  #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) bK[b] = 0.5 * (bU[b] * bU[b] + bU[(long)B + b] * bU[(long)B + b] + bU[2L * B + b] * bU[2L * B + b]);
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) dpdt[c] = m.rdt * (p[c] - p_old[c]);
 }
 
@@ -510,6 +585,7 @@ void y_prep(const M& m) {
   if (has("out_gradY")) std::copy(g.begin(), g.end(), d("out_gradY"));
   // sumYDiffError = sum_i rhoD_i*grad(Y_i); boundary field = product of boundary fields
   auto fold_sum = [&](int n, const double* rd, const double* gy, double* se) {
+    #pragma omp parallel for collapse(2) schedule(static)
     for (int k = 0; k < 3; ++k) for (int i = 0; i < n; ++i) {
       double a = 0.0;
       for (int s = 0; s < S; ++s) a += rd[(long)s * n + i] * gy[(long)n * s * 3 + (long)n * k + i];
@@ -520,6 +596,7 @@ void y_prep(const M& m) {
   fold_sum(B, brhoD, bg.data(), bsumE);
   // hDiffCorrFlux = sum_i hai_i*(rhoD_i*grad(Y_i) - Y_i*sumYDiffError)
   auto fold_h = [&](int n, const double* ha, const double* rd, const double* y, const double* gy, const double* se, double* hd) {
+    #pragma omp parallel for collapse(2) schedule(static)
     for (int k = 0; k < 3; ++k) for (int i = 0; i < n; ++i) {
       double a = 0.0;
       for (int s = 0; s < S; ++s) {
@@ -536,6 +613,7 @@ void y_prep(const M& m) {
   std::vector<double> ah(C);
   for (int s = 0; s < S; ++s) {
     const double *y = Y + (long)s * C, *by = bY + (long)s * B, *hs = hai + (long)s * C, *bhs = bhai + (long)s * B;
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) ah[c] = alpha[c] * hs[c];
     auto lap = integrate(m, tY,
         [&](int f) { int o = m.own[f], n = m.nei[f];
@@ -547,6 +625,7 @@ void y_prep(const M& m) {
           }
           double sng = (t == FV || t == CALC || t == FIX_E || is_mixed(t)) ? m.bdc[b] * (by[b] - y[c]) : 0.0;
           return balpha[b] * bhs[b] * m.bmagSf[b] * sng; });
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) dAD[c] = dAD[c] + lap[c] / m.V[c];
   }
 }
@@ -563,6 +642,7 @@ void y_assemble(const M& m) {
   double *lo = d("out_lower"), *up = d("out_upper"), *dg = d("out_diag"), *sr = d("out_source");
   double *icA = d("out_internal_coeffs"), *bcA = d("out_boundary_coeffs");
   std::vector<double> phiUc(F), bphiUc(B, 0.0);
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) {
     int o = m.own[f], n = m.nei[f];
     double w = m.w[f];
@@ -579,6 +659,7 @@ void y_assemble(const M& m) {
   if (has("out_phiUc")) { std::copy(phiUc.begin(), phiUc.end(), d("out_phiUc")); std::copy(bphiUc.begin(), bphiUc.end(), d("out_boundary_phiUc")); }
   // multivariate Gauss upwind: weights pos0(phi) for both fluxes
   std::vector<double> L1(F), U1(F), L2(F), U2(F), UL(F);
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) {
     double w = phi[f] >= 0 ? 1.0 : 0.0;
     L1[f] = -w * phi[f]; U1[f] = L1[f] + phi[f];
@@ -593,12 +674,15 @@ void y_assemble(const M& m) {
   for (int s = 0; s < S; ++s) {
     if (s == inert) continue;
     const double *rd = rhoD + (long)s * C, *brd = brhoD + (long)s * B, *y = Y + (long)s * C, *by = bY + (long)s * B;
+    #pragma omp parallel for schedule(static)
     for (int f = 0; f < F; ++f) UL[f] = m.dc[f] * (interp_f(m.w[f], rd[m.own[f]], rd[m.nei[f]]) * m.magSf[f]);
     auto dL = neg_sum_diag(m, UL.data(), UL.data());
+    #pragma omp parallel for schedule(static)
     for (int f = 0; f < F; ++f) {
       lo[(long)s * F + f] = (L1[f] + L2[f]) - UL[f];
       up[(long)s * F + f] = (U1[f] + U2[f]) - UL[f];
     }
+    #pragma omp parallel for schedule(static)
     for (int c = 0; c < C; ++c) {
       dg[(long)s * C + c] = (m.rdt * rho[c] * m.V[c] + (d1[c] + d2[c])) - dL[c];
       sr[(long)s * C + c] = m.rdt * rho_old[c] * y[c] * m.V[c] + m.V[c] * RR[(long)s * C + c];
@@ -620,6 +704,7 @@ void y_inert(const M& m) {
   const int inert = ia("inert_index")[0];
   const int* tY = ia("ptype_Y");
   double *Y = d("Y"), *bY = d("boundary_Y");
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < m.C; ++c) {
     double sum = 0;
     for (int s = 0; s < m.S; ++s) {
@@ -649,8 +734,10 @@ void e_assemble(const M& m) {
   double *ic = d("out_internal_coeffs"), *bc = d("out_boundary_coeffs");
   const double* egrad = has("boundary_heGradient") ? d("boundary_heGradient") : nullptr;
   std::vector<double> L1(F), U1(F), UL(F);
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { double w = phi[f] >= 0 ? 1.0 : 0.0; L1[f] = -w * phi[f]; U1[f] = L1[f] + phi[f]; }
   auto d1 = neg_sum_diag(m, L1.data(), U1.data());
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) UL[f] = m.dc[f] * (interp_f(m.w[f], alpha[m.own[f]], alpha[m.nei[f]]) * m.magSf[f]);
   auto dL = neg_sum_diag(m, UL.data(), UL.data());
   auto divK = integrate(m, tK, [&](int f) { return phi[f] * interp_f(m.w[f], K[m.own[f]], K[m.nei[f]]); },
@@ -663,7 +750,9 @@ void e_assemble(const M& m) {
         double h[3];
         for (int k = 0; k < 3; ++k) h[k] = bface(m, t, hD + (long)k * C, bhD + (long)k * B, b, c);
         return m.bsf(0, b) * h[0] + m.bsf(1, b) * h[1] + m.bsf(2, b) * h[2]; });
+  #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { lower[f] = L1[f] - UL[f]; upper[f] = U1[f] - UL[f]; }
+  #pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c) {
     double V = m.V[c];
     diag[c] = (m.rdt * rho[c] * V + d1[c]) - dL[c];
@@ -787,6 +876,7 @@ void thermo_point(const Thermo& th, bool fixT, double& T, double& he, double p, 
 void energy_gradient(const M& m) {
   const int* the = ia("ptype_he");
   double *T = d("T"), *Y = d("Y"), *bY = d("boundary_Y"), *eg = d("boundary_heGradient");
+  #pragma omp parallel for schedule(static)
   for (int b = 0; b < m.B; ++b) {
     eg[b] = 0.0;
     if (the[m.slot_patch[b]] != GRAD_E) continue;
@@ -805,8 +895,10 @@ void thermo_correct(const M& m, bool from_T) {
   double *bT = d("boundary_T"), *bhe = d("boundary_he"), *bp = d("boundary_p"), *bY = d("boundary_Y"),
          *bpsi = d("boundary_psi"), *brho = d("boundary_rho"), *bmu = d("boundary_mu"), *balpha = d("boundary_alpha"),
          *brhoD = d("boundary_rhoD"), *bhai = d("boundary_hai");
+#pragma omp parallel for schedule(static)
   for (int c = 0; c < C; ++c)
     thermo_point(g_th, from_T, T[c], he[c], p[c], Y + c, C, psi[c], rho[c], mu[c], alpha[c], rhoD + c, hai + c, C);
+#pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) {
     int t = tT[m.slot_patch[b]];
     if (t == EMPTY) continue;
@@ -868,6 +960,7 @@ int orc_grad_scalar(const char* field, const char* bfield, const char* ptype, co
 int orc_thermo_points(int n, int fixT, double* T, double* he, const double* p, const double* Y, double* psi, double* rho,
                       double* mu, double* alpha, double* rhoD, double* hai) {
   try {
+#pragma omp parallel for schedule(static)
     for (int c = 0; c < n; ++c)
       thermo_point(g_th, fixT != 0, T[c], he[c], p[c], Y + c, n, psi[c], rho[c], mu[c], alpha[c], rhoD + c, hai + c, n);
     return 0;
