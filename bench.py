@@ -12,8 +12,8 @@ cells), processor-patch halos and solver reductions go over RCCL (xGMI).
 
 Output: one JSON line (rank 0) with the driver's contract fields plus
   roofline      -- the dominant kernel's algorithmic bytes / its mean HIP-event duration,
-  cpu_baseline  -- the CPU oracle (sequential C++ restatement + direct sparse solves) timed on
-                   a bounded sample of the same workload on this host.
+  cpu_baseline  -- CPU-A: the OpenMP C++ implementation of the same step behind the same C ABI
+                   (baseline/cpu_a), timed on this host's cores on the same 128^3 workload.
 """
 from __future__ import annotations
 
@@ -110,55 +110,64 @@ def parse():
                          "storage its gathers are contiguous runs and it measured fastest), 8x8x4 bricks on a Z-order "
                          "curve, plain Morton, or reverse Cuthill-McKee")
     ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
-    ap.add_argument("--cpu-n", type=int, default=16, help="cells per direction of the CPU baseline sample")
+    ap.add_argument("--cpu-n", type=int, default=128, help="cells per direction of the CPU-A baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=2, help="timed outer iterations of the CPU-A baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-flame", action="store_true", help="skip the BASELINE config 2 (1D flame) side line")
     return ap.parse_args()
 
 
+def host_cpu():
+    """(usable cores, machine cores, CPU model string) of this host (the lscpu 'Model name' field)"""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return len(os.sched_getaffinity(0)), os.cpu_count(), model
+
+
 def cpu_baseline(args, table, ym, inert):
-    """The oracle (TEST INFRASTRUCTURE, the checker) timed on a bounded sample on the host, 1 core:
-    the flow part on a cpu_n^3 box (sequential C++ restatement + exact sparse solves), plus -- when the
-    GPU step integrates chemistry -- the oracle's per-cell chemistry (SciPy BDF, the reference's
-    CVODE tolerances) timed on cells sampled from the same initial state; cell-updates/s =
-    1 / (flow seconds per cell + chemistry seconds per cell)."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    """CPU-A: the build's OpenMP C++ implementation of the same step behind the
+    same C ABI (baseline/cpu_a/libdfmi_cpu_a.so: the oracle's FV/thermo restatement with parallel gathers,
+    Jacobi-BiCGStab and AMG-PCG at the GPU path's tolerances, ROS3 chemistry with the compiled-in
+    kinetics), on every core OpenMP is given on this host (OMP_NUM_THREADS), on the headline's own
+    workload: the cpu_n^3 box (default 128^3 = config 3) with the same initial state and chemistry.
+    Bounded sample: one untimed step, then --cpu-steps timed steps."""
+    from dfmi.lib import Context
+    from dfmi.kinetics import parse_mechanism
     from dfmi.mesh import hex_box
     from dfmi import case
+    path = os.path.join(ROOT, "baseline", "cpu_a", "libdfmi_cpu_a.so")
     n = args.cpu_n
-    m = hex_box(n, n, n)
-    pt = case.default_patch_types(m)
-    f = reference_fields(m, ym["species"]) if args.init == "reference" else case.tgv_fields(m, ym["species"])
-    st = host_state(m, table, f)
-    o = O.Oracle(m, table, st, pt, inert, 1.0 / args.dt)
-    t0 = time.perf_counter()
-    steps = 0
-    while True:
-        o.time_step(args.ncorr)
-        steps += 1
-        if time.perf_counter() - t0 > 10.0 or steps >= 5:
-            break
-    el = time.perf_counter() - t0
-    flow_s_per_cell = el / (m.n_cells * steps)
-    sample = (f"flow: oracle/df_oracle.cpp (sequential C++ restatement) + scipy spsolve, {n}^3 = {m.n_cells} cells "
-              f"periodic TGV, {table.S} species, {steps} outer iterations in {el:.1f} s")
-    chem_s_per_cell = 0.0
+    L = 2 * 3.141592653589793e-3
+    m = hex_box(n, n, n, lengths=(L, L, L))
+    ctx = Context(0, lib_path=path)
+    case.setup_context(ctx, m, table, inert, args.dt)
     if args.chem == "ode":
-        from chem_oracle import Kinetics
-        from dfmi.kinetics import parse_mechanism
-        yml = MECHS[args.mech][0]
-        kin = Kinetics(parse_mechanism(os.path.join(ROOT, "tests", "golden", yml)), ym["nasa"], ym["W"])
-        rng = np.random.default_rng(0)
-        idx = rng.choice(m.n_cells, 24, replace=False)
-        t1 = time.perf_counter()
-        kin.reaction_rates(st["T"][idx], st["p"][idx], st["rho"][idx], st["Y"][:, idx], args.dt, rtol=1e-6, atol=1e-10)
-        chem_s_per_cell = (time.perf_counter() - t1) / idx.size
-        sample += (f"; chemistry: oracle/chem_oracle.py SciPy BDF (rtol 1e-6, atol 1e-10) on {idx.size} sampled cells, "
-                   f"{chem_s_per_cell * 1e3:.2f} ms/cell")
-    return {"value": 1.0 / (flow_s_per_cell + chem_s_per_cell), "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": sample}
+        ctx.chem_set_mechanism(parse_mechanism(os.path.join(ROOT, "tests", "golden", MECHS[args.mech][0])))
+        ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    f = reference_fields(m, ym["species"]) if args.init == "reference" else case.tgv_fields(m, ym["species"])
+    case.init_state(ctx, m, table.S, f["T"], f["p"], f["U"], f["Y"])
+    ctx.time_step(args.ncorr)                      # untimed: first-touch allocations, chemistry step sizes
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        ctx.time_step(args.ncorr)
+    el = time.perf_counter() - t0
+    threads = int(ctx.lib.dfmi_version().decode().split("(OpenMP, ")[1].split(" ")[0])
+    iters = {e: ctx.solver_stats(e)[0] for e in ("U", "Y", "E", "p")}
+    ctx.close()
+    usable, machine, model = host_cpu()
+    chem = "ROS3 chemistry (rtol 1e-6, atol 1e-10)" if args.chem == "ode" else "no chemistry"
+    return {"value": m.n_cells * args.cpu_steps / el, "unit": "cell-updates/s", "cores": threads, "kind": "CPU-A",
+            "sample": f"baseline/cpu_a (OpenMP C++, fp64, same ABI and step) on {n}^3 = {m.n_cells} cells, "
+                      f"{table.S} species, {chem}, {args.cpu_steps} timed outer iterations in {el:.1f} s after "
+                      f"1 untimed; last-step solver iterations {iters}",
+            "host": {"omp_threads": threads, "affinity_cpus": usable, "nproc": machine, "model": model}}
 
 
 def reference_fields(m, species):

@@ -20,6 +20,7 @@
 // products and solution stay fp64 -- which halves the preconditioner's bytes per iteration.
 #include "dfmi_ctx.h"
 #include "amg.h"
+#include "amg_graph.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -178,148 +179,19 @@ __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __re
 }
 
 // ---------------------------------------------------------------- host: hierarchy
-struct Graph {                  // symmetric strength graph, CSR, no self entries
-  int n = 0;
-  std::vector<int> start, adj;
-  std::vector<double> w;
-};
-
-// one greedy pairwise matching on g: each unmatched vertex (in index order) pairs with its
-// strongest unmatched neighbour (ties: lowest index). Returns group id per vertex, group count.
-int pair_match(const Graph& g, std::vector<int>& grp) {
-  grp.assign(g.n, -1);
-  int ng = 0;
-  for (int v = 0; v < g.n; ++v) {
-    if (grp[v] >= 0) continue;
-    int best = -1;
-    double bw = -1.0;
-    for (int e = g.start[v]; e < g.start[v + 1]; ++e) {
-      const int u = g.adj[e];
-      if (u == v || grp[u] >= 0) continue;
-      // strengths within 1e-9 relative are ties (rounding must not break the geometric pattern)
-      if (g.w[e] > bw * (1 + 1e-9)) { bw = g.w[e]; best = u; }
-      else if (std::fabs(g.w[e] - bw) <= 1e-9 * bw && u < best) best = u;
-    }
-    grp[v] = ng;
-    if (best >= 0) grp[best] = ng;
-    ++ng;
-  }
-  return ng;
-}
-
-// collapse g by a grouping (edge strengths summed, intra-group edges dropped)
-Graph collapse(const Graph& g, const std::vector<int>& grp, int ng) {
-  std::vector<std::vector<std::pair<int, double>>> e(ng);
-  for (int v = 0; v < g.n; ++v)
-    for (int k = g.start[v]; k < g.start[v + 1]; ++k) {
-      const int a = grp[v], b = grp[g.adj[k]];
-      if (a != b) e[a].push_back({b, g.w[k]});
-    }
-  Graph c;
-  c.n = ng;
-  c.start.assign(ng + 1, 0);
-  for (int a = 0; a < ng; ++a) {
-    auto& l = e[a];
-    std::sort(l.begin(), l.end(), [](auto& x, auto& y) { return x.first < y.first; });
-    std::vector<std::pair<int, double>> m;
-    for (auto& p : l) {
-      if (!m.empty() && m.back().first == p.first) m.back().second += p.second;
-      else m.push_back(p);
-    }
-    for (auto& p : m) { c.adj.push_back(p.first); c.w.push_back(p.second); }
-    c.start[a + 1] = (int)c.adj.size();
-  }
-  return c;
-}
-
-// Build the next level from level `f` (ELL cols [Wf][nf], strength graph g). Fills f's agg/members
-// and galerkin maps, returns the coarse level's ELL structure and strength graph.
+// (aggregation in amg_graph.h, shared with the CPU-A baseline; here the result is uploaded)
 void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLevel& c, std::vector<int>& ccol,
                 Graph& cg, hipStream_t st) {
-  const int nf = f.n, Wf = f.W;
-  // three pairwise passes -> aggregates of up to 8
-  std::vector<int> agg(nf);
-  std::iota(agg.begin(), agg.end(), 0);
-  Graph cur = g;
-  int ng = nf;
-  for (int pass = 0; pass < 3; ++pass) {
-    std::vector<int> grp;
-    ng = pair_match(cur, grp);
-    for (int v = 0; v < nf; ++v) agg[v] = grp[agg[v]];
-    cur = collapse(cur, grp, ng);
-  }
-  // renumber coarse cells by their first fine member (locality)
-  std::vector<int> first(ng, INT32_MAX);
-  for (int v = 0; v < nf; ++v) first[agg[v]] = std::min(first[agg[v]], v);
-  std::vector<int> ord(ng);
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return first[a] < first[b]; });
-  std::vector<int> ren(ng);
-  for (int i = 0; i < ng; ++i) ren[ord[i]] = i;
-  for (int v = 0; v < nf; ++v) agg[v] = ren[agg[v]];
-  const int nc = ng;
-  // coarse strength graph (same collapse, renumbered)
-  cg = collapse(g, agg, nc);
-  // members
-  std::vector<int> mstart(nc + 1, 0), members(nf);
-  for (int v = 0; v < nf; ++v) mstart[agg[v] + 1]++;
-  for (int i = 0; i < nc; ++i) mstart[i + 1] += mstart[i];
-  {
-    std::vector<int> pos(mstart.begin(), mstart.end() - 1);
-    for (int v = 0; v < nf; ++v) members[pos[agg[v]]++] = v;
-  }
-  // coarse ELL columns: sorted unique neighbour aggregates over rank-local fine couplings
-  std::vector<std::vector<int>> nb(nc);
-  for (int v = 0; v < nf; ++v)
-    for (int k = 0; k < Wf; ++k) {
-      const int j = fcol[(size_t)k * nf + v];
-      if (j >= nf || j == v) continue;    // halo or padding
-      const int A = agg[v], Bc = agg[j];
-      if (A != Bc) nb[A].push_back(Bc);
-    }
-  int Wc = 1;
-  for (auto& l : nb) {
-    std::sort(l.begin(), l.end());
-    l.erase(std::unique(l.begin(), l.end()), l.end());
-    Wc = std::max(Wc, (int)l.size());
-  }
-  ccol.assign((size_t)Wc * nc, 0);
-  for (int I = 0; I < nc; ++I)
-    for (int k = 0; k < Wc; ++k) ccol[(size_t)k * nc + I] = k < (int)nb[I].size() ? nb[I][k] : I;
-  // Galerkin contribution lists: slot k < Wc -> coarse entry (I, nb[I][k]); slot Wc -> diagonal.
-  // Fine sources in (member ascending, fine slot ascending) order; fine diag first per member.
-  const int slots = Wc + 1;
-  std::vector<std::vector<int>> lists((size_t)slots * nc);
-  for (int I = 0; I < nc; ++I) {
-    for (int e = mstart[I]; e < mstart[I + 1]; ++e) {
-      const int v = members[e];
-      lists[(size_t)Wc * nc + I].push_back(-(v + 1));
-      for (int k = 0; k < Wf; ++k) {
-        const int j = fcol[(size_t)k * nf + v];
-        if (j >= nf || j == v) continue;
-        const int src = k * nf + v;
-        const int Bc = agg[j];
-        if (Bc == I) lists[(size_t)Wc * nc + I].push_back(src);
-        else {
-          const int kk = (int)(std::lower_bound(nb[I].begin(), nb[I].end(), Bc) - nb[I].begin());
-          lists[(size_t)kk * nc + I].push_back(src);
-        }
-      }
-    }
-  }
-  std::vector<int> gstart((size_t)slots * nc + 1, 0), gsrc;
-  for (size_t s = 0; s < lists.size(); ++s) {
-    for (int v : lists[s]) gsrc.push_back(v);
-    gstart[s + 1] = (int)gsrc.size();
-  }
-  if (gsrc.empty()) gsrc.push_back(0);
-  f.agg.upload(agg, st);
-  f.mstart.upload(mstart, st);
-  f.members.upload(members, st);
-  f.gstart.upload(gstart, st);
-  f.gsrc.upload(gsrc, st);
-  c.n = nc;
-  c.W = Wc;
+  AmgCoarse k = amg_coarsen(fcol, f.W, f.n, g);
+  f.agg.upload(k.agg, st);
+  f.mstart.upload(k.mstart, st);
+  f.members.upload(k.members, st);
+  f.gstart.upload(k.gstart, st);
+  f.gsrc.upload(k.gsrc, st);
+  c.n = k.nc;
+  c.W = k.Wc;
+  ccol.swap(k.ccol);
+  cg = std::move(k.cg);
   c.col.upload(ccol, st);
 }
 
@@ -352,37 +224,20 @@ void amg_setup(Ctx& x) {
     DFMI_HIP(hipMemcpy(bmag.data(), x.bmagSf.p, x.B * sizeof(double), hipMemcpyDeviceToHost));
     DFMI_HIP(hipMemcpy(bdc.data(), x.bdc.p, x.B * sizeof(double), hipMemcpyDeviceToHost));
   }
-  Graph g;
-  g.n = C;
-  {
-    std::vector<std::vector<std::pair<int, double>>> e(C);
-    for (int f = 0; f < x.F; ++f) {
-      const double s = mag[x.h_fst[f]] * dcf[x.h_fst[f]];
-      e[x.h_own[f]].push_back({x.h_nei[f], s});
-      e[x.h_nei[f]].push_back({x.h_own[f], s});
-    }
-    for (int p = 0; p < x.P; ++p) {
-      if (x.pkind[p] != 1) continue;
-      const int q = x.cyc_nbr[p];
-      for (int i = 0; i < x.psize[p]; ++i) {
-        const int b = x.poff[p] + i;
-        const int c = x.h_bfc[b], o = x.h_bfc[x.poff[q] + i];
-        if (c != o) e[c].push_back({o, bmag[b] * bdc[b]});
-      }
-    }
-    g.start.assign(C + 1, 0);
-    for (int c = 0; c < C; ++c) {
-      auto& l = e[c];
-      std::sort(l.begin(), l.end(), [](auto& u, auto& v) { return u.first < v.first; });
-      std::vector<std::pair<int, double>> m;
-      for (auto& p : l) {
-        if (!m.empty() && m.back().first == p.first) m.back().second += p.second;
-        else m.push_back(p);
-      }
-      for (auto& p : m) { g.adj.push_back(p.first); g.w.push_back(p.second); }
-      g.start[c + 1] = (int)g.adj.size();
+  std::vector<int> fo(x.F), fn(x.F);
+  std::vector<double> fs(x.F);
+  for (int f = 0; f < x.F; ++f) { fo[f] = x.h_own[f]; fn[f] = x.h_nei[f]; fs[f] = mag[x.h_fst[f]] * dcf[x.h_fst[f]]; }
+  std::vector<int> co, cn;
+  std::vector<double> cs;
+  for (int p = 0; p < x.P; ++p) {
+    if (x.pkind[p] != 1) continue;
+    const int q = x.cyc_nbr[p];
+    for (int i = 0; i < x.psize[p]; ++i) {
+      const int b = x.poff[p] + i;
+      co.push_back(x.h_bfc[b]); cn.push_back(x.h_bfc[x.poff[q] + i]); cs.push_back(bmag[b] * bdc[b]);
     }
   }
+  Graph g = strength_graph(C, fo, fn, fs, co, cn, cs);
   a.lv.emplace_back();
   a.lv[0].n = C;
   a.lv[0].W = x.ell.W;

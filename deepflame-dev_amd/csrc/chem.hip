@@ -493,6 +493,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 // ---- generated fast path: the mechanism compiled in (dfmi/chem_codegen.py), state in registers
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wunused-variable"
+#define DFMI_HD __device__   // the generated kinetics are plain C++; here they run on the device
 #include "chem_gen_burke9.inc"
 #include "chem_gen_es80.inc"
 #pragma clang diagnostic pop

@@ -12,17 +12,20 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdfmi.so")
 
-_lib = None
+_libs = {}
 
 
-def load() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"libdfmi.so not found at {LIB_PATH}; run __graft_entry__.build()")
-        _lib = C.CDLL(LIB_PATH)
-        _declare(_lib)
-    return _lib
+def load(path: str | None = None) -> C.CDLL:
+    """the HIP library (default), or another implementation of include/dfmi.h given by path (the CPU-A
+    baseline, baseline/cpu_a/libdfmi_cpu_a.so, which only bench.py's cpu_baseline leg and its tests use)"""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError(f"{os.path.basename(path)} not found at {path}; run __graft_entry__.build()")
+        lib = C.CDLL(path)
+        _declare(lib)
+        _libs[path] = lib
+    return _libs[path]
 
 
 _P = C.c_void_p
@@ -149,8 +152,8 @@ def _i32(a):
 class Context:
     """One device-resident database (one rank, one GPU)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load()
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self.lib = load(lib_path)
         h = _P()
         self._keep = []
         self._call("dfmi_create", C.byref(h), device)
