@@ -440,6 +440,8 @@ def main():
     T0, p0 = f["T"].copy(), f["p"].copy()
     del f
 
+    for e in ("U", "Y", "E", "p"):
+        ctx.solver_work(e, reset=True)             # work counts of the whole run (profiles/: frac from rocprof)
     for _ in range(args.warmup):
         ctx.time_step(args.ncorr)
     ctx.sync()
@@ -466,8 +468,7 @@ def main():
     # solver work counted on the device (after the headline, so the instrumentation never inflates it)
     extra = {"ode": ["k_chem", "k_bin"], "dnn": ["k_mlp_gemm"], "off": []}[args.chem]
     ctx.kernel_timer(",".join(ROOF_KERNELS + tuple(extra)))
-    for e in ("U", "Y", "E", "p"):
-        ctx.solver_work(e, reset=True)
+    work_pre = {e: ctx.solver_work(e, reset=True) for e in ("U", "Y", "E", "p")}
     if args.chem == "dnn":
         ctx.dnn_stats()
     for _ in range(args.roof_steps):
@@ -553,6 +554,14 @@ def main():
                                                "launches")} for k, v in roofs.items()},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "solver_work_roof_pass": work,
+        "solver_work_run": {"system_iterations": {e: work_pre[e] + work[e] for e in work},
+                            "time_steps": args.warmup + args.steps + args.roof_steps,
+                            "note": "every solve of this process's time steps (warmup + timed + roof pass): with a "
+                                    "rocprofv3 --stats summary of the same command, frac = bytes_per_unit x units / "
+                                    "summed kernel time (scripts/roof_from_profile.py)",
+                            "bytes_per_unit": {k: algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots,
+                                                                    table.S, m.n_coupled_slots)
+                                               for k in ("k_bcg_spmv", "k_cg_spmv")}},
         "amg_levels": ctx.amg_info(),
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,

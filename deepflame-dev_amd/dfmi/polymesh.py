@@ -10,13 +10,15 @@ these arrays from OpenFOAM's fvMesh), computing the geometry the way OpenFOAM do
   * weights: surfaceInterpolation::makeWeights  w = |Sf.(Cn - Cf)| / (|Sf.(Cf - Co)| + |Sf.(Cn - Cf)|);
     deltaCoeffs 1 / |Cn - Co| (mesh.deltaCoeffs(), what createGPUSolver.H:338-339 passes);
   * non-coupled patches: w = 1, deltaCoeffs = 1 / |nf.(Cf - Co)| (fvPatch::delta, patch-normal);
-  * cyclic (translational): w = dn / (d + dn), deltaCoeffs = 1 / |delta - delta_nbr| with
-    d = nf.(Cf - Co) on each side (cyclicFvPatch::makeWeights / delta).
+  * cyclic (translational): w = dn / (d + dn) with d = nf.(Cf - Co) on each side
+    (cyclicFvPatch::makeWeights), deltaCoeffs = 1 / |(Cf - Co) - (Cf' - Cn')| (cyclicFvPatch::delta:
+    full vectors, coupledFvPatch::delta, not the patch-normal ones of fvPatch::delta).
 
 `hex_polymesh` + `write_polymesh` write the single-block hex box of `mesh.hex_box` as polyMesh files (faces
 in the same order, OpenFOAM orientation: internal normals owner -> neighbour, boundary normals outward), so
 a blockMesh-generated case and the in-process generator can be checked against each other. Text
-parsing only; serial meshes (decomposed processor directories are not read)."""
+parsing only; serial meshes here -- decomposed processor* directories are written and read by
+dfmi/partition.py."""
 from __future__ import annotations
 
 import gzip
@@ -175,24 +177,24 @@ def read_polymesh(directory: str) -> Mesh:
         sf = Sf[sl]
         mag = np.linalg.norm(sf, axis=1)
         nfv = sf / np.maximum(mag, 1e-300)[:, None]
-        delta = np.einsum("ij,ij->i", nfv, Cf[sl] - cc[fc])[:, None] * nfv   # patch-normal delta
-        geo.append((fc, sf, mag, nfv, delta))
+        delta = np.einsum("ij,ij->i", nfv, Cf[sl] - cc[fc])[:, None] * nfv   # patch-normal delta (fvPatch::delta)
+        geo.append((fc, sf, mag, nfv, delta, Cf[sl] - cc[fc]))
     for pi, (name, d) in enumerate(bnd):
         t = d["type"].strip()
         if t not in _KIND:
             raise ValueError(f"polyMesh patch {name}: type {t} not supported (serial meshes only)")
         kind = _KIND[t]
-        fc, sf, mag, nfv, delta = geo[pi]
+        fc, sf, mag, nfv, delta, dfull = geo[pi]
         if kind == "empty":
             patches.append(Patch(name, "empty", fc[:0].astype(np.int32), sf[:0], mag[:0], np.ones(0), np.ones(0)))
             continue
         if kind == "cyclic":
             q = names.index(d["neighbourPatch"].strip())
-            nd = geo[q][4]
             di = np.einsum("ij,ij->i", nfv, delta)
-            dni = np.einsum("ij,ij->i", geo[q][3], nd)
+            dni = np.einsum("ij,ij->i", geo[q][3], geo[q][4])
             wgt = dni / (di + dni)
-            dc = 1.0 / np.linalg.norm(delta - nd, axis=1)
+            # cyclicFvPatch::delta: the full own-side (Cf - C) minus the partner's (translational cyclic)
+            dc = 1.0 / np.linalg.norm(dfull - geo[q][5], axis=1)
             p = Patch(name, "cyclic", fc.astype(np.int32), sf, mag, wgt, dc)
             p.neighbour_patch = q
         else:

@@ -1,0 +1,36 @@
+"""Recompute the solver SpMV rooflines from committed profiles alone: a rocprofv3 --kernel-trace --stats
+summary (scripts/prof_summary.py output) and the bench JSON line of the SAME profiled command, whose
+"solver_work_run" holds the system-iterations of every solve in that process and the algorithmic bytes per
+unit. k_bcg_spmv: 2 SpMVs (spmv1 + spmv2 launches) per BiCGStab system-iteration; k_cg_spmv: 1 per PCG
+iteration. Usage: python scripts/roof_from_profile.py profiles/r02_kernel_stats.csv profiles/r02_bench_prof.json"""
+import csv
+import json
+import sys
+
+PEAK = 8000.0   # GB/s, MI355X HBM3E
+
+
+def main(stats_csv, bench_json):
+    rows = [r for r in csv.reader(l for l in open(stats_csv) if not l.startswith("#"))]
+    head, rows = rows[0], rows[1:]
+    ms = {}
+    for r in rows:
+        d = dict(zip(head, r))
+        name = d["kernel"].split("::")[-1]
+        fam = "k_bcg_spmv" if name.startswith("k_bcg_spmv") else ("k_cg_spmv" if name.startswith("k_cg_spmv") else None)
+        if fam:
+            ms[fam] = ms.get(fam, 0.0) + float(d["total_ms"])
+    b = json.loads([l for l in open(bench_json) if l.strip().startswith("{")][-1])
+    w = b["solver_work_run"]
+    it = w["system_iterations"]
+    units = {"k_bcg_spmv": 2.0 * (it["U"] + it["Y"] + it["E"]), "k_cg_spmv": it["p"]}
+    out = {}
+    for k, t in ms.items():
+        gbs = w["bytes_per_unit"][k] * units[k] / (t / 1e3) / 1e9
+        out[k] = {"units": units[k], "bytes_per_unit": w["bytes_per_unit"][k], "kernel_ms": t, "achieved_GBs": gbs,
+                  "frac": gbs / PEAK}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:3])
