@@ -27,6 +27,7 @@ struct Amg {
   double omega = 0.85;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
+  int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;
 };

@@ -84,6 +84,34 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __
   r[c] = bc - y;
 }
 
+// coarse levels (latency-bound): the first smoothing sweep from zero, the residual and its restriction
+// in one pass over the aggregates -- thread I owns coarse cell I, visits its fine members v in order
+// (x_v = omega b_v / D_v stored for the prolongation; a neighbour's x_j re-formed from b_j / D_j) and
+// sums their residuals: the same arithmetic, in the same order, as k_smooth_res + k_restrict
+template <class T, class TB>
+__global__ void __launch_bounds__(TPB) k_smooth_restrict(int nc, const int* __restrict__ mstart,
+                                                         const int* __restrict__ members, int n, int W,
+                                                         const int* __restrict__ col, const T* __restrict__ val,
+                                                         const T* __restrict__ D, const TB* __restrict__ b, T omega,
+                                                         T* __restrict__ x, T* __restrict__ bc, const double* act) {
+  const int I = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= nc || (act && *act == 0.0)) return;
+  T a = 0;
+  for (int e = mstart[I]; e < mstart[I + 1]; ++e) {
+    const int v = members[e];
+    const T bv = (T)b[v];
+    const T xv = omega * bv / D[v];
+    T y = D[v] * xv;
+    for (int k = 0; k < W; ++k) {
+      const int j = col[(long)k * n + v];
+      if (j < n) y += val[(long)k * n + v] * (omega * (T)b[j] / D[j]);
+    }
+    x[v] = xv;
+    a += bv - y;
+  }
+  bc[I] = a;
+}
+
 template <class T>
 __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
                            const T* __restrict__ r, T* __restrict__ bc, const double* act) {
@@ -206,6 +234,10 @@ void amg_setup(Ctx& x) {
   a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
   a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
   a.overcorr = env_d("DFMI_AMG_OVERCORR", 1.35);
+  // fused smoothing + restriction per level: measured slower (19.7 -> 21.8 ms/step with levels >= 1 fused,
+  // 22.2 with all): one thread per aggregate walks 8 members' rows serially -- 8x less parallelism on
+  // levels that are latency-bound already. Off by default, DFMI_AMG_FUSED=1/2 to re-measure.
+  a.fused_coarse = (int)env_d("DFMI_AMG_FUSED", 0);
   {
     const char* pe = std::getenv("DFMI_AMG_PREC");
     a.fp32 = !(pe && std::string(pe) == "f64");
@@ -331,6 +363,17 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
   for (int l = 0; l + 1 < L; ++l) {
     AmgLevel& f = a.lv[l];
     const dim3 g(blocks_for(f.n, TPB));
+    if ((l > 0 && a.fused_coarse >= 1) || a.fused_coarse >= 2) {   // one launch per level instead of two
+      KScope _ks(x, "k_smooth_restrict");
+      const dim3 gc(blocks_for(a.lv[l + 1].n, TPB));
+      if (l == 0)
+        hipLaunchKernelGGL((k_smooth_restrict<T, double>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
+                           f.members.p, f.n, f.W, COL(0), VAL(0), DD(0), r, om, XV(0), BV(1), act);
+      else
+        hipLaunchKernelGGL((k_smooth_restrict<T, T>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
+                           f.members.p, f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
+      continue;
+    }
     {
       KScope _ks(x, "k_smooth_res");
       if (l == 0)

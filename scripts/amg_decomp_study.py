@@ -5,7 +5,8 @@ copies) split an n^3 periodic box (the reference TGV fields tiled, Burke 9 speci
 decomposePar blocks; each configuration runs a few outer iterations with the production solver controls
 and reports the p-solve iterations. Prints one JSON line per R.
 
-Usage: python scripts/amg_decomp_study.py [n=64] [steps=4]"""
+Usage: python scripts/amg_decomp_study.py [n=64] [steps=4] [strong|weak]
+(strong: one n^3 box split R ways; weak: an n^3 block per rank, the bench's --gpus N layout)"""
 import json
 import os
 import sys
@@ -17,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 sys.path.insert(0, ROOT)
 
 
-def run(n, decomp, steps, hub):
+def run(n, decomp, steps, hub, weak=False):
     import numpy as np
     from bench import MECHS, reference_fields
     from dfmi.mesh import hex_box
@@ -33,7 +34,11 @@ def run(n, decomp, steps, hub):
 
     def work(r):
         try:
-            m = hex_box(n, n, n, lengths=(L, L, L), decomp=decomp, rank=r)
+            if weak:
+                m = hex_box(n * decomp[0], n * decomp[1], n * decomp[2], lengths=(L * decomp[0], L * decomp[1], L * decomp[2]),
+                            decomp=decomp, rank=r)
+            else:
+                m = hex_box(n, n, n, lengths=(L, L, L), decomp=decomp, rank=r)
             ctx = Context(0)
             comm = {"hub": hub, "nranks": nr, "rank": r} if nr > 1 else None
             case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, comm=comm)
@@ -70,10 +75,12 @@ def run(n, decomp, steps, hub):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    weak = len(sys.argv) > 3 and sys.argv[3] == "weak"
     for i, decomp in enumerate([(1, 1, 1), (2, 1, 1), (2, 2, 1), (2, 2, 2)]):
-        r = run(n, decomp, steps, 900 + i)
-        print(json.dumps({"ranks": int(decomp[0] * decomp[1] * decomp[2]), "decomp": decomp, "global_cells": n ** 3,
-                          **r}), flush=True)
+        r = run(n, decomp, steps, 900 + i, weak)
+        R = int(decomp[0] * decomp[1] * decomp[2])
+        print(json.dumps({"ranks": R, "decomp": decomp, "mode": "weak" if weak else "strong",
+                          "global_cells": n ** 3 * (R if weak else 1), **r}), flush=True)
 
 
 if __name__ == "__main__":
