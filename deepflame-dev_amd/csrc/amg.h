@@ -1,6 +1,8 @@
 // amg.h -- aggregation-AMG preconditioner state (amg.hip)
 #pragma once
 #include "dfmi_common.h"
+#include <array>
+#include <map>
 
 namespace dfmi {
 
@@ -30,6 +32,15 @@ struct Amg {
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;
+  // the V-cycle's launches captured once per (operands, precision) and replayed as one graph launch
+  // (DFMI_AMG_GRAPH=0: direct launches); not used while kernel timers are armed
+  bool use_graph = false;
+  std::map<std::array<uintptr_t, 8>, hipGraphExec_t> graphs;
+  void clear_graphs() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
+  ~Amg() { clear_graphs(); }
 };
 
 void amg_setup(Ctx& x);

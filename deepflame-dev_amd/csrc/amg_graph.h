@@ -101,15 +101,15 @@ struct AmgCoarse {
   Graph cg;
 };
 
-inline AmgCoarse amg_coarsen(const std::vector<int>& fcol, int Wf, int nf, const Graph& g) {
+inline AmgCoarse amg_coarsen(const std::vector<int>& fcol, int Wf, int nf, const Graph& g, int passes = 3) {
   AmgCoarse r;
-  // three pairwise passes -> aggregates of up to 8
+  // `passes` pairwise passes -> aggregates of up to 2^passes cells (3: 2x2x2 on a hex mesh)
   std::vector<int>& agg = r.agg;
   agg.resize(nf);
   std::iota(agg.begin(), agg.end(), 0);
   Graph cur = g;
   int ng = nf;
-  for (int pass = 0; pass < 3; ++pass) {
+  for (int pass = 0; pass < passes; ++pass) {
     std::vector<int> grp;
     ng = pair_match(cur, grp);
     for (int v = 0; v < nf; ++v) agg[v] = grp[agg[v]];
