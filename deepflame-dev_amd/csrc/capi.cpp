@@ -497,6 +497,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     Ctx& x = ctx->x;
     require_ready(x);
     copy_old(x);                    // preTimeStep
+    if (x.chem.mode == 2) dnn_prepare(x);   // reacting cells of this step's T (read after the UEqn polls)
     rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
     do_U(x);                        // UEqn
     do_Y(x);                        // YEqn

@@ -84,6 +84,12 @@ struct Dnn {
   DevBuf<int> bc, idx;
   DevBuf<_Float16> x0, h0, h1;
   DevBuf<float> part;           // fused output layer: per-row partial dot products [net][2 N tiles][chunk]
+  // reacting-cell count: compacted at the start of the time step (T is frozen until correctThermo) and
+  // copied to pinned memory behind an event, read by dnn_solve after the UEqn solve's polls -- no drain
+  PinnedBuf<int> nr_host;
+  hipEvent_t nr_ev = nullptr;
+  bool prepared = false;
+  ~Dnn() { if (nr_ev) (void)hipEventDestroy(nr_ev); }
 };
 
 // per-cell chemistry (chem.hip): mechanism arrays (dfmi/kinetics.py layout) and integrator controls
@@ -281,6 +287,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
 // dnn.hip
 void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* params, const double* xmu,
                 const double* xstd, const double* ymu, const double* ystd, double T_react, double dt_infer);
+void dnn_prepare(Ctx& x);   // reacting-cell compaction + count read-back, ahead of dnn_solve
 void dnn_solve(Ctx& x, const char* rho_field);   // RR scaled by rho_field (reference: d_rho_old, dfYEqn.cu:449)
 // chem.hip
 void chem_upload(Ctx& x, int R, const int* idata, const int* irs, const double* dd);

@@ -359,22 +359,35 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
   d.ready = true;
 }
 
-void dnn_solve(Ctx& x, const char* rho_field) {
+void dnn_prepare(Ctx& x) {
   Dnn& d = x.dnn;
   DFMI_CHECK(d.ready, "DNN model not set (dfmi_dnn_set_model)");
-  const int C = x.C, S = x.S, L = (int)d.dims.size() - 1;
+  const int C = x.C;
   const int nb = blocks_for(C, CB);
   if (d.bc.n < (size_t)nb + 1) d.bc.alloc(nb + 1);
   if (d.idx.n < (size_t)C) d.idx.alloc(C);
-  double* RR = x.f("RR");
-  hipLaunchKernelGGL(k_zero, dim3(blocks_for((long)S * C, 256)), dim3(256), 0, x.stream, (long)S * C, RR);
   hipLaunchKernelGGL(k_react_count, dim3(nb), dim3(CB), 0, x.stream, C, x.f("T"), d.T_react, d.bc.p);
   hipLaunchKernelGGL(k_react_scan, dim3(1), dim3(64), 0, x.stream, nb, d.bc.p, d.bc.p + nb);
   hipLaunchKernelGGL(k_react_scatter, dim3(nb), dim3(CB), 0, x.stream, C, x.f("T"), d.T_react, d.bc.p, d.idx.p);
   DFMI_HIP(hipGetLastError());
-  int nr = 0;
-  DFMI_HIP(hipMemcpyAsync(&nr, d.bc.p + nb, sizeof(int), hipMemcpyDeviceToHost, x.stream));
-  DFMI_HIP(hipStreamSynchronize(x.stream));
+  d.nr_host.ensure(1);
+  if (!d.nr_ev) DFMI_HIP(hipEventCreateWithFlags(&d.nr_ev, hipEventDisableTiming));
+  DFMI_HIP(hipMemcpyAsync(d.nr_host.p, d.bc.p + nb, sizeof(int), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipEventRecord(d.nr_ev, x.stream));
+  d.prepared = true;
+}
+
+void dnn_solve(Ctx& x, const char* rho_field) {
+  Dnn& d = x.dnn;
+  DFMI_CHECK(d.ready, "DNN model not set (dfmi_dnn_set_model)");
+  const int C = x.C, S = x.S, L = (int)d.dims.size() - 1;
+  if (!d.prepared) dnn_prepare(x);
+  d.prepared = false;
+  double* RR = x.f("RR");
+  hipLaunchKernelGGL(k_zero, dim3(blocks_for((long)S * C, 256)), dim3(256), 0, x.stream, (long)S * C, RR);
+  // the count was copied behind an event at the step start; the solver polls since then have passed it
+  DFMI_HIP(hipEventSynchronize(d.nr_ev));
+  const int nr = d.nr_host.p[0];
   d.last_reacting = nr;
   if (nr == 0) return;
   const int chunk = std::min(nr, d.chunk);
