@@ -2,7 +2,8 @@
 summary (scripts/prof_summary.py output) and the bench JSON line of the SAME profiled command, whose
 "solver_work_run" holds the system-iterations of every solve in that process and the algorithmic bytes per
 unit. k_bcg_spmv: 2 SpMVs (spmv1 + spmv2 launches) per BiCGStab system-iteration; k_cg_spmv: 1 per PCG
-iteration. Usage: python scripts/roof_from_profile.py profiles/r02_kernel_stats.csv profiles/r02_bench_prof.json"""
+iteration. Usage: python scripts/roof_from_profile.py profiles/r02_kernel_stats.csv profiles/r02_bench_prof.json
+(profiles/r02_roof_from_profile.json is its output for the committed round-2 profile)"""
 import csv
 import json
 import sys
@@ -15,8 +16,10 @@ def main(stats_csv, bench_json):
     head, rows = rows[0], rows[1:]
     ms = {}
     for r in rows:
-        d = dict(zip(head, r))
-        name = d["kernel"].split("::")[-1]
+        if len(r) < len(head):
+            continue
+        d = dict(zip(head[:-1], r[:len(head) - 1]))
+        name = ",".join(r[len(head) - 1:]).split("::")[-1]   # kernel names contain commas
         fam = "k_bcg_spmv" if name.startswith("k_bcg_spmv") else ("k_cg_spmv" if name.startswith("k_cg_spmv") else None)
         if fam:
             ms[fam] = ms.get(fam, 0.0) + float(d["total_ms"])
