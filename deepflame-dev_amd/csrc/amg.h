@@ -35,6 +35,7 @@ struct Amg {
   // the V-cycle's launches captured once per (operands, precision) and replayed as one graph launch
   // (DFMI_AMG_GRAPH=0: direct launches); not used while kernel timers are armed
   bool use_graph = false;
+  int coop_blocks = 0;   // > 0: levels >= 1 of the V-cycle run as one cooperative launch of this many blocks
   std::map<std::array<uintptr_t, 8>, hipGraphExec_t> graphs;
   void clear_graphs() {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);

@@ -21,6 +21,7 @@
 #include "dfmi_ctx.h"
 #include "amg.h"
 #include "amg_graph.h"
+#include <hip/hip_cooperative_groups.h>
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -206,6 +207,107 @@ __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __re
   for (int c = threadIdx.x; c < n; c += CTPB) x[c] = (TO)cur[c];
 }
 
+// ---------------------------------------------------------------- coarse levels in one launch
+// Levels 1 .. L-1 of the V-cycle (down sweeps + restrictions, the coarsest solve, up sweeps) as ONE
+// cooperative kernel: a grid of one 1024-thread block per CU walks each level's cells in grid-stride
+// order and meets at a grid barrier between dependent phases, instead of a chain of 4-8 us launches
+// (the coarse levels are latency-bound: 13 launches per V-cycle, ~2 ms per step). Per phase the
+// arithmetic is k_smooth_res / k_restrict / k_coarsest / k_prolong_smooth's, in the same order, so
+// the V-cycle's result is bitwise the launch-chain's. The corrected x of level l >= 1 goes to xo[l].
+constexpr int PL = 10;
+template <class T> struct CoarseArgs {
+  int L;
+  int n[PL], W[PL];
+  const int* col[PL];
+  const T* val[PL];
+  const T* D[PL];
+  T* b[PL];
+  T* x[PL];
+  T* r[PL];
+  T* xo[PL];
+  const int* agg[PL];
+  const int* mstart[PL];
+  const int* members[PL];
+  T omega, sc;
+  int sweeps;
+  const double* act;
+};
+
+template <class T>
+__global__ void __launch_bounds__(CTPB) k_amg_coarse(CoarseArgs<T> a) {
+  if (a.act && *a.act == 0.0) return;   // uniform over the grid: no block reaches a barrier alone
+  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+  const T om = a.omega;
+  for (int l = 1; l + 1 < a.L; ++l) {   // down: one sweep from zero + residual, then restriction
+    const int n = a.n[l], W = a.W[l];
+    const int* col = a.col[l];
+    const T *val = a.val[l], *D = a.D[l], *b = a.b[l];
+    for (int c = tid; c < n; c += nth) {
+      const T bc = b[c];
+      const T xc = om * bc / D[c];
+      T y = D[c] * xc;
+      for (int k = 0; k < W; ++k) {
+        const int j = col[(long)k * n + c];
+        if (j < n) y += val[(long)k * n + c] * (om * b[j] / D[j]);
+      }
+      a.x[l][c] = xc;
+      a.r[l][c] = bc - y;
+    }
+    grid.sync();
+    const int nc = a.n[l + 1];
+    for (int I = tid; I < nc; I += nth) {
+      T s = 0;
+      for (int e = a.mstart[l][I]; e < a.mstart[l][I + 1]; ++e) s += a.r[l][a.members[l][e]];
+      a.b[l + 1][I] = s;
+    }
+    grid.sync();
+  }
+  if (blockIdx.x == 0) {   // coarsest: weighted-Jacobi sweeps from zero, LDS-resident (k_coarsest)
+    __shared__ T xa[COARSEST], xb[COARSEST];
+    __shared__ T sv[LDS_ENT];
+    __shared__ int sc_[LDS_ENT];
+    __shared__ T sd[COARSEST], sb[COARSEST];
+    const int l = a.L - 1, n = a.n[l], W = a.W[l];
+    for (int e = threadIdx.x; e < n * W; e += CTPB) { sv[e] = a.val[l][e]; sc_[e] = a.col[l][e]; }
+    for (int c = threadIdx.x; c < n; c += CTPB) { sd[c] = a.D[l][c]; sb[c] = a.b[l][c]; xa[c] = om * a.b[l][c] / a.D[l][c]; }
+    __syncthreads();
+    T* cur = xa;
+    T* nxt = xb;
+    for (int s = 1; s < a.sweeps; ++s) {
+      for (int c = threadIdx.x; c < n; c += CTPB) {
+        T y = sd[c] * cur[c];
+        for (int k = 0; k < W; ++k) {
+          const int j = sc_[k * n + c];
+          if (j < n) y += sv[k * n + c] * cur[j];
+        }
+        nxt[c] = cur[c] + om * (sb[c] - y) / sd[c];
+      }
+      __syncthreads();
+      T* t = cur; cur = nxt; nxt = t;
+    }
+    for (int c = threadIdx.x; c < n; c += CTPB) a.x[l][c] = cur[c];
+  }
+  grid.sync();
+  for (int l = a.L - 2; l >= 1; --l) {   // up: prolongate the scaled coarse correction + one sweep
+    const int n = a.n[l], W = a.W[l];
+    const int* col = a.col[l];
+    const int* agg = a.agg[l];
+    const T *val = a.val[l], *D = a.D[l], *b = a.b[l], *x = a.x[l];
+    const T* xc = l + 1 == a.L - 1 ? a.x[l + 1] : a.xo[l + 1];
+    for (int c = tid; c < n; c += nth) {
+      const T yc = x[c] + a.sc * xc[agg[c]];
+      T ay = D[c] * yc;
+      for (int k = 0; k < W; ++k) {
+        const int j = col[(long)k * n + c];
+        if (j < n) ay += val[(long)k * n + c] * (x[j] + a.sc * xc[agg[j]]);
+      }
+      a.xo[l][c] = yc + om * (b[c] - ay) / D[c];
+    }
+    if (l > 1) grid.sync();
+  }
+}
+
 // ---------------------------------------------------------------- host: hierarchy
 // (aggregation in amg_graph.h, shared with the CPU-A baseline; here the result is uploaded)
 void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLevel& c, std::vector<int>& ccol,
@@ -231,7 +333,18 @@ void amg_setup(Ctx& x) {
   Amg& a = x.amg;
   a.clear_graphs();
   a.lv.clear();
-  a.use_graph = env_d("DFMI_AMG_GRAPH", 0) != 0;   // measured: 19.5 -> 19.9 ms/step with graphs (GPU-side latency, not host launches, bounds the coarse levels)
+  a.use_graph = env_d("DFMI_AMG_GRAPH", 0) != 0;
+  a.coop_blocks = 0;
+  // measured: 19.6 -> 26.4 ms/step (grid barriers cost more than the launches they replace); DFMI_AMG_COOP=1
+  if (env_d("DFMI_AMG_COOP", 0) != 0) {   // one co-resident 1024-thread block per CU (cooperative launch)
+    int dev = 0, coop = 0, ncu = 0, per_cu = 0;
+    DFMI_HIP(hipGetDevice(&dev));
+    DFMI_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+    DFMI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const void* k = a.fp32 ? (const void*)k_amg_coarse<float> : (const void*)k_amg_coarse<double>;
+    DFMI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, CTPB, 0));
+    if (coop && per_cu >= 1) a.coop_blocks = ncu;
+  }   // measured: 19.5 -> 19.9 ms/step with graphs (GPU-side latency, not host launches, bounds the coarse levels)
   a.omega = env_d("DFMI_AMG_OMEGA", 0.85);
   a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
   a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
@@ -361,6 +474,43 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
   auto XV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fx.p; else return a.lv[l].x.p; };
   auto RV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fr.p; else return a.lv[l].r.p; };
   auto XO = [&](int l) -> T* { if constexpr (F) return a.lv[l].fxo.p; else return a.lv[l].xo.p; };
+  if (a.coop_blocks > 0 && L >= 3 && !a.fused_coarse) {   // level 0 by launches, levels >= 1 in one
+    AmgLevel& f = a.lv[0];
+    const dim3 g(blocks_for(f.n, TPB));
+    {
+      KScope _ks(x, "k_smooth_res");
+      launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
+               DD(0), r, om, XV(0), RV(0), act);
+    }
+    {
+      KScope _ks(x, "k_restrict");
+      hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[1].n,
+                         f.mstart.p, f.members.p, (const T*)RV(0), BV(1), act);
+    }
+    CoarseArgs<T> ca{};
+    ca.L = L;
+    for (int l = 1; l < L; ++l) {
+      AmgLevel& v = a.lv[l];
+      ca.n[l] = v.n; ca.W[l] = v.W; ca.col[l] = COL(l); ca.val[l] = VAL(l); ca.D[l] = DD(l);
+      ca.b[l] = BV(l); ca.x[l] = XV(l); ca.r[l] = RV(l); ca.xo[l] = XO(l);
+      ca.agg[l] = v.agg.p; ca.mstart[l] = v.mstart.p; ca.members[l] = v.members.p;
+    }
+    ca.omega = om; ca.sc = sc; ca.sweeps = a.coarse_sweeps; ca.act = act;
+    {
+      KScope _ks(x, "k_amg_coarse");
+      void* args[] = {&ca};
+      DFMI_HIP(hipLaunchCooperativeKernel((const void*)k_amg_coarse<T>, dim3(a.coop_blocks), dim3(CTPB), args, 0,
+                                          x.stream));
+    }
+    {
+      KScope _ks(x, "k_prolong_smooth");
+      launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
+               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p,
+               (const T*)(L == 2 ? XV(1) : XO(1)), om, sc, z, partial, act);
+    }
+    DFMI_HIP(hipGetLastError());
+    return;
+  }
   // down: smooth from zero + residual, restrict
   for (int l = 0; l + 1 < L; ++l) {
     AmgLevel& f = a.lv[l];

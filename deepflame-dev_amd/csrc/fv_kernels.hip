@@ -1399,11 +1399,18 @@ void y_prep(Ctx& x) {
                         x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),    \
                         x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"),         \
                         x.f("diffAlphaD"), gout)
-  DFMI_SWITCH_S(x.S, CALL,
-                LAUNCH_SW(k_y_prep_gen, YCH, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
-                       x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"),
-                       x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),
-                       x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout))
+#define GEN(CH) LAUNCH_SW(k_y_prep_gen, CH, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),     \
+                       x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
+                       x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                  \
+                       x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout)
+  // DFMI_YPREP_CH=3|4|8: the species-chunked kernel for any S (A/B: a smaller per-pass gather footprint)
+  const char* ech = std::getenv("DFMI_YPREP_CH");
+  const int ch = ech ? std::atoi(ech) : 0;
+  if (ch == 3) GEN(3);
+  else if (ch == 4) GEN(4);
+  else if (ch == 8) GEN(8);
+  else DFMI_SWITCH_S(x.S, CALL, GEN(YCH))
+#undef GEN
 #undef CALL
   halo_fields(x, {"sumYDiffError", "hDiffCorrFlux"});
   LAUNCH(k_phiuc_face, x.Fs, m, x.f("sumYDiffError"), x.f("phiUc"));
