@@ -15,6 +15,7 @@
 //    Cantera setState_TPY reactor state and RR scaled by the step-start density (chem.hip), one cell
 //    per OpenMP iteration (dynamic schedule: stiff cells cost 10-100x the others).
 // Single rank (no processor patches); DNN chemistry, renumbering and kernel timers are GPU-path only.
+// Also runs BASELINE configs 1 (dfmi_zero_d_step) and 2 (the 1D flame's mixed outlet) for bench.py.
 #include "../../include/dfmi.h"
 #include "../../deepflame-dev_amd/csrc/amg_graph.h"
 
@@ -1038,7 +1039,42 @@ int dfmi_chem_solve(dfmi_ctx* ctx, double dt) {
 }
 int dfmi_chem_set_max_steps(dfmi_ctx* ctx, int n) { return guard([&] { CHECK(n > 0, "max_steps must be positive"); ctx->x.max_steps = n; }); }
 int dfmi_chem_info(dfmi_ctx* ctx, int* generated) { return guard([&] { if (generated) *generated = ctx->x.generated; }); }
-int dfmi_zero_d_step(dfmi_ctx*, double, int) { return guard([&] { throw Error("dfmi (CPU-A): df0DFoam steps are a GPU-path feature"); }); }
+// df0DFoam steps (df0DFoam.C:99-113; the GPU path's zero_d_step, fv_kernels.hip): chemistry at the
+// current density, YEqn ddt(rho, Y) == RR with clipping and the inert remainder, he held, correctThermo
+int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    require_ready(x);
+    CHECK(dt > 0 && n_steps >= 1, "0D step: dt and n_steps must be positive");
+    CHECK(x.mode == 1, "CPU-A 0D step: chemistry mode must be 1 (ODE)");
+    const long C = x.C;
+    const int S = x.S, inert = x.inert;
+    for (int it = 0; it < n_steps; ++it) {
+      std::memcpy(x.f("rho_old"), x.f("rho"), C * sizeof(double));
+      chem_solve(x, dt, "rho");
+      const double rdt = 1.0 / dt;
+      const double *V = x.w("volume"), *ro = x.f("rho_old"), *rho = x.f("rho"), *RR = x.f("RR");
+      double* Y = x.f("Y");
+#pragma omp parallel for schedule(static)
+      for (long c = 0; c < C; ++c) {
+        const double vol = V[c], dg = rdt * rho[c] * vol, r0 = rdt * ro[c];
+        double sum = 0.0;
+        for (int s = 0; s < S; ++s) {
+          if (s == inert) continue;
+          double y = (r0 * Y[s * C + c] * vol + vol * RR[s * C + c]) / dg;
+          y = y > 0 ? y : 0;
+          Y[s * C + c] = y;
+          sum += y;
+        }
+        sum = 1 - sum;
+        Y[inert * C + c] = sum > 0 ? sum : 0;
+      }
+      orc(orc_correct_bc("Y", "boundary_Y", "ptype_Y", S), "Y boundary");
+      orc(orc_thermo_correct(0), "correctThermo");
+      rho_from_psi(x);
+    }
+  });
+}
 
 int dfmi_dnn_set_model(dfmi_ctx*, int, int, const int*, const float*, const double*, const double*, const double*,
                        const double*, double, double) {

@@ -117,6 +117,27 @@ def parse():
     return ap.parse_args()
 
 
+def hbm_copy_peak(device: int, gib: float = 4.0, reps: int = 10) -> float:
+    """Measured device-to-device copy bandwidth (GB/s, read + write bytes) of a gib-GiB buffer: the
+    STREAM-copy reference SURVEY 8(d) asks for beside the 8 TB/s datasheet peak"""
+    import torch
+    n = int(gib * (1 << 30)) // 8
+    a = torch.ones(n, dtype=torch.float64, device=f"cuda:{device}")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    s.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e.record()
+    torch.cuda.synchronize(device)
+    gbs = 2.0 * 8 * n * reps / (s.elapsed_time(e) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def host_cpu():
     """(usable cores, machine cores, CPU model string) of this host (the lscpu 'Model name' field)"""
     model = "unknown"
@@ -161,13 +182,23 @@ def cpu_baseline(args, table, ym, inert):
     threads = int(ctx.lib.dfmi_version().decode().split("(OpenMP, ")[1].split(" ")[0])
     iters = {e: ctx.solver_stats(e)[0] for e in ("U", "Y", "E", "p")}
     ctx.close()
+    # BASELINE.md section 2 also times configs 1 and 2 on CPU-A (same step definitions as the GPU lines)
+    configs = {}
+    if args.chem == "ode" and not args.no_flame:
+        fl = flame1d_line(steps=20, warmup=2, lib_path=path)
+        configs["config2_flame1d"] = {"cell_updates_per_s": fl["cell_updates_per_s"], "ms_per_step": fl["ms_per_step"],
+                                      "steps": fl["steps"]}
+        zd = zero_d_line(n_steps=200, lib_path=path)
+        configs["config1_zeroD"] = {"chem_integrations_per_s": zd["chem_integrations_per_s"], "steps": 200,
+                                    "T_end": zd["T_end"], "T_end_oracle": zd["T_end_oracle"]}
     usable, machine, model = host_cpu()
     chem = "ROS3 chemistry (rtol 1e-6, atol 1e-10)" if args.chem == "ode" else "no chemistry"
     return {"value": m.n_cells * args.cpu_steps / el, "unit": "cell-updates/s", "cores": threads, "kind": "CPU-A",
             "sample": f"baseline/cpu_a (OpenMP C++, fp64, same ABI and step) on {n}^3 = {m.n_cells} cells, "
                       f"{table.S} species, {chem}, {args.cpu_steps} timed outer iterations in {el:.1f} s after "
                       f"1 untimed; last-step solver iterations {iters}",
-            "host": {"omp_threads": threads, "affinity_cpus": usable, "nproc": machine, "model": model}}
+            "host": {"omp_threads": threads, "affinity_cpus": usable, "nproc": machine, "model": model},
+            "configs": configs}
 
 
 def reference_fields(m, species):
@@ -214,7 +245,7 @@ def host_state(m, table, f):
     return s
 
 
-def flame1d_line(steps=100, warmup=10):
+def flame1d_line(steps=100, warmup=10, lib_path=None):
     """BASELINE config 2: the reference's 1D H2/air flame (test/Tu500K-Phi1, 880 cells, 9 species,
     direct chemistry, dt 1e-6) on one GPU -- a latency-bound case (one wave of cells), reported
     beside the headline line, not as it."""
@@ -226,12 +257,13 @@ def flame1d_line(steps=100, warmup=10):
     ym = read_yaml_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml"))
     t = read_thermo_table(os.path.join(golden, "thermo_Burke2012_s9r23.txt"), ym["species"])
     m = case.flame1d_mesh()
-    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")), lib_path=lib_path)
     case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, case.flame1d_patch_types(m))
     ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml")))
     ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
     f, bv = case.flame1d_fields(os.path.join(golden, "flame1d"), ym["species"])
-    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], bvals=bv)
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], bvals=bv,
+                    gammas=case.flame1d_gamma(os.path.join(golden, "flame1d")))
     for _ in range(warmup):
         ctx.time_step(2)
     ctx.sync()
@@ -242,7 +274,7 @@ def flame1d_line(steps=100, warmup=10):
     el = time.perf_counter() - t0
     ctx.close()
     return {"workload": "1D freely-propagating H2/air flame (test/Tu500K-Phi1), 880 cells, Burke2012 9 species, "
-                        "direct integration, dt=1e-6, nCorr=2 (BASELINE config 2)",
+                        "waveTransmissive outlet, direct integration, dt=1e-6, nCorr=2 (BASELINE config 2)",
             "ms_per_step": el / steps * 1e3, "cell_updates_per_s": m.n_cells * steps / el, "steps": steps}
 
 
@@ -302,7 +334,7 @@ def dnn53_line(m, T, p, steps=3, warmup=1):
                               "frac": tf / 2500.0 if tf else None}}
 
 
-def zero_d_line(n_steps=1000):
+def zero_d_line(n_steps=1000, lib_path=None):
     """BASELINE config 1: the reference df0DFoam case (examples/df0DFoam/zeroD_cubicReactor/H2/
     cvodeIntegrator: 10^3 cells of the same reactor, ES80_H2-7-16, T0 = 1000 K, 1 atm, dt 1e-6, 1000 steps,
     constant pressure) through dfmi_zero_d_step; chem-integrations/s = cells x steps / wall time."""
@@ -317,7 +349,7 @@ def zero_d_line(n_steps=1000):
     ym = read_yaml_mechanism(os.path.join(golden, ref["mechanism"]))
     t = read_thermo_table(os.path.join(golden, "thermo_ES80_H2-7-16.txt"), ym["species"])
     m = hex_box(10, 10, 10, lengths=(5e-3,) * 3, periodic=(False,) * 3)
-    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
+    ctx = Context(int(os.environ.get("LOCAL_RANK", "0")), lib_path=lib_path)
     case.setup_context(ctx, m, t, ym["species"].index("N2"), ref["dt"])
     ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, ref["mechanism"])))
     ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
@@ -576,6 +608,10 @@ def main():
                 if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
     }
+    if world == 1:   # the headline kernel against a measured copy peak as well as the datasheet's
+        peak_copy = hbm_copy_peak(local)
+        out["roofline"]["measured_copy_peak_GBs"] = peak_copy
+        out["roofline"]["frac_of_measured_copy_peak"] = out["roofline"]["achieved"] / peak_copy
     U0 = ctx.get_field("U", (3, m.n_cells)) if (rank == 0 and world == 1 and n == 128 and not args.no_flame) else None
     ctx.close()
     if rank == 0 and world == 1 and n == 128 and not args.no_flame:
