@@ -126,3 +126,29 @@ def test_chemistry_matches_bdf():
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     assert np.abs(ref).max() > 0
     assert (np.abs(rr - ref) / scale).max() < 1e-4
+
+
+def test_zero_d_steps_follow_the_oracle_trajectory():
+    """BASELINE config 1 on CPU-A (dfmi_zero_d_step): the df0DFoam reactor of the reference example
+    against the committed oracle trajectory (tests/golden/zeroD_cubicReactor.json)"""
+    import json
+    from dfmi import case
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.kinetics import parse_mechanism
+    ref = json.load(open(os.path.join(GOLDEN, "zeroD_cubicReactor.json")))
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, ref["mechanism"]))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
+    m = hex_box(3, 3, 3, lengths=(5e-3,) * 3, periodic=(False,) * 3)
+    ctx = _ctx()
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), ref["dt"])
+    ctx.chem_set_mechanism(parse_mechanism(os.path.join(GOLDEN, ref["mechanism"])))
+    ctx.chem_set_options(1, rtol=1e-12, atol=1e-22)   # the fixture's converged trajectory (test_gpu_zero_d)
+    C = m.n_cells
+    case.init_state(ctx, m, t.S, np.full(C, ref["T0"]), np.full(C, ref["p"]), np.zeros((3, C)),
+                    np.repeat(np.asarray(ref["Y0"])[:, None], C, axis=1))
+    n = min(300, ref["n_steps"])
+    ctx.zero_d_step(ref["dt"], n)
+    T = ctx.get_field("T", (C,))
+    assert np.ptp(T) <= 1e-12 * T[0]
+    assert abs(T[0] - ref["T"][n]) <= 2e-5 * ref["T"][n]
