@@ -890,6 +890,8 @@ int dfmi_renumber_faces(int, int, const int*, const int*, const int*, int*, int*
   return guard([&] { throw Error("dfmi (CPU-A): renumbering is provided by the GPU library"); });
 }
 
+int dfmi_set_traversal(dfmi_ctx*, const int*) { return 0; }   // a GPU visiting order: nothing to do here
+
 int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* pt) {
   return guard([&] {
     Ctx& x = ctx->x;

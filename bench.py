@@ -109,6 +109,8 @@ def parse():
                     help="cell order (dfmi_renumber_cells): blockMesh order (default: with the owner-slot face "
                          "storage its gathers are contiguous runs and it measured fastest), 8x8x4 bricks on a Z-order "
                          "curve, plain Morton, or reverse Cuthill-McKee")
+    ap.add_argument("--traversal", default="none", choices=["bricks", "none"],
+                    help="visiting order of the gather kernels over the blockMesh-ordered data (dfmi_set_traversal)")
     ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
     ap.add_argument("--cpu-n", type=int, default=128, help="cells per direction of the CPU-A baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=2, help="timed outer iterations of the CPU-A baseline")
@@ -456,6 +458,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = {"uid": uid[0], "nranks": world, "rank": rank}
     case.setup_context(ctx, m, table, inert, args.dt, comm=comm)
+    if args.traversal == "bricks" and hasattr(m, "local_index"):
+        from dfmi.lib import renumber_cells
+        ijk = np.stack(m.local_index, axis=1).astype(np.float64)
+        ctx.set_traversal(renumber_cells(m.n_cells, ijk, m.owner, m.neighbour, "bricks"))
     if args.chem == "ode":
         from dfmi.kinetics import parse_mechanism
         ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, yml)))
@@ -575,6 +581,7 @@ def main():
                                f"{cells_total} hex cells ({m.n_cells} per GPU), H2/air {table.S} species "
                                f"({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
                    "cells_per_gpu": m.n_cells, "species": table.S, "cell_order": args.renumber,
+                   "traversal": args.traversal,
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
         "roofline": dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "

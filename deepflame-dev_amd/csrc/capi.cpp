@@ -406,6 +406,21 @@ int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type
   });
 }
 
+int dfmi_set_traversal(dfmi_ctx* ctx, const int* order) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_sizes, "call dfmi_set_constant_values first");
+    if (!order) { x.trav.release(); return; }
+    std::vector<char> seen(x.C, 0);
+    for (int t = 0; t < x.C; ++t) {
+      DFMI_CHECK(order[t] >= 0 && order[t] < x.C && !seen[order[t]], "traversal order is not a permutation of the cells");
+      seen[order[t]] = 1;
+    }
+    x.trav.upload(order, x.C, x.stream);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
 int dfmi_set_patch_param(dfmi_ctx* ctx, const char* field, int patch, const char* name, double value) {
   return guard([&] {
     Ctx& x = ctx->x;

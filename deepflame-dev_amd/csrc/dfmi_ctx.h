@@ -35,6 +35,7 @@ struct MeshView {
   const int *ecol, *esrc;   // solver gather rows [W][C] (linsolve.hip build_ell): the face loops read them
   int W;
   double rdt;
+  const int* trav;          // optional traversal order of the per-cell gather kernels (thread t -> cell)
 };
 
 struct Field {
@@ -188,6 +189,7 @@ struct Ctx {
   std::map<std::string, StatSnap> stat_snap;
   DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
+  DevBuf<int> trav;   // dfmi_set_traversal: the order threads visit cells in the gather kernels (empty: natural)
   ~Ctx();
   int n_corr = 2;
 
@@ -199,6 +201,7 @@ struct Ctx {
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
     m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
     m.rdt = rdt;
+    m.trav = trav.n ? trav.p : nullptr;
     return m;
   }
   double* f(const std::string& name) {

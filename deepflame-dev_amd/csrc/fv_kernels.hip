@@ -23,6 +23,11 @@ __device__ __forceinline__ double interp_f(double w, double vo, double vn) { ret
 __device__ __forceinline__ double interp_b(double w, double vo, double vn) { return w * vo + (1.0 - w) * vn; }
 
 struct BCoef { double vic, vbc, gic, gbc; };
+
+// the cell a gather-kernel thread works on: thread order, or the traversal dfmi_set_traversal installed
+// (e.g. 8x8x4 bricks on a Z-order curve over blockMesh-ordered data: same data layout, cache-compact
+// visiting order). Each cell's arithmetic is unchanged, so results are bitwise independent of it.
+__device__ __forceinline__ int cell_of(const MeshView& m, int t) { return (m.trav && t < m.C) ? m.trav[t] : t; }
 // per-slot data of the mixed conditions of one field: waveTransmissive (advectiveFvPatchField, Euler ddt:
 // refValue = the old-time boundary value, valueFraction = 1 / (1 + w dt deltaCoeffs) set at the pEqn
 // assembly) and inletOutlet (refValue = inletValue, valueFraction = 1 - pos0(phi))
@@ -143,7 +148,7 @@ template <int WT>
 __global__ void k_rho(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ rho_old,
                       const double* __restrict__ phi, const double* __restrict__ bphi, double* __restrict__ rho,
                       double* __restrict__ odiag, double* __restrict__ osrc) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   double div = 0.0;
   each_face<WT>(m, c, [&](int f, int, bool own) { if (own) div += phi[f]; else div -= phi[f]; });
@@ -169,7 +174,7 @@ template <int WT>
 __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
                          const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
                          double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double s[9];
@@ -236,7 +241,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
     const double* __restrict__ bp, const double* __restrict__ T, const double* __restrict__ bT,
     double* __restrict__ lower, double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src,
     double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU, MixBC mxU) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
@@ -321,7 +326,7 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
     const double* __restrict__ bU, const double* __restrict__ lower, const double* __restrict__ upper,
     const double* __restrict__ src, const double* __restrict__ ic, const double* __restrict__ bc,
     double* __restrict__ H) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
 #pragma unroll
@@ -448,7 +453,7 @@ __global__ void k_p_cell(MeshView m, const int8_t* __restrict__ tyP, const doubl
                          const double* __restrict__ ph, const double* __restrict__ bph, const double* __restrict__ p,
                          const double* __restrict__ p_old, const double* __restrict__ psi, const double* __restrict__ rho,
                          const double* __restrict__ rho_old, double* __restrict__ diag, double* __restrict__ src) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   double dL = 0.0, div = 0.0;
   each_face<WT>(m, c, [&](int f, int, bool own) {
@@ -496,7 +501,7 @@ __global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const 
                               const double* __restrict__ bp, const double* __restrict__ p_old,
                               const double* __restrict__ H, const double* __restrict__ rAU, double* __restrict__ U,
                               double* __restrict__ K, double* __restrict__ dpdt) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double g[3] = {0.0, 0.0, 0.0};
@@ -534,7 +539,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
     const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
     const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
     double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   // One pass over the cell's faces computes every species' Gauss gradient AND its diffAlphaD
@@ -687,7 +692,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
     double* __restrict__ bc, MixBC mxY) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, d2 = 0.0;
@@ -747,7 +752,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
     double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
   double d1 = 0.0, d2 = 0.0;
@@ -932,7 +937,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
     const double* __restrict__ alpha, const double* __restrict__ balpha, double* __restrict__ sumE,
     double* __restrict__ bsumE, double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD,
     double* __restrict__ gout) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
   const double ac = alpha[c], vol = m.V[c];
@@ -1015,7 +1020,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
     double* __restrict__ bc, MixBC mxY) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   const double vol = m.V[c];
@@ -1079,7 +1084,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
     double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
   const double vol = m.V[c];
@@ -1178,7 +1183,7 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
     const double* __restrict__ bhD, const double* __restrict__ dpdt, const double* __restrict__ dAD,
     const double* __restrict__ egrad, double* __restrict__ lower, double* __restrict__ upper,
     double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic, double* __restrict__ bc) {
-  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0, divK = 0.0, divh = 0.0;

@@ -47,6 +47,7 @@ SIGNATURES = {
     "dfmi_set_patch_types": [_P, C.c_char_p, _IP],
     "dfmi_set_inert_index": [_P, C.c_int],
     "dfmi_set_patch_param": [_P, C.c_char_p, C.c_int, C.c_char_p, C.c_double],
+    "dfmi_set_traversal": [_P, _IP],
     "dfmi_thermo_set_coeffs": [_P, C.c_int, _DP, _DP, _DP, _DP, _DP],
     "dfmi_thermo_load": [_P, C.c_char_p],
     "dfmi_set_field": [_P, C.c_char_p, _DP, C.c_long, C.c_int],
@@ -228,6 +229,14 @@ class Context:
 
     def set_patch_param(self, field, patch, name, value):
         self._call("dfmi_set_patch_param", self.h, field.encode(), int(patch), name.encode(), float(value))
+
+    def set_traversal(self, order):
+        """visiting order of the gather kernels (None: natural); see include/dfmi.h"""
+        if order is None:
+            self._call("dfmi_set_traversal", self.h, None)
+        else:
+            a = _i32(order)
+            self._call("dfmi_set_traversal", self.h, _ip(a))
 
     def set_inert_index(self, i):
         self._call("dfmi_set_inert_index", self.h, int(i))

@@ -89,6 +89,12 @@ int dfmi_renumber_faces(int num_cells, int num_faces, const int* owner, const in
                         const int* cell_new_to_old, int* face_new_to_old, int* new_owner, int* new_neighbour,
                         int* flipped);
 
+/* the order in which the per-cell gather kernels visit cells (order[C]: a permutation; thread t works on
+ * cell order[t]) -- e.g. dfmi_renumber_cells(..., "bricks", ...) of a blockMesh box: the data stay in
+ * their order, only the visiting order becomes cache-compact. NULL restores the natural order. Results
+ * are bitwise independent of it (each cell's arithmetic is unchanged). No reference counterpart. */
+int dfmi_set_traversal(dfmi_ctx* ctx, const int* order);
+
 /* ---- per-equation patch types ------------------------------------------------------------ */
 /* dfUEqn/dfYEqn/dfEEqn/dfpEqn/dfRhoEqn/dfThermo::setConstantFields (e.g. dfUEqn.cu:364-379,
  * dfEEqn.cu setConstantFields, dfThermo.cu setConstantFields). field in

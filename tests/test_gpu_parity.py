@@ -47,7 +47,7 @@ def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
 
 
 def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False,
-          renumber=None, mixed=False):
+          renumber=None, mixed=False, traversal=False):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.lib import Context
     from dfmi import case
@@ -67,6 +67,10 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
     inert = ym["species"].index("N2")
     dt = 1e-6
     case.setup_context(ctx, m, t, inert, dt, pt)
+    if traversal:     # gather kernels visit the cells in 8x8x4 bricks (dfmi_set_traversal); data order unchanged
+        from dfmi.lib import renumber_cells
+        ijk = np.stack(m.local_index, axis=1).astype(np.float64)
+        ctx.set_traversal(renumber_cells(m.n_cells, ijk, m.owner, m.neighbour, "bricks"))
     f = case.tgv_fields(m, ym["species"], kernel_radius=1.2e-3)
     if mech == "gri53":   # every one of the 53 species present (Dirichlet-like draws)
         from dfmi.synthetic import gri53_mass_fractions
@@ -102,7 +106,7 @@ def _oracle(m, t, st, pt, inert, dt):
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
                                         "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
-                                        "mixed", "mixed-generic"])
+                                        "mixed", "mixed-generic", "walls-trav"])
 def periodic(request):
     generic = request.param.endswith("-generic")
     if generic:
@@ -111,7 +115,8 @@ def periodic(request):
     if request.param.endswith("-csr"):     # face loops by the CSR walk instead of the gather rows
         os.environ["DFMI_FACE_CSR"] = "1"
         request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
-    param = request.param.replace("-generic", "").replace("-csr", "")
+    traversal = request.param.endswith("-trav")
+    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
@@ -142,7 +147,8 @@ def periodic(request):
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
         return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber,
-                     mixed=mixed)
+                     mixed=mixed, traversal=traversal, nx=16 if traversal else 6, ny=12 if traversal else 5,
+                     nz=8 if traversal else 4)
     return _case(mech=param, renumber=renumber, nx=16 if renumber else 6, ny=8 if renumber else 5,
                  nz=4 if renumber else 4)
 
