@@ -9,8 +9,9 @@
 //
 // Integrator: ROS3 Rosenbrock (L-stable, order 3, embedded order-2 error estimate, one Jacobian and
 // one LU per step) with adaptive step size; alternative (DFMI_CHEM_METHOD=extrap): linearly-implicit
-// Euler extrapolation with step sequence 1, 2, 3. Analytic Jacobian of the mass-action terms (the
-// fall-off [M]-dependence of k is omitted, an approximation the step control absorbs). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
+// Euler extrapolation with step sequence 1, 2, 3. Analytic Jacobian: mass action, third-body factors and
+// the fall-off rate constants' [M]-dependence (without the latter the stiff 1D-flame cells needed 2-5x
+// more steps: a Rosenbrock method loses order with an inexact Jacobian). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
 // mass fractions) by default.
 //
 // Scheduling: cells are launched in descending order of the integrator steps they needed in the
@@ -128,6 +129,33 @@ __device__ __forceinline__ void rcoef(const ChemMech& m, const Lane<S>& L, int r
   k = k * Pr / (1 + Pr) * F;
 }
 
+// d fo / d[M] of a fall-off reaction (k = k_inf fo, fo = Pr / (1 + Pr) F): the [M]-dependence of the rate
+// constant, which Rosenbrock methods need in the Jacobian for their order (chem_codegen.py derives the
+// same expression for the generated kernels)
+template <int S>
+__device__ __forceinline__ double falloff_dfo(const ChemMech& m, const Lane<S>& L, int r, double T, const double (&C)[S]) {
+  const int* id = m.idata + r * 8;
+  const double* d = m.dd + (long)r * m.ndd;
+  double M = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) M += d[17 + i] * C[i];
+  const double kinf = L.K(L.kf, r), k0 = L.K(L.k0, r);
+  const double Pr = k0 * M / kinf;
+  double F = 1.0, corr = 0.0;
+  if (id[0] == 3) {
+    const double a = d[12], T3 = d[13], T1 = d[14], T2 = d[15];
+    const double Fc = (1 - a) * exp(-T / T3) + a * exp(-T / T1) + (id[4] ? exp(-T2 / T) : 0.0);
+    const double lFc = log10(fmax(Fc, 1e-300));
+    const double c = -0.4 - 0.67 * lFc, n = 0.75 - 1.27 * lFc;
+    const double lPr = log10(fmax(Pr, 1e-300));
+    const double u = n - 0.14 * (lPr + c);
+    const double f1 = (lPr + c) / u;
+    F = exp10(lFc / (1 + f1 * f1));
+    corr = F * 2.0 * lFc * f1 * n / ((1.0 + Pr) * (1.0 + f1 * f1) * (1.0 + f1 * f1) * u * u);
+  }
+  return k0 / kinf * (F / ((1.0 + Pr) * (1.0 + Pr)) - corr);
+}
+
 __device__ __forceinline__ double ipow(double c, double nu) {
   return nu == 1.0 ? c : (nu == 2.0 ? c * c : (nu == 3.0 ? c * c * c : pow(c, nu)));
 }
@@ -200,6 +228,16 @@ __device__ void build_matrix(const ChemMech& m, const Lane<S>& L, double T, cons
       }
       q0 = f - b;
     }
+    double qf = 0.0;   // fall-off: (d fo / d[M]) (k_inf prod_f - k_inf / Kc prod_b)
+    if (id[0] >= 2) {
+      const double kinf = L.K(L.kf, r);
+      double f = kinf, b = id[1] ? kinf * L.K(L.ikc, r) : 0.0;
+      for (int j = 0; j < 3; ++j) {
+        if (ix[j] >= 0) f *= ipow(cr[j], d[3 + j]);
+        if (ix[3 + j] >= 0) b *= ipow(cp[j], d[6 + j]);
+      }
+      qf = falloff_dfo<S>(m, L, r, T, C) * (f - b);
+    }
     // rows touched: reactants (-nu_r) and products (+nu_p)
     for (int a = 0; a < 6; ++a) {
       const int row = ix[a];   // reactant slots 0..2, product slots 3..5
@@ -210,6 +248,9 @@ __device__ void build_matrix(const ChemMech& m, const Lane<S>& L, double T, cons
       if (Mc != 0.0)
 #pragma unroll
         for (int j = 0; j < S; ++j) L.M(row, j) -= h * nu * d[17 + j] * q0;
+      if (qf != 0.0)
+#pragma unroll
+        for (int j = 0; j < S; ++j) L.M(row, j) -= h * nu * d[17 + j] * qf;
     }
   }
 }
