@@ -951,6 +951,7 @@ int dfmi_thermo_psip0(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x);
 int dfmi_thermo_correct_psip_rho(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); correct_psip_rho(ctx->x); }); }
 int dfmi_time_step(dfmi_ctx* ctx, int n_corr) { return guard([&] { require_ready(ctx->x); time_step(ctx->x, n_corr); }); }
 int dfmi_sync(dfmi_ctx*) { return 0; }
+int dfmi_hbm_copy_peak(dfmi_ctx*, double, int, double*) { return guard([&] { throw Error("dfmi (CPU-A): no device memory"); }); }
 
 int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
   return guard([&] {

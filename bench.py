@@ -119,27 +119,6 @@ def parse():
     return ap.parse_args()
 
 
-def hbm_copy_peak(device: int, gib: float = 4.0, reps: int = 10) -> float:
-    """Measured device-to-device copy bandwidth (GB/s, read + write bytes) of a gib-GiB buffer: the
-    STREAM-copy reference SURVEY 8(d) asks for beside the 8 TB/s datasheet peak"""
-    import torch
-    n = int(gib * (1 << 30)) // 8
-    a = torch.ones(n, dtype=torch.float64, device=f"cuda:{device}")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(device)
-    s.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e.record()
-    torch.cuda.synchronize(device)
-    gbs = 2.0 * 8 * n * reps / (s.elapsed_time(e) / 1e3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
-
-
 def host_cpu():
     """(usable cores, machine cores, CPU model string) of this host (the lscpu 'Model name' field)"""
     model = "unknown"
@@ -616,7 +595,7 @@ def main():
         "finite": finite,
     }
     if world == 1:   # the headline kernel against a measured copy peak as well as the datasheet's
-        peak_copy = hbm_copy_peak(local)
+        peak_copy = ctx.hbm_copy_peak(4.0, 20)     # dfmi_hbm_copy_peak: 16-B vector streaming copy
         out["roofline"]["measured_copy_peak_GBs"] = peak_copy
         out["roofline"]["frac_of_measured_copy_peak"] = out["roofline"]["achieved"] / peak_copy
     U0 = ctx.get_field("U", (3, m.n_cells)) if (rank == 0 and world == 1 and n == 128 and not args.no_flame) else None

@@ -592,6 +592,13 @@ int dfmi_kernel_time(dfmi_ctx* ctx, double* total_ms, int* launches) {
 
 int dfmi_sync(dfmi_ctx* ctx) { return guard([&] { DFMI_HIP(hipStreamSynchronize(ctx->x.stream)); }); }
 
+int dfmi_hbm_copy_peak(dfmi_ctx* ctx, double gib, int reps, double* gbs) {
+  return guard([&] {
+    DFMI_CHECK(gib > 0 && reps > 0 && gbs, "bad arguments");
+    *gbs = hbm_copy_gbs(ctx->x, (size_t)(gib * (1ull << 30)), reps);
+  });
+}
+
 int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
   return guard([&] {
     Ctx& x = ctx->x;

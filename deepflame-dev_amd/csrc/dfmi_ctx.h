@@ -290,6 +290,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
 // dnn.hip
 void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* params, const double* xmu,
                 const double* xstd, const double* ymu, const double* ystd, double T_react, double dt_infer);
+double hbm_copy_gbs(Ctx& x, size_t bytes, int reps);   // measured device copy bandwidth (fv_kernels.hip)
 void dnn_prepare(Ctx& x);   // reacting-cell compaction + count read-back, ahead of dnn_solve
 void dnn_solve(Ctx& x, const char* rho_field);   // RR scaled by rho_field (reference: d_rho_old, dfYEqn.cu:449)
 // chem.hip

@@ -1486,6 +1486,31 @@ void zero_d_step(Ctx& x, double dt) {
   thermo_rho_from_psi(x);
 }
 
+// ---- measured HBM copy peak (diagnostic): 16-B vector loads/stores, grid-stride, enough blocks to fill
+// the chip; read + write bytes / time. The reference point for `roofline.achieved` beside the datasheet.
+__global__ void __launch_bounds__(256) k_stream_copy(long n, const double2* __restrict__ a, double2* __restrict__ b) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+double hbm_copy_gbs(Ctx& x, size_t bytes, int reps) {
+  const long n = (long)(bytes / sizeof(double2));
+  DevBuf<double2> a, b;
+  a.alloc(n); b.alloc(n);
+  DFMI_HIP(hipMemsetAsync(a.p, 0, n * sizeof(double2), x.stream));
+  const dim3 g(8192), bl(256);
+  hipLaunchKernelGGL(k_stream_copy, g, bl, 0, x.stream, n, (const double2*)a.p, b.p);
+  hipEvent_t e0, e1;
+  DFMI_HIP(hipEventCreate(&e0)); DFMI_HIP(hipEventCreate(&e1));
+  DFMI_HIP(hipEventRecord(e0, x.stream));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_stream_copy, g, bl, 0, x.stream, n, (const double2*)a.p, b.p);
+  DFMI_HIP(hipEventRecord(e1, x.stream));
+  DFMI_HIP(hipEventSynchronize(e1));
+  float ms = 0.0f;
+  DFMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+  return 2.0 * (double)n * sizeof(double2) * reps / (ms / 1e3) / 1e9;
+}
+
 void thermo_rho_from_psi(Ctx& x) {   // dfThermo::updateRho (dfThermo.cu:673-679)
   LAUNCH(k_mul, x.C, (long)x.C, x.f("p"), x.f("psi"), x.f("rho"));
   LAUNCH(k_mul, x.B, (long)x.B, x.f("boundary_p"), x.f("boundary_psi"), x.f("boundary_rho"));

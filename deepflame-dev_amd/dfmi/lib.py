@@ -57,6 +57,7 @@ SIGNATURES = {
     "dfmi_thermo_update_rho": [_P], "dfmi_thermo_psip0": [_P], "dfmi_thermo_correct_psip_rho": [_P],
     "dfmi_U_get_HbyA": [_P], "dfmi_p_process": [_P], "dfmi_post_time_step": [_P],
     "dfmi_time_step": [_P, C.c_int], "dfmi_sync": [_P],
+    "dfmi_hbm_copy_peak": [_P, C.c_double, C.c_int, _DP],
     "dfmi_assemble": [_P, C.c_char_p],
     "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
     "dfmi_get_solver_rows": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
@@ -357,6 +358,12 @@ class Context:
         else:
             self._call("dfmi_kernel_time_named", self.h, name.encode(), C.byref(ms), C.byref(n))
         return ms.value, n.value
+
+    def hbm_copy_peak(self, gib=4.0, reps=20):
+        """measured copy bandwidth, GB/s (read + write)"""
+        v = C.c_double()
+        self._call("dfmi_hbm_copy_peak", self.h, float(gib), int(reps), C.byref(v))
+        return v.value
 
     def sync(self):
         self._call("dfmi_sync", self.h)

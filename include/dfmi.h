@@ -139,6 +139,9 @@ int dfmi_post_time_step(dfmi_ctx* ctx);         /* dfMatrixDataBase::postTimeSte
 /* the whole loop body above with n_corr pressure correctors */
 int dfmi_time_step(dfmi_ctx* ctx, int n_corr);   /* non-zero also when chemistry hit its step limit */
 int dfmi_sync(dfmi_ctx* ctx);
+/* diagnostic: measured device-memory copy bandwidth (read + write GB/s) of a gib-GiB buffer copied reps
+ * times by a 16-B-vector streaming kernel -- the measured peak beside the datasheet's 8 TB/s */
+int dfmi_hbm_copy_peak(dfmi_ctx* ctx, double gib, int reps, double* gbs);
 /* correct_boundary_conditions_{scalar,vector} (dfMatrixOpBase.cu:2402-2491) for field in
  * {"U","p","he","T","rho","K","Y"} using that field's patch types */
 int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field);
