@@ -1,0 +1,70 @@
+"""BASELINE config 3 at its full size (128^3 = 2,097,152 cells, the reference TGV fields tiled, Burke 9
+species, ROS3 chemistry), checked through properties that do not need the oracle at this size:
+
+- determinism: the same state stepped twice gives bitwise identical fields (no floating-point atomics,
+  fixed-order reductions) -- the property that makes the bitwise oracle tests meaningful at scale;
+- discrete conservation: rhoEqn on a periodic box changes the total mass only by rounding
+  (sum over cells of the face-flux divergence vanishes), species sum to 1 in every cell, T stays in
+  the physical range and the solvers meet their tolerance.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _headline(n=128):
+    sys.path.insert(0, ROOT)
+    from bench import MECHS, reference_fields
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.kinetics import parse_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, MECHS["burke9"][0]))
+    t = read_thermo_table(os.path.join(GOLDEN, MECHS["burke9"][1]), ym["species"])
+    m = hex_box(n, n, n, lengths=(2 * np.pi * 1e-3,) * 3)
+    ctx = Context(0)
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6)
+    ctx.chem_set_mechanism(parse_mechanism(os.path.join(GOLDEN, MECHS["burke9"][0])))
+    ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
+    f = reference_fields(m, ym["species"])
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"])
+    return ctx, m, t
+
+
+def test_full_size_steps_are_deterministic_and_conservative():
+    from dfmi import case
+    ctx, m, t = _headline()
+    C, S = m.n_cells, t.S
+    ctx.time_step(2)                                   # develop the state a little
+    st = case.pull_state(ctx, m, S)
+    runs = []
+    for _ in range(2):
+        case.push_state(ctx, st)
+        ctx.set_field("chem_stats", np.zeros((3, C)))
+        ctx.time_step(2)
+        runs.append({n: ctx.get_field(n, (C,)) for n in ("T", "p", "rho", "he")} |
+                    {"U": ctx.get_field("U", (3, C)), "Y": ctx.get_field("Y", (S, C))})
+    for k in runs[0]:
+        assert np.array_equal(runs[0][k], runs[1][k]), k
+    T, Y = runs[0]["T"], runs[0]["Y"]
+    assert np.isfinite(T).all() and 290.0 < T.min() and T.max() < 2600.0
+    assert np.abs(Y.sum(axis=0) - 1.0).max() < 1e-12 and Y.min() >= 0.0
+    for e in ("U", "Y", "E", "p"):
+        it, r0, rel = ctx.solver_stats(e)
+        assert rel <= 1e-5 or it == 20, (e, it, rel)
+    # rhoEqn alone: sum(rho V) is conserved on the periodic box (divergence of the face fluxes sums to 0)
+    ctx.call("pre_time_step")
+    rho_old = ctx.get_field("rho_old", (C,))
+    ctx.call("rho_process")
+    rho = ctx.get_field("rho", (C,))
+    V = m.volume
+    assert abs(np.sum(rho * V) - np.sum(rho_old * V)) <= 1e-13 * np.sum(rho_old * V)
+    assert np.abs(rho - rho_old).max() > 0.0           # the fluxes were not zero
+    ctx.close()
