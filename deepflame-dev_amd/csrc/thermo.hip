@@ -21,14 +21,17 @@ constexpr double SQRT8 = 2.8284271247461903;
 struct TC {   // coefficient table pointers
   const double *W, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;
   int sym;      // bdiff[i][j] == bdiff[j][i] bitwise (binary diffusion fits are symmetric)
+  const double *nasaT, *bdiffT, *vc1T, *vc2T;   // species-minor copies (Thermo::dnasaT ...), coop kernel
 };
 
-// NASA7 polynomials of species i at T: cp/R and h/(R T)
-__device__ __forceinline__ void nasa_cp_h(const double* a, double T, double& cpR, double& hRT) {
-  const int o = (T > a[0]) ? 1 : 8;
+// NASA7 polynomials of species i at T: cp/R and h/(R T); coefficient k at a[k * st] (st = 1: the
+// species-major table, st = S: the species-minor copy)
+__device__ __forceinline__ void nasa_cp_h(const double* a, double T, double& cpR, double& hRT, int st = 1) {
+  const int o = ((T > a[0]) ? 1 : 8) * st;
   const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;
-  cpR = a[o] + a[o + 1] * T + a[o + 2] * T2 + a[o + 3] * T3 + a[o + 4] * T4;
-  hRT = a[o] + a[o + 1] * T / 2 + a[o + 2] * T2 / 3 + a[o + 3] * T3 / 4 + a[o + 4] * T4 / 5 + a[o + 5] / T;
+  const double a0 = a[o], a1 = a[o + st], a2 = a[o + 2 * st], a3 = a[o + 3 * st], a4 = a[o + 4 * st], a5 = a[o + 5 * st];
+  cpR = a0 + a1 * T + a2 * T2 + a3 * T3 + a4 * T4;
+  hRT = a0 + a1 * T / 2 + a2 * T2 / 3 + a3 * T3 / 4 + a4 * T4 / 5 + a5 / T;
 }
 
 // mixture h and cp at T, ryw[i] = R Y_i / W_i
@@ -239,23 +242,39 @@ __global__ void k_energy_gradient(MeshView m, TC t, const int8_t* __restrict__ t
 
 
 // ---------------------------------------------------------------- large mechanisms (S > 16)
-// One cell per group of TG = 16 lanes (4 cells per wave, 16 per workgroup): lane l owns species
-// l, l + 16, l + 32, l + 48 in registers; the O(S^2) Wilke and mixture-averaged-diffusion rows are
-// split over the lanes, reading the cell's mole fractions and species viscosities from LDS; mixture
-// sums are butterfly reductions inside the group (every lane ends with the identical value, so the
-// Newton iteration and the group's control flow stay uniform). Same formulas as thermo_point; only
-// the summation order of the mixture sums differs (agrees with the sequential oracle to rounding).
-constexpr int TG = 16, TCB = 256, TCELLS = TCB / TG, SMAX = 64, SPL = SMAX / TG;
+// A group of TG = 16 lanes evaluates NCB cells together: lane l owns species l, l + 16, l + 32,
+// l + 48 of all NCB cells in registers. The O(S^2) Wilke and mixture-averaged-diffusion rows are
+// split over the lanes; every pair-coefficient load (vc1, vc2, the 5 binary-diffusion fit
+// coefficients, from the species-minor tables so a group's load is one contiguous run) is used by
+// the NCB cells at once -- with one cell per group the kernel was bound by those loads through the
+// vector L1 (measured 13 ms per 2M cells x 53 species). The cells' mole fractions and species
+// viscosities sit in LDS; mixture sums are butterfly reductions inside the group (every lane ends
+// with the identical value, so each cell's Newton iteration and control flow stay uniform over its
+// group). Same formulas as thermo_point; the summation order of the mixture sums and the
+// contraction of the polynomial products into FMAs differ (agrees with the sequential oracle to
+// rounding: the tests hold it to 1e-12).
+constexpr int TCB = 256, SMAX = 64;
 
+template <int TG>
 __device__ __forceinline__ double gsum(double v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+#pragma unroll
+  for (int o = 1; o < TG; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
+// 1/x from the hardware reciprocal estimate refined by two Newton steps (correctly rounded in all
+// but rare last-bit cases; x is a positive normal number here): a short dependency chain in place of
+// the IEEE division sequence, which left the pair loops latency-bound
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
 // slots == nullptr: cells (index = cell, stride n); otherwise boundary slots with per-slot types
+template <int TG, int NCB>
 __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fixT_all, const int8_t* __restrict__ ty,
     const int8_t* __restrict__ sprim, const int* __restrict__ bfc, long Cc, const double* __restrict__ cT,
     const double* __restrict__ che, const double* __restrict__ cpsi, const double* __restrict__ crho,
@@ -263,161 +282,296 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     const double* __restrict__ chai, double* __restrict__ T, double* __restrict__ he, const double* __restrict__ p,
     const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho, double* __restrict__ mu,
     double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
-  __shared__ double sX[TCELLS][SMAX], sS[TCELLS][SMAX], sR[TCELLS][SMAX];
+#pragma clang fp contract(fast)
+  constexpr int GPB = TCB / TG, SPL = SMAX / TG;      // groups per block, species per lane
+  constexpr int CPB = GPB * NCB;                      // cells per block
+  // per-cell rows (+1: groups on distinct banks); a group only touches its own NCB rows except in the
+  // block-wide transposes that load Y and store rhoD/hai with cell-contiguous (coalesced) accesses
+  __shared__ double sX[CPB][SMAX + 1], sR[CPB][SMAX + 1];
+  __shared__ int sLive[CPB];
   const int grp = threadIdx.x / TG, l = threadIdx.x % TG;
   const int blk = ty ? (int)blockIdx.x : xcd_block();
-  const int idx = blk * TCELLS + grp;
-  bool live = idx < n;
-  bool fixT = fixT_all != 0;
-  if (live && ty) {
-    const int tt = ty[idx];
-    if (tt == EMPTY) live = false;
-    else if (bc_proc(tt) && !sprim[idx]) {   // processor [internal n] slot: copy the cell's values
-      const int c = bfc[idx];
-      if (l == 0) { T[idx] = cT[c]; he[idx] = che[c]; psi[idx] = cpsi[c]; rho[idx] = crho[c]; mu[idx] = cmu[c]; alpha[idx] = calpha[c]; }
-      for (int i = l; i < S; i += TG) { rhoD[(long)i * n + idx] = crhoD[i * Cc + c]; hai[(long)i * n + idx] = chai[i * Cc + c]; }
-      live = false;
-    } else if (bc_fixes_value(tt)) fixT = true;
+  const long base = (long)blk * CPB;
+  for (int e = threadIdx.x; e < CPB * S; e += TCB) {
+    const int sp = e / CPB, cl = e % CPB;
+    sX[cl][sp] = base + cl < n ? Y[(long)sp * n + base + cl] : 0.0;
   }
-  // species owned by this lane; groups without work evaluate a dummy state (uniform barriers below)
-  double y[SPL], X[SPL], ryw[SPL];
-  double sum = 0.0;
+  __syncthreads();
+  int idx[NCB];
+  bool live[NCB], fixT[NCB];
 #pragma unroll
-  for (int q = 0; q < SPL; ++q) {
-    const int i = q * TG + l;
-    y[q] = (i < S) ? (live ? Y[(long)i * n + idx] : (i == 0 ? 1.0 : 0.0)) : 0.0;
-    if (i < S) sum += y[q] / t.W[i];
+  for (int c = 0; c < NCB; ++c) {
+    idx[c] = (blk * GPB + grp) * NCB + c;
+    live[c] = idx[c] < n;
+    fixT[c] = fixT_all != 0;
+    if (live[c] && ty) {
+      const int k = idx[c], tt = ty[k];
+      if (tt == EMPTY) live[c] = false;
+      else if (bc_proc(tt) && !sprim[k]) {   // processor [internal n] slot: copy the cell's values
+        const int cc = bfc[k];
+        if (l == 0) { T[k] = cT[cc]; he[k] = che[cc]; psi[k] = cpsi[cc]; rho[k] = crho[cc]; mu[k] = cmu[cc]; alpha[k] = calpha[cc]; }
+        for (int i = l; i < S; i += TG) { rhoD[(long)i * n + k] = crhoD[i * Cc + cc]; hai[(long)i * n + k] = chai[i * Cc + cc]; }
+        live[c] = false;
+      } else if (bc_fixes_value(tt)) fixT[c] = true;
+    }
+    if (!live[c]) fixT[c] = true;
+    if (l == 0) sLive[grp * NCB + c] = live[c];
   }
-  sum = gsum(sum);
-  const double rsum = 1.0 / sum;
-  double wm = 0.0;
+  // species owned by this lane; cells without work evaluate a dummy state (uniform barriers below)
+  double X[NCB][SPL], ryw[NCB][SPL], Wm[NCB];
 #pragma unroll
-  for (int q = 0; q < SPL; ++q) {
-    const int i = q * TG + l;
-    X[q] = i < S ? y[q] / t.W[i] * rsum : 0.0;
-    ryw[q] = i < S ? R_GAS / t.W[i] * y[q] : 0.0;
-    if (i < S) wm += X[q] * t.W[i];
+  for (int c = 0; c < NCB; ++c) {
+    double y[SPL], sum = 0.0;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+      const int i = q * TG + l;
+      y[q] = (i < S) ? (live[c] ? sX[grp * NCB + c][i] : (i == 0 ? 1.0 : 0.0)) : 0.0;
+      if (i < S) sum += y[q] / t.W[i];
+    }
+    const double rsum = 1.0 / gsum<TG>(sum);
+    double wm = 0.0;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+      const int i = q * TG + l;
+      X[c][q] = i < S ? y[q] / t.W[i] * rsum : 0.0;
+      ryw[c][q] = i < S ? R_GAS / t.W[i] * y[q] : 0.0;
+      if (i < S) wm += X[c][q] * t.W[i];
+    }
+    Wm[c] = gsum<TG>(wm);
   }
-  const double Wm = gsum(wm);
-  double Tc = live ? T[idx] : 300.0, hc = live ? he[idx] : 0.0;
-  const double pc = live ? p[idx] : 101325.0;
-  if (!live) fixT = true;
-  auto hcp = [&](double TT, double& h, double& cp) {
-    double hh = 0.0, cc = 0.0;
+  double Tc[NCB], hc[NCB], pc[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    Tc[c] = live[c] ? T[idx[c]] : 300.0;
+    hc[c] = live[c] ? he[idx[c]] : 0.0;
+    pc[c] = live[c] ? p[idx[c]] : 101325.0;
+  }
+  // mixture h and cp of the cells flagged in `on` at temperatures TT (NASA coefficients loaded once
+  // per species for all NCB cells, both ranges; each cell picks its own)
+  auto hcp = [&](const double (&TT)[NCB], const bool (&on)[NCB], double (&h)[NCB], double (&cp)[NCB]) {
+    double hh[NCB], cc[NCB];
+    double P1[NCB], P2[NCB], P3[NCB], P4[NCB], Q1[NCB], Q2[NCB], Q3[NCB], Q4[NCB], RT[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      hh[c] = 0.0; cc[c] = 0.0;
+      const double T1 = TT[c], T2 = T1 * T1, T3 = T2 * T1, T4 = T3 * T1;
+      P1[c] = T1; P2[c] = T2; P3[c] = T3; P4[c] = T4;
+      Q1[c] = T1 * 0.5; Q2[c] = T2 / 3; Q3[c] = T3 * 0.25; Q4[c] = T4 / 5; RT[c] = 1.0 / T1;
+    }
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
       const int i = q * TG + l;
       if (i < S) {
-        double c1, h1;
-        nasa_cp_h(t.nasa + i * 15, TT, c1, h1);
-        hh += h1 * TT * ryw[q];
-        cc += c1 * ryw[q];
+        const double* a = t.nasaT + i;
+        const double tm = a[0];
+        double hi[6], lo[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) { hi[k] = a[(1 + k) * S]; lo[k] = a[(8 + k) * S]; }
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          const double T1 = TT[c];
+          const bool up = T1 > tm;
+          const double a0 = up ? hi[0] : lo[0], a1 = up ? hi[1] : lo[1], a2 = up ? hi[2] : lo[2];
+          const double a3 = up ? hi[3] : lo[3], a4 = up ? hi[4] : lo[4], a5 = up ? hi[5] : lo[5];
+          const double c1 = a0 + a1 * P1[c] + a2 * P2[c] + a3 * P3[c] + a4 * P4[c];
+          const double h1 = a0 + a1 * Q1[c] + a2 * Q2[c] + a3 * Q3[c] + a4 * Q4[c] + a5 * RT[c];
+          hh[c] += h1 * T1 * ryw[c][q];
+          cc[c] += c1 * ryw[c][q];
+        }
       }
     }
-    h = gsum(hh);
-    cp = gsum(cc);
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (on[c]) { h[c] = gsum<TG>(hh[c]); cp[c] = gsum<TG>(cc[c]); }
   };
-  double cpm;
-  if (fixT) {
-    hcp(Tc, hc, cpm);
-  } else {
-    double tt = Tc;
-    for (int it = 0; it < 20; ++it) {
-      double h, cp;
-      hcp(tt, h, cp);
-      const double dT = (h - hc) / cp;
-      tt -= dT;
-      if (fabs(h - hc) < 1e-7 || fabs(dT / tt) < 1e-7) break;
+  double cpm[NCB];
+  {
+    bool act[NCB], any = false;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { act[c] = !fixT[c]; any = any || act[c]; }
+    for (int it = 0; it < 20 && any; ++it) {
+      double h[NCB], cp[NCB];
+      hcp(Tc, act, h, cp);
+      any = false;
+#pragma unroll
+      for (int c = 0; c < NCB; ++c)
+        if (act[c]) {
+          const double dT = (h[c] - hc[c]) / cp[c];
+          Tc[c] -= dT;
+          if (fabs(h[c] - hc[c]) < 1e-7 || fabs(dT / Tc[c]) < 1e-7) act[c] = false;
+          any = any || act[c];
+        }
     }
-    Tc = tt;
-    double h_;
-    hcp(Tc, h_, cpm);
+    bool all[NCB];
+    double h[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { all[c] = true; h[c] = 0.0; }
+    hcp(Tc, all, h, cpm);
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (fixT[c]) hc[c] = h[c];
   }
-  const double lnT = log(Tc);
-  double poly[5];
-  poly[0] = 1.0; poly[1] = lnT; poly[2] = poly[1] * poly[1]; poly[3] = poly[1] * poly[2]; poly[4] = poly[2] * poly[2];
-  const double ps = Wm / (R_GAS * Tc);
-  const double rh = pc * ps;
-  double sv[SPL];
+  // from here on each result is stored as soon as it is known (short live ranges: NCB cells' state
+  // stays in registers without spilling)
+  double poly[NCB][5], sT[NCB], rdp[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const double lnT = log(Tc[c]);
+    poly[c][0] = 1.0; poly[c][1] = lnT; poly[c][2] = lnT * lnT; poly[c][3] = lnT * poly[c][2];
+    poly[c][4] = poly[c][2] * poly[c][2];
+    sT[c] = sqrt(Tc[c]);
+    const double ps = Wm[c] / (R_GAS * Tc[c]), rh = pc[c] * ps;
+    rdp[c] = rh / pc[c];
+    if (live[c] && l == 0) { const int k = idx[c]; T[k] = Tc[c]; he[k] = hc[c]; psi[k] = ps; rho[k] = rh; }
+  }
+  // species enthalpies hai (depend on T only)
+  double ha[NCB][SPL];
 #pragma unroll
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
-    double dp = 0.0;
-    if (i < S)
 #pragma unroll
-      for (int j = 0; j < 5; ++j) dp += t.visc[i * 5 + j] * poly[j];
-    sv[q] = dp;
-    if (i < S) { sX[grp][i] = X[q] * (1.0 / SQRT8); sS[grp][i] = dp; sR[grp][i] = 1.0 / dp; }
-  }
-  __syncthreads();
-  // Wilke rows
-  double mpart = 0.0;
+    for (int c = 0; c < NCB; ++c) ha[c][q] = 0.0;
+    if (i >= S) continue;
+    const double* a = t.nasaT + i;
+    const double tm = a[0], rw = R_GAS / t.W[i];
 #pragma unroll
-  for (int q = 0; q < SPL; ++q) {
-    const int i = q * TG + l;
-    if (i >= S) break;
-    double s2 = 0.0;
-    for (int j = 0; j < S; ++j) {
-      const double tmp = 1.0 + (sv[q] * sR[grp][j]) * t.vc2[i * S + j];
-      s2 += sX[grp][j] * t.vc1[i * S + j] * (tmp * tmp);
+    for (int c = 0; c < NCB; ++c) {
+      const double T1 = Tc[c], T2 = T1 * T1, T3 = T2 * T1, T4 = T3 * T1;
+      const int o = (T1 > tm) ? 1 : 8;
+      const double h1 = a[o * S] + a[(o + 1) * S] * (T1 * 0.5) + a[(o + 2) * S] * (T2 / 3) + a[(o + 3) * S] * (T3 * 0.25) +
+                        a[(o + 4) * S] * (T4 / 5) + a[(o + 5) * S] * (1.0 / T1);
+      ha[c][q] = h1 * T1 * rw;
     }
-    mpart += X[q] * (sv[q] * sv[q]) / s2;
   }
-  const double sT = sqrt(Tc);
-  const double mum = gsum(mpart) * sT;
-  double sc = 0.0, sic = 0.0;
+  {
+    double sv[NCB][SPL];
 #pragma unroll
-  for (int q = 0; q < SPL; ++q) {
-    const int i = q * TG + l;
-    if (i >= S) break;
-    double dp = 0.0;
+    for (int q = 0; q < SPL; ++q) {
+      const int i = q * TG + l;
+      double vc[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) dp += t.cond[i * 5 + j] * poly[j];
-    const double lam = dp * sT;
-    sc += X[q] * lam;
-    sic += X[q] / lam;
+      for (int k = 0; k < 5; ++k) vc[k] = i < S ? t.visc[i * 5 + k] : 0.0;
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        double dp = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dp += vc[k] * poly[c][k];
+        sv[c][q] = dp;
+        if (i < S) { sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8); sR[grp * NCB + c][i] = 1.0 / dp; }
+      }
+    }
+    __syncthreads();
+    // Wilke rows
+    double mpart[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) mpart[c] = 0.0;
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+      const int i = q * TG + l;
+      if (i >= S) break;
+      double s2[NCB];
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) s2[c] = 0.0;
+      for (int j = 0; j < S; ++j) {
+        const double v2 = t.vc2T[j * S + i], v1 = t.vc1T[j * S + i];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          const double tmp = 1.0 + (sv[c][q] * sR[grp * NCB + c][j]) * v2;
+          s2[c] += sX[grp * NCB + c][j] * v1 * (tmp * tmp);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) mpart[c] += X[c][q] * (sv[c][q] * sv[c][q]) / s2[c];
+    }
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const double mum = gsum<TG>(mpart[c]) * sT[c];
+      if (live[c] && l == 0) mu[idx[c]] = mum;
+    }
   }
-  sc = gsum(sc);
-  sic = gsum(sic);
-  const double al = 0.5 * (sc + 1.0 / sic) / cpm;
+  {
+    double sc[NCB], sic[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { sc[c] = 0.0; sic[c] = 0.0; }
+#pragma unroll
+    for (int q = 0; q < SPL; ++q) {
+      const int i = q * TG + l;
+      if (i >= S) break;
+      double kc[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) kc[k] = t.cond[i * 5 + k];
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        double dp = 0.0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dp += kc[k] * poly[c][k];
+        const double lam = dp * sT[c];
+        sc[c] += X[c][q] * lam;
+        sic[c] += X[c][q] / lam;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const double al = 0.5 * (gsum<TG>(sc[c]) + 1.0 / gsum<TG>(sic[c])) / cpm[c];
+      if (live[c] && l == 0) alpha[idx[c]] = al;
+    }
+  }
   __syncthreads();   // mole fractions (unscaled) for the diffusion rows
 #pragma unroll
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
-    if (i < S) sX[grp][i] = X[q];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (i < S) sX[grp * NCB + c][i] = X[c][q];
   }
   __syncthreads();
-  const double powT = Tc * sT, rdp = rh / pc;
-  double rd[SPL], ha[SPL];
+  double rpT[NCB], rdv[NCB][SPL];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) rpT[c] = 1.0 / (Tc[c] * sT[c]);
 #pragma unroll
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
-    rd[q] = 0.0; ha[q] = 0.0;
-    if (i >= S) continue;
-    if (!(X[q] + 1e-10 > 1.)) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int j = 0; j < S; ++j) {
-        if (j == i) continue;
-        const double* bd = t.bdiff + (i * S + j) * 5;
-        const double tmp = bd[0] * poly[0] + bd[1] * poly[1] + bd[2] * poly[2] + bd[3] * poly[3] + bd[4] * poly[4];
-        const double inv = 1.0 / (tmp * powT);
-        const double xj = sX[grp][j];
-        s1 += xj * inv;
-        s2 += xj * t.W[j] * inv;
+    if (i >= S) break;
+    double s1[NCB], s2[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { s1[c] = 0.0; s2[c] = 0.0; }
+    for (int j = 0; j < S; ++j) {
+      const double* bd = t.bdiffT + j * 5 * S + i;
+      const double b0 = bd[0], b1 = bd[S], b2 = bd[2 * S], b3 = bd[3 * S], b4 = bd[4 * S];
+      const double wj = t.W[j];
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const double tmp = b0 * poly[c][0] + b1 * poly[c][1] + b2 * poly[c][2] + b3 * poly[c][3] + b4 * poly[c][4];
+        const double inv = rpT[c] * rcp_nr(tmp);    // 1 / D_ij, D_ij = T^1.5 poly(ln T)
+        const double xj = j == i ? 0.0 : sX[grp * NCB + c][j];
+        s1[c] += xj * inv;
+        s2[c] += xj * wj * inv;
       }
-      const double q2 = s2 * (X[q] / (Wm - X[q] * t.W[i]));
-      rd[q] = 1 / (s1 + q2) * rdp;
     }
-    double c1, h1;
-    nasa_cp_h(t.nasa + i * 15, Tc, c1, h1);
-    ha[q] = h1 * Tc * (R_GAS / t.W[i]);
-  }
-  if (!live) return;
-  if (l == 0) { T[idx] = Tc; he[idx] = hc; psi[idx] = ps; rho[idx] = rh; mu[idx] = mum; alpha[idx] = al; }
 #pragma unroll
-  for (int q = 0; q < SPL; ++q) {
+    for (int c = 0; c < NCB; ++c) {
+      double rd = 0.0;
+      if (!(X[c][q] + 1e-10 > 1.)) {
+        const double q2 = s2[c] * (X[c][q] / (Wm[c] - X[c][q] * t.W[i]));
+        rd = 1 / (s1[c] + q2) * rdp[c];
+      }
+      rdv[c][q] = rd;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < SPL; ++q) {   // the group's own rows (read only by this group, all reads done)
     const int i = q * TG + l;
-    if (i < S) { rhoD[(long)i * n + idx] = rd[q]; hai[(long)i * n + idx] = ha[q]; }
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (i < S) { sX[grp * NCB + c][i] = rdv[c][q]; sR[grp * NCB + c][i] = ha[c][q]; }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < CPB * S; e += TCB) {
+    const int sp = e / CPB, cl = e % CPB;
+    if (base + cl < n && sLive[cl]) {
+      rhoD[(long)sp * n + base + cl] = sX[cl][sp];
+      hai[(long)sp * n + base + cl] = sR[cl][sp];
+    }
   }
 }
 
@@ -454,6 +608,21 @@ void thermo_upload(Ctx& x) {
   t.dbdiff.upload(t.bdiff, x.stream);
   t.dvc1.upload(t.vc1, x.stream);
   t.dvc2.upload(t.vc2, x.stream);
+  const int S = t.S;
+  std::vector<double> nT(15 * S), bT(5 * S * S), v1(S * S), v2(S * S);
+  for (int i = 0; i < S; ++i) {
+    for (int k = 0; k < 15; ++k) nT[k * S + i] = t.nasa[i * 15 + k];
+    for (int j = 0; j < S; ++j) {
+      for (int k = 0; k < 5; ++k) bT[(j * 5 + k) * S + i] = t.bdiff[(i * S + j) * 5 + k];
+      v1[j * S + i] = t.vc1[i * S + j];
+      v2[j * S + i] = t.vc2[i * S + j];
+    }
+  }
+  t.dnasaT.upload(nT, x.stream);
+  t.dbdiffT.upload(bT, x.stream);
+  t.dvc1T.upload(v1, x.stream);
+  t.dvc2T.upload(v2, x.stream);
+  DFMI_HIP(hipStreamSynchronize(x.stream));   // the staging vectors above go out of scope
 }
 
 void thermo_energy_gradient(Ctx& x) {
@@ -464,7 +633,7 @@ void thermo_energy_gradient(Ctx& x) {
   bool any = false;
   for (int p = 0; p < x.P; ++p) any = any || pt[p] == GRADIENT_ENERGY;
   if (!any) return;   // the field stays zero
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0};
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                  \
   hipLaunchKernelGGL(k_energy_gradient<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t, x.st("he"), \
@@ -491,7 +660,7 @@ void thermo_correct(Ctx& x, bool from_T) {
     for (int j = 0; j < th.S && sym; ++j)
       for (int k = 0; k < 5; ++k)
         if (th.bdiff[(i * th.S + j) * 5 + k] != th.bdiff[(j * th.S + i) * 5 + k]) { sym = 0; break; }
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym};
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                   \
   do {                                                                                                            \
@@ -508,22 +677,38 @@ void thermo_correct(Ctx& x, bool from_T) {
   } while (0)
   if (species_generic(x.S)) {
     DFMI_CHECK(x.S <= SMAX, "thermo: at most 64 species");
-    if (x.C > 0) {
-      KScope _ks(x, "k_thermo_cells");
-      hipLaunchKernelGGL(k_thermo_coop, dim3(blocks_for(x.C, TCELLS)), dim3(TCB), 0, x.stream, x.C, x.S, t, (int)from_T,
-                         (const int8_t*)nullptr, (const int8_t*)nullptr, (const int*)nullptr, 0L, (const double*)nullptr,
-                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr, (const double*)nullptr,
-                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr, x.f("T"), x.f("he"),
-                         x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), x.f("rhoD"), x.f("hai"));
-    }
-    DFMI_HIP(hipGetLastError());
-    if (x.B > 0)
-      hipLaunchKernelGGL(k_thermo_coop, dim3(blocks_for(x.B, TCELLS)), dim3(TCB), 0, x.stream, x.B, x.S, t, (int)from_T,
-                         x.st("T"), m.sprim, m.bfc, (long)x.C, x.f("T"), x.f("he"), x.f("psi"), x.f("rho"), x.f("mu"),
-                         x.f("alpha"), x.f("rhoD"), x.f("hai"), x.f("boundary_T"), x.f("boundary_he"),
-                         x.f("boundary_p"), x.f("boundary_Y"), x.f("boundary_psi"), x.f("boundary_rho"),
-                         x.f("boundary_mu"), x.f("boundary_alpha"), x.f("boundary_rhoD"), x.f("boundary_hai"));
-    DFMI_HIP(hipGetLastError());
+    // lanes per cell group and cells per group (DFMI_THERMO_COOP=TGxNCB: 16x1 16x2 16x4 64x2 64x4 64x8)
+    const char* e = std::getenv("DFMI_THERMO_COOP");
+    const std::string cfg = e ? e : "64x4";
+#define COOP(TG, NCB)                                                                                                  \
+  do {                                                                                                            \
+    constexpr int CPB = TCB / TG * NCB;                                                                           \
+    if (x.C > 0) {                                                                                                \
+      KScope _ks(x, "k_thermo_cells");                                                                            \
+      hipLaunchKernelGGL((k_thermo_coop<TG, NCB>), dim3(blocks_for(x.C, CPB)), dim3(TCB), 0, x.stream, x.C, x.S, t,     \
+                         (int)from_T, (const int8_t*)nullptr, (const int8_t*)nullptr, (const int*)nullptr, 0L,    \
+                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr,                 \
+                         (const double*)nullptr, (const double*)nullptr, (const double*)nullptr,                 \
+                         (const double*)nullptr, (const double*)nullptr, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), \
+                         x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), x.f("rhoD"), x.f("hai"));              \
+    }                                                                                                             \
+    DFMI_HIP(hipGetLastError());                                                                                  \
+    if (x.B > 0)                                                                                                  \
+      hipLaunchKernelGGL((k_thermo_coop<TG, NCB>), dim3(blocks_for(x.B, CPB)), dim3(TCB), 0, x.stream, x.B, x.S, t,     \
+                         (int)from_T, x.st("T"), m.sprim, m.bfc, (long)x.C, x.f("T"), x.f("he"), x.f("psi"),      \
+                         x.f("rho"), x.f("mu"), x.f("alpha"), x.f("rhoD"), x.f("hai"), x.f("boundary_T"),         \
+                         x.f("boundary_he"), x.f("boundary_p"), x.f("boundary_Y"), x.f("boundary_psi"),           \
+                         x.f("boundary_rho"), x.f("boundary_mu"), x.f("boundary_alpha"), x.f("boundary_rhoD"),    \
+                         x.f("boundary_hai"));                                                                    \
+    DFMI_HIP(hipGetLastError());                                                                                  \
+  } while (0)
+    if (cfg == "16x1") COOP(16, 1);
+    else if (cfg == "16x2") COOP(16, 2);
+    else if (cfg == "16x4") COOP(16, 4);
+    else if (cfg == "64x2") COOP(64, 2);
+    else if (cfg == "64x8") COOP(64, 8);
+    else COOP(64, 4);
+#undef COOP
   } else switch (x.S) {
     case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break;
     case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break;
