@@ -796,6 +796,8 @@ void set_comm(Ctx& x, int nranks, int rank, const int* neighb) {
   x.nranks = nranks;
   x.rank = rank;
   x.peer.assign(neighb, neighb + x.P);
+  const char* e = std::getenv("DFMI_HALO_OVERLAP");   // overlapped solver halos (default off)
+  x.halo_overlap = e && std::atoi(e) != 0;
 }
 // the exchange lists need the boundary topology: built now, or at the end of
 // dfmi_init_constant_fields_boundary (every rank reaches both points in the same order)

@@ -176,7 +176,11 @@ struct Ctx {
     bool ready = false;
     DevBuf<int> col;             // column: cell id, or C + halo index for a processor face
     DevBuf<int> src;             // coefficient: 2f = lower[f], 2f+1 = upper[f], -(b+1) = -boundaryCoeffs[b]
+    DevBuf<int8_t> bflag;        // [C] 1: the row has a processor (halo) column
+    DevBuf<int> brow;            // those rows, ascending
+    int nb = 0;
   } ell;
+  bool halo_overlap = false;     // DFMI_HALO_OVERLAP=1: solver halo exchanges overlap the interior rows
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
   Chem chem;
   Dnn dnn;
@@ -229,7 +233,7 @@ struct KScope {
   Ctx& x;
   int idx;
   static int match(const std::vector<std::string>& ts, const char* name) {   // template arguments ignored
-    if (ts.empty()) return -1;
+    if (ts.empty() || !name) return -1;
     while (*name == '(') ++name;
     size_t n = 0;
     while (name[n] && name[n] != '<') ++n;
@@ -316,6 +320,11 @@ struct HaloItem {
 };
 bool halo_active(const Ctx& x);
 void halo_update(Ctx& x, const HaloItem* items, int n);
+// overlapped form (solver SpMVs, Ctx::halo_overlap): the exchange runs on the halo's comm stream between
+// halo_begin and halo_end; the compute stream meanwhile runs only work that touches no halo entry
+bool halo_overlap(const Ctx& x);
+void halo_begin(Ctx& x, const HaloItem* items, int n);
+void halo_end(Ctx& x);
 inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
   if (!halo_active(x)) return;
   std::vector<HaloItem> it;

@@ -27,7 +27,7 @@ namespace dfmi {
 struct Transport {
   virtual ~Transport() = default;
   // per peer i: send cnt[i] doubles from sbuf+off[i], receive cnt[i] doubles into rbuf+off[i]
-  virtual void sendrecv(Ctx& x, const double* sbuf, double* rbuf, const std::vector<int>& peers,
+  virtual void sendrecv(Ctx& x, hipStream_t st, const double* sbuf, double* rbuf, const std::vector<int>& peers,
                         const std::vector<long>& off, const std::vector<long>& cnt) = 0;
   virtual void allgather(Ctx& x, const double* s, double* r, long count) = 0;
 };
@@ -41,12 +41,12 @@ struct Transport {
 struct RcclTransport : Transport {
   ncclComm_t comm = nullptr;
   ~RcclTransport() override { if (comm) (void)ncclCommDestroy(comm); }
-  void sendrecv(Ctx& x, const double* sbuf, double* rbuf, const std::vector<int>& peers, const std::vector<long>& off,
-                const std::vector<long>& cnt) override {
+  void sendrecv(Ctx&, hipStream_t st, const double* sbuf, double* rbuf, const std::vector<int>& peers,
+                const std::vector<long>& off, const std::vector<long>& cnt) override {
     DFMI_NCCL(ncclGroupStart());
     for (size_t i = 0; i < peers.size(); ++i) {
-      DFMI_NCCL(ncclSend(sbuf + off[i], cnt[i], ncclDouble, peers[i], comm, x.stream));
-      DFMI_NCCL(ncclRecv(rbuf + off[i], cnt[i], ncclDouble, peers[i], comm, x.stream));
+      DFMI_NCCL(ncclSend(sbuf + off[i], cnt[i], ncclDouble, peers[i], comm, st));
+      DFMI_NCCL(ncclRecv(rbuf + off[i], cnt[i], ncclDouble, peers[i], comm, st));
     }
     DFMI_NCCL(ncclGroupEnd());
   }
@@ -83,29 +83,29 @@ struct LocalTransport : Transport {
     (void)hipEventDestroy(hub->ev1[rank]);
     (void)hipEventDestroy(hub->ev2[rank]);
   }
-  void finish(Ctx& x) {   // nobody reuses its send buffer before every peer has copied out of it
+  void finish(hipStream_t st) {   // nobody reuses its send buffer before every peer has copied out of it
     Hub& h = *hub;
-    DFMI_HIP(hipEventRecord(h.ev2[rank], x.stream));
+    DFMI_HIP(hipEventRecord(h.ev2[rank], st));
     h.barrier();
-    for (int q = 0; q < h.n; ++q) if (q != rank) DFMI_HIP(hipStreamWaitEvent(x.stream, h.ev2[q], 0));
+    for (int q = 0; q < h.n; ++q) if (q != rank) DFMI_HIP(hipStreamWaitEvent(st, h.ev2[q], 0));
     h.barrier();
   }
-  void sendrecv(Ctx& x, const double* sbuf, double* rbuf, const std::vector<int>& peers, const std::vector<long>& off,
-                const std::vector<long>& cnt) override {
+  void sendrecv(Ctx&, hipStream_t st, const double* sbuf, double* rbuf, const std::vector<int>& peers,
+                const std::vector<long>& off, const std::vector<long>& cnt) override {
     Hub& h = *hub;
     h.sb[rank] = sbuf; h.peers[rank] = peers; h.off[rank] = off;
-    DFMI_HIP(hipEventRecord(h.ev1[rank], x.stream));
+    DFMI_HIP(hipEventRecord(h.ev1[rank], st));
     h.barrier();
     for (size_t i = 0; i < peers.size(); ++i) {
       const int q = peers[i];
       const auto& qp = h.peers[q];
       const long j = std::find(qp.begin(), qp.end(), rank) - qp.begin();
       DFMI_CHECK(j < (long)qp.size(), "halo: peer does not list this rank");
-      DFMI_HIP(hipStreamWaitEvent(x.stream, h.ev1[q], 0));
+      DFMI_HIP(hipStreamWaitEvent(st, h.ev1[q], 0));
       DFMI_HIP(hipMemcpyAsync(rbuf + off[i], h.sb[q] + h.off[q][j], cnt[i] * sizeof(double), hipMemcpyDeviceToDevice,
-                              x.stream));
+                              st));
     }
-    finish(x);
+    finish(st);
   }
   void allgather(Ctx& x, const double* s, double* r, long count) override {
     Hub& h = *hub;
@@ -116,7 +116,7 @@ struct LocalTransport : Transport {
       if (q != rank) DFMI_HIP(hipStreamWaitEvent(x.stream, h.ev1[q], 0));
       DFMI_HIP(hipMemcpyAsync(r + (long)q * count, h.sb[q], count * sizeof(double), hipMemcpyDeviceToDevice, x.stream));
     }
-    finish(x);
+    finish(x.stream);
   }
 };
 
@@ -127,7 +127,16 @@ struct Halo {
   DevBuf<int> send_cells, recv_slots, h_off, h_cnt;   // per halo index
   DevBuf<double> sbuf, rbuf;
   std::vector<long> off, cnt;               // per peer, in doubles, for the current exchange
-  ~Halo() { delete tr; }
+  // overlapped exchanges (halo_begin / halo_end): pack, transfer and unpack run on their own stream
+  hipStream_t cs = nullptr;
+  hipEvent_t ev_start = nullptr, ev_done = nullptr;
+  bool pending = false;
+  ~Halo() {
+    delete tr;
+    if (cs) { (void)hipStreamSynchronize(cs); (void)hipStreamDestroy(cs); }
+    if (ev_start) (void)hipEventDestroy(ev_start);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+  }
 };
 
 void halo_destroy(Halo* h) { delete h; }
@@ -163,31 +172,37 @@ __global__ void k_unpack(int H, int K, PackArgs a, const int* __restrict__ slots
   a.dst[k][idx] = v;
 }
 
-void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<double*>& dst, bool to_slots) {
+// pack, send/receive and unpack on stream st (x.stream: in order with the compute; the comm stream:
+// overlapped, the kernel timers are not used there)
+void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<double*>& dst, bool to_slots,
+              hipStream_t st) {
   Halo& h = *x.halo;
+  const bool timed = st == x.stream;
   const int K = (int)src.size();
   for (int k0 = 0; k0 < K; k0 += MAXK) {
     const int kk = std::min(MAXK, K - k0);
     PackArgs a{};
     for (int k = 0; k < kk; ++k) { a.src[k] = src[k0 + k]; a.dst[k] = dst[k0 + k]; }
     dim3 g(blocks_for(x.H, 256), kk);
-    { KScope _ks(x, "k_halo_pack"); hipLaunchKernelGGL(k_pack, g, dim3(256), 0, x.stream, x.H, kk, a, h.send_cells.p, h.h_off.p, h.h_cnt.p, h.sbuf.p); }
+    {
+      KScope _ks(x, timed ? "k_halo_pack" : nullptr);
+      hipLaunchKernelGGL(k_pack, g, dim3(256), 0, st, x.H, kk, a, h.send_cells.p, h.h_off.p, h.h_cnt.p, h.sbuf.p);
+    }
     DFMI_HIP(hipGetLastError());
     h.off.resize(h.peers.size()); h.cnt.resize(h.peers.size());
     for (size_t i = 0; i < h.peers.size(); ++i) { h.off[i] = (long)kk * h.pf_off[i]; h.cnt[i] = (long)kk * h.pf_cnt[i]; }
-    h.tr->sendrecv(x, h.sbuf.p, h.rbuf.p, h.peers, h.off, h.cnt);
-    { KScope _ks(x, "k_halo_unpack"); hipLaunchKernelGGL(k_unpack, g, dim3(256), 0, x.stream, x.H, kk, a, to_slots ? h.recv_slots.p : nullptr, x.C, h.h_off.p, h.h_cnt.p, h.rbuf.p); }
+    h.tr->sendrecv(x, st, h.sbuf.p, h.rbuf.p, h.peers, h.off, h.cnt);
+    {
+      KScope _ks(x, timed ? "k_halo_unpack" : nullptr);
+      hipLaunchKernelGGL(k_unpack, g, dim3(256), 0, st, x.H, kk, a, to_slots ? h.recv_slots.p : nullptr, x.C, h.h_off.p,
+                         h.h_cnt.p, h.rbuf.p);
+    }
     DFMI_HIP(hipGetLastError());
   }
 }
 
-}  // namespace
-
-void halo_update(Ctx& x, const HaloItem* items, int n) {
-  if (!halo_active(x)) return;
-  std::vector<const double*> src;
-  std::vector<double*> dst;
-  bool slots = true;
+void collect(const HaloItem* items, int n, std::vector<const double*>& src, std::vector<double*>& dst, bool& slots) {
+  slots = true;
   for (int i = 0; i < n; ++i) {
     if (i == 0) slots = items[i].to_slots;
     DFMI_CHECK(items[i].to_slots == slots, "halo_update: mixed slot / vector destinations");
@@ -196,7 +211,49 @@ void halo_update(Ctx& x, const HaloItem* items, int n) {
       dst.push_back(items[i].dst + k * items[i].dstride);
     }
   }
-  if (!src.empty()) exchange(x, src, dst, slots);
+}
+
+}  // namespace
+
+void halo_update(Ctx& x, const HaloItem* items, int n) {
+  if (!halo_active(x)) return;
+  DFMI_CHECK(!x.halo->pending, "halo_update while an overlapped exchange is in flight");
+  std::vector<const double*> src;
+  std::vector<double*> dst;
+  bool slots = true;
+  collect(items, n, src, dst, slots);
+  if (!src.empty()) exchange(x, src, dst, slots, x.stream);
+}
+
+bool halo_overlap(const Ctx& x) { return halo_active(x) && x.halo_overlap; }
+
+// overlapped exchange: everything queued on x.stream so far (the values to send) completes before the
+// comm stream packs; the compute stream may run work that reads no halo entry (and writes none of the
+// sent vectors) until halo_end joins the comm stream back
+void halo_begin(Ctx& x, const HaloItem* items, int n) {
+  Halo& h = *x.halo;
+  DFMI_CHECK(!h.pending, "halo_begin: an overlapped exchange is already in flight");
+  if (!h.cs) {
+    DFMI_HIP(hipStreamCreateWithFlags(&h.cs, hipStreamNonBlocking));
+    DFMI_HIP(hipEventCreateWithFlags(&h.ev_start, hipEventDisableTiming));
+    DFMI_HIP(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming));
+  }
+  std::vector<const double*> src;
+  std::vector<double*> dst;
+  bool slots = true;
+  collect(items, n, src, dst, slots);
+  DFMI_HIP(hipEventRecord(h.ev_start, x.stream));
+  DFMI_HIP(hipStreamWaitEvent(h.cs, h.ev_start, 0));
+  if (!src.empty()) exchange(x, src, dst, slots, h.cs);
+  DFMI_HIP(hipEventRecord(h.ev_done, h.cs));
+  h.pending = true;
+}
+
+void halo_end(Ctx& x) {
+  Halo& h = *x.halo;
+  DFMI_CHECK(h.pending, "halo_end without halo_begin");
+  DFMI_HIP(hipStreamWaitEvent(x.stream, h.ev_done, 0));
+  h.pending = false;
 }
 
 void halo_allgather(Ctx& x, const double* send, double* recv, long count) {

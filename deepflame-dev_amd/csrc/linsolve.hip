@@ -64,7 +64,31 @@ template <int NV> __device__ __forceinline__ void red_sum(const Red& r, int s, d
 }
 
 // block partial of NV values -> partial[(s * nblk + blockIdx.x) * NV + k]
-template <int NV> __device__ __forceinline__ void block_partials(double (&v)[NV], double* partial, int s) {
+// Row sets of the halo-overlapped SpMVs (multi-rank, DFMI_HALO_OVERLAP=1): part 1 = the rows without a
+// processor column (they run while the halo exchange is in flight on the comm stream), part 2 = the
+// listed boundary rows (after it). Each part writes its block partials into its own half of a
+// [system][2 nblk] layout, which the consumer reduces in fixed order. part 0 = every row, one pass.
+struct RowSet {
+  int part = 0;
+  const int8_t* flag = nullptr;   // [C] 1: the row has a processor column
+  const int* list = nullptr;      // the boundary rows
+  int nb = 0;
+};
+__device__ __forceinline__ int rows_begin() { return xcd_block() * blockDim.x + threadIdx.x; }
+template <class F> __device__ __forceinline__ void for_rows(long C, const RowSet& rs, F&& f) {
+  const int stride = gridDim.x * blockDim.x;
+  if (rs.part == 2) {
+    for (int k = rows_begin(); k < rs.nb; k += stride) f(rs.list[k]);
+  } else {
+    for (int c = rows_begin(); c < C; c += stride) {
+      if (rs.part == 1 && rs.flag[c]) continue;
+      f(c);
+    }
+  }
+}
+
+template <int NV> __device__ __forceinline__ void block_partials(double (&v)[NV], double* partial, int s,
+                                                                const RowSet& rs = RowSet{}) {
   __shared__ double sh[NW][NV];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -74,7 +98,8 @@ template <int NV> __device__ __forceinline__ void block_partials(double (&v)[NV]
     double a = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) a += sh[w][threadIdx.x];
-    partial[((long)s * gridDim.x + blockIdx.x) * NV + threadIdx.x] = a;
+    const int gt = rs.part ? 2 * gridDim.x : gridDim.x, bo = rs.part == 2 ? gridDim.x : 0;
+    partial[((long)s * gt + bo + blockIdx.x) * NV + threadIdx.x] = a;
   }
 }
 
@@ -203,7 +228,8 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const 
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const int* __restrict__ col,
                                                    const double* __restrict__ val, int it, int max_iter, double tol,
-                                                   double abs_tol, Red red, double* scal, BV b, double* partial) {
+                                                   double abs_tol, Red red, double* scal, BV b, double* partial,
+                                                   RowSet rs) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (it > 0 && st[6] == 0.0) return;   // stopped earlier (uniform per block)
@@ -213,7 +239,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
   const double rho = it == 0 ? v2[1] : st[8];   // r0.r: initial, or the previous update's recurrence
   const double res0 = it == 0 ? res : st[4];
   const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || st[3] == 0.0));
-  if (leader()) {
+  if (leader() && rs.part != 2) {
     if (it == 0) st[4] = res;
     st[0] = rho;
     st[5] = res; st[7] = it;
@@ -222,13 +248,13 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
   if (stop) return;
   const double* vs = val + (long)s * W * C;
   double acc[1] = {0.0};
-  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for_rows(C, rs, [&](int c) {
     const long i = s * Ce + c;
     const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], b.p + s * Ce, c);
     b.v[i] = y;
     acc[0] += b.r0[i] * y;
-  }
-  block_partials<1>(acc, partial, s);
+  });
+  block_partials<1>(acc, partial, s, rs);
 }
 
 // multi-rank only: s = r - alpha v into sv, whose processor-boundary values the halo exchange sends
@@ -252,21 +278,21 @@ __global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double*
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, const int* __restrict__ col,
                                                    const double* __restrict__ val, Red red, double* scal, BV b,
-                                                   double* partial) {
+                                                   double* partial, RowSet rows) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;   // uniform per block
   double v1[1];
   red_sum<1>(red, s, v1);
   const double alpha = v1[0] != 0.0 ? st[0] / v1[0] : 0.0;
-  if (leader()) st[2] = alpha;
+  if (leader() && rows.part != 2) st[2] = alpha;
   const int W = WT > 0 ? WT : W_;
   const double* vs = val + (long)s * W * C;
   const double* rs = b.r + s * Ce;
   const double* ws = b.v + s * Ce;
   const double* hs = b.sv + s * Ce;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for_rows(C, rows, [&](int c) {
     const long i = s * Ce + c;
     const double sc = rs[c] - alpha * ws[c];
     double o = 0.0;
@@ -283,8 +309,8 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, cons
     acc[1] += y * y;
     acc[2] += r0 * y;
     acc[3] += r0 * sc;
-  }
-  block_partials<4>(acc, partial, s);
+  });
+  block_partials<4>(acc, partial, s, rows);
 }
 
 // prologue: omega = (t.s)/(t.t); rho_new = r0.s - omega r0.t; beta = (rho_new / rho)(alpha / omega);
@@ -343,7 +369,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
                                                  const double* __restrict__ val, int it, int max_iter, double tol,
                                                  double abs_tol, Red red_rz, Red red_rr, double* scal, CV v,
                                                  const double* __restrict__ pold, double* __restrict__ pnew,
-                                                 double* partial) {
+                                                 double* partial, RowSet rs) {
   if (it > 0 && scal[6] == 0.0) return;   // stopped earlier
   double a[1], b[1];
   red_sum<1>(red_rz, 0, a);
@@ -352,7 +378,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
   const double res0 = it == 0 ? res : scal[4];
   const double rzp = scal[1];
   const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && rzp == 0.0);
-  if (leader()) {
+  if (leader() && rs.part != 2) {
     if (it == 0) scal[4] = res;
     if (it == 0 || scal[6] != 0.0) { scal[5] = res; scal[7] = it; }
     scal[6] = stop ? 0.0 : 1.0;
@@ -363,7 +389,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
   const double* z = v.z;
   const int Wr = WT > 0 ? WT : W;
   double acc[1] = {0.0};
-  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+  for_rows(C, rs, [&](int c) {
     const double pc = z[c] + beta * pold[c];
     pnew[c] = pc;
     double y = v.dS[c] * pc;
@@ -374,8 +400,8 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
     }
     v.q[c] = y;
     acc[0] += pc * y;
-  }
-  block_partials<1>(acc, partial, 0);
+  });
+  block_partials<1>(acc, partial, 0, rs);
 }
 
 // prologue: alpha = rz / (p.q); x += alpha p; r -= alpha q; partials (r.z, r.r); with the Jacobi
@@ -410,17 +436,18 @@ struct Launch {
   int nblk, nsys;
   // make the partials of the last kernel readable by the next (slot: independent buffers for
   // reductions that are alive at the same time)
-  Red after(double* partial, int NV, int slot = 0) {
-    if (x.nranks == 1) return Red{partial, nblk, NV, (long)nblk * NV};
+  Red after(double* partial, int NV, int slot = 0, int np = 0) {
+    if (np == 0) np = nblk;
+    if (x.nranks == 1) return Red{partial, np, NV, (long)np * NV};
     const size_t per = (size_t)nsys * 4;   // up to 4 values per system per slot
     if (x.ws.red_local.n < 2 * per) x.ws.red_local.alloc(2 * per);
     if (x.ws.red_all.n < 2 * per * x.nranks) x.ws.red_all.alloc(2 * per * x.nranks);
     double* loc = x.ws.red_local.p + slot * per;
     double* all = x.ws.red_all.p + slot * per * x.nranks;
-    if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
-    else if (NV == 2) hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
-    else if (NV == 3) hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
-    else hipLaunchKernelGGL(k_red_local<4>, dim3(nsys), dim3(TPB), 0, x.stream, partial, nblk, loc);
+    if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
+    else if (NV == 2) hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
+    else if (NV == 3) hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
+    else hipLaunchKernelGGL(k_red_local<4>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
     DFMI_HIP(hipGetLastError());
     halo_allgather(x, loc, all, (long)nsys * NV);
     return Red{all, x.nranks, (long)nsys * NV, NV};
@@ -441,6 +468,25 @@ void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce) {
   std::vector<HaloItem> it;
   for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false});
   halo_update(x, it.data(), (int)it.size());
+}
+
+// An SpMV-type launch that reads the halo entries of `vecs`: with overlap, the interior rows run while
+// the exchange is in flight and the boundary rows after it (partials in two halves, np = 2 nblk);
+// otherwise exchange, then all rows. launch(RowSet) enqueues the kernel; returns the partial count.
+template <class F>
+int spmv_with_halo(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce, int nblk, F&& launch) {
+  if (!halo_overlap(x)) {
+    halo_vecs(x, vecs, nsys, Ce);
+    launch(RowSet{});
+    return nblk;
+  }
+  std::vector<HaloItem> it;
+  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false});
+  halo_begin(x, it.data(), (int)it.size());
+  launch(RowSet{1, x.ell.bflag.p, x.ell.brow.p, x.ell.nb});
+  halo_end(x);
+  launch(RowSet{2, x.ell.bflag.p, x.ell.brow.p, x.ell.nb});
+  return 2 * nblk;
 }
 
 // Convergence polling without draining the stream: every `check` iterations the solver state is
@@ -547,6 +593,16 @@ void build_ell(Ctx& x) {
   x.ell.W = W;
   x.ell.col.upload(col, x.stream);
   x.ell.src.upload(src, x.stream);
+  std::vector<int8_t> bflag(C, 0);
+  std::vector<int> brow;
+  for (int c = 0; c < C; ++c) {
+    for (auto& e : ent[c]) if (e.first >= C) bflag[c] = 1;
+    if (bflag[c]) brow.push_back(c);
+  }
+  x.ell.nb = (int)brow.size();
+  if (brow.empty()) brow.push_back(0);
+  x.ell.bflag.upload(bflag, x.stream);
+  x.ell.brow.upload(brow, x.stream);
   DFMI_HIP(hipStreamSynchronize(x.stream));
   x.ell.ready = true;
 }
@@ -559,7 +615,7 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
-  const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 8 + 64;
+  const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 12 + 64;
   if (x.ws.buf.n < need) x.ws.buf.alloc(need);
   const long N = nsys * Ce;
   *dS = x.ws.buf.p;
@@ -657,8 +713,8 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   double* val = base + BCG_VECS * N;
   // one partial buffer per reduction site (a converged system's last sums stay intact)
   double* pR = val + (size_t)nsys * W * C;          // (||D r||^2, rho0 | 0): init, xp
-  double* pV = pR + (size_t)nsys * nblk * 2;        // r0.v
-  double* pT = pV + (size_t)nsys * nblk;            // (t.s, t.t, r0.t, r0.s)
+  double* pV = pR + (size_t)nsys * nblk * 2;        // r0.v (x 2: the overlapped SpMV's two row sets)
+  double* pT = pV + (size_t)nsys * nblk * 2;        // (t.s, t.t, r0.t, r0.s) (x 2 likewise)
   Sys q{lower, upper, diag, source, ic, bc, lstride, ustride, dstride, sstride, bstride, xsol, xstride};
   MeshView m = x.view();
   const int8_t* ty = x.st(type_field);
@@ -680,25 +736,26 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   Poller poll(x, WS.scal.p, nsys);
   const int check = 2;
   for (int it = 0;; ++it) {
-    halo_vecs(x, {b.p}, nsys, Ce);
-    dispatch_W(W, [&](auto wt) {
-      constexpr int WT = decltype(wt)::value;
-      KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL((k_bcg_spmv1<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
-                         cfg.abs_tol, red, WS.scal.p, b, pV);
+    const int np1 = spmv_with_halo(x, {b.p}, nsys, Ce, nblk, [&](RowSet rs) {
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_bcg_spmv");
+        hipLaunchKernelGGL((k_bcg_spmv1<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, it, cfg.max_iter,
+                           cfg.tol, cfg.abs_tol, red, WS.scal.p, b, pV, rs);
+      });
     });
     if (it >= cfg.max_iter) break;
-    red = L.after(pV, 1);
-    if (halo_active(x)) {   // processor neighbours read s from the exchanged sv
-      { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
-      halo_vecs(x, {b.sv}, nsys, Ce);
-    }
-    dispatch_W(W, [&](auto wt) {
-      constexpr int WT = decltype(wt)::value;
-      KScope _ks(x, "k_bcg_spmv");
-      hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, red, WS.scal.p, b, pT);
+    red = L.after(pV, 1, 0, np1);
+    // processor neighbours read s from the exchanged sv
+    if (halo_active(x)) { KScope _ks(x, "k_bcg_s"); hipLaunchKernelGGL(k_bcg_s, g, bl, 0, x.stream, C, Ce, red, WS.scal.p, b); }
+    const int np2 = spmv_with_halo(x, {b.sv}, nsys, Ce, nblk, [&](RowSet rs) {
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_bcg_spmv");
+        hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, red, WS.scal.p, b, pT, rs);
+      });
     });
-    const Red red_t = L.after(pT, 4, 0);
+    const Red red_t = L.after(pT, 4, 0, np2);
     { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_bcg_xp, g, bl, 0, x.stream, C, Ce, red_t, q, smap, WS.scal.p, b, pR); }
     DFMI_HIP(hipGetLastError());
     red = L.after(pR, 2, 0);
@@ -725,7 +782,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   CV v{base, base + Ce, base + 2 * Ce, base + 3 * Ce, base + 4 * Ce, base + 5 * Ce, base + 6 * Ce, base + 7 * Ce};
   double* val = base + 8 * Ce;
   double* q1 = val + (size_t)W * C;    // p.q
-  double* q2 = q1 + (size_t)nblk * 2;  // (r.z [Jacobi], r.r)
+  double* q2 = q1 + (size_t)nblk * 2;  // (r.z [Jacobi], r.r); q1 holds 2 nblk for the overlapped SpMV
   double* q3 = q2 + (size_t)nblk * 2;  // r.z (AMG)
   Sys q{lower, upper, diag, source, ic, bc, 0, 0, 0, 0, 0, xsol, 0};
   MeshView m = x.view();
@@ -779,15 +836,16 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   double* pold = v.pa;
   double* pnew = v.pb;
   for (int it = 0;; ++it) {
-    halo_vecs(x, {v.z, pold}, 1, Ce);
-    dispatch_W(W, [&](auto wt) {
-      constexpr int WT = decltype(wt)::value;
-      KScope _ks(x, "k_cg_spmv");
-      hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
-                         cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1);
+    const int np = spmv_with_halo(x, {v.z, pold}, 1, Ce, nblk, [&](RowSet rs) {
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_cg_spmv");
+        hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
+                           cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1, rs);
+      });
     });
     if (it >= cfg.max_iter) break;
-    Red red = L.after(q1, 1);
+    Red red = L.after(q1, 1, 0, np);
     {
       KScope _ks(x, "k_cg_x");
       if (amg) hipLaunchKernelGGL(k_cg_x<false>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);

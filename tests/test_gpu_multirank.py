@@ -34,7 +34,7 @@ def _setup(m, t, ym, dt, comm=None):
     return ctx
 
 
-def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True, renumber=None):
+def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True, renumber=None, overlap=False):
     from dfmi.mesh import hex_box, global_cell_ids
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
@@ -91,11 +91,18 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
         except Exception as e:   # surfaced below
             err[r] = e
 
+    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work)
+    prev = os.environ.get("DFMI_HALO_OVERLAP")
+    os.environ["DFMI_HALO_OVERLAP"] = "1" if overlap else "0"
     th = [threading.Thread(target=work, args=(r,)) for r in range(nr)]
     for x in th:
         x.start()
     for x in th:
         x.join(timeout=300)
+    if prev is None:
+        os.environ.pop("DFMI_HALO_OVERLAP", None)
+    else:
+        os.environ["DFMI_HALO_OVERLAP"] = prev
     assert not any(x.is_alive() for x in th), "decomposed run hung"
     for e in err:
         if e is not None:
@@ -208,11 +215,19 @@ def test_partitioned_polymesh_matches_oracle(method, nparts, from_dirs):
         except Exception as e:
             err[r] = e
 
+    overlap = method == "graph"   # the graph-partitioned cases run the overlapped solver halos
+    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work)
+    prev = os.environ.get("DFMI_HALO_OVERLAP")
+    os.environ["DFMI_HALO_OVERLAP"] = "1" if overlap else "0"
     th = [threading.Thread(target=work, args=(r,)) for r in range(nr)]
     for x in th:
         x.start()
     for x in th:
         x.join(timeout=300)
+    if prev is None:
+        os.environ.pop("DFMI_HALO_OVERLAP", None)
+    else:
+        os.environ["DFMI_HALO_OVERLAP"] = prev
     assert not any(x.is_alive() for x in th), "decomposed run hung"
     for e in err:
         if e is not None:
@@ -223,4 +238,28 @@ def test_partitioned_polymesh_matches_oracle(method, nparts, from_dirs):
             a[:, meshes[r].cell_map] = out[r][n].reshape(k, -1)
         ref = orc[n].reshape(k, -1)
         e = rel_err(a, ref)
+        assert e < 1e-9, (n, e)
+
+
+@pytest.mark.parametrize("decomp", [(2, 1, 1), (2, 2, 2)])
+def test_overlapped_halo_step_matches(decomp):
+    """Solver halos on the comm stream (DFMI_HALO_OVERLAP=1): the interior rows of every SpMV run while
+    the exchange is in flight, the boundary rows after it. Same per-row arithmetic, reductions summed in
+    two halves: agrees with the in-order exchange to rounding, with the oracle to 1e-9, and is bitwise
+    reproducible run to run."""
+    ref, g1 = _run(10, 8, 6, decomp, overlap=True)
+    _, g0 = _run(10, 8, 6, decomp, overlap=False)
+    _, g2 = _run(10, 8, 6, decomp, overlap=True)
+    for n in ("T", "p", "rho", "he", "U", "Y"):
+        assert np.array_equal(g1[n], g2[n]), ("run-to-run", n)
+        e = rel_err(g1[n], g0[n])
+        assert e < 1e-11, ("overlap vs in-order", n, e)
+        e = rel_err(g1[n], ref["oracle"][n])
+        assert e < 1e-9, ("oracle", n, e)
+
+
+def test_overlapped_halo_walls_two_steps():
+    ref, glob = _run(8, 4, 4, (2, 2, 1), n_steps=2, periodic=False, overlap=True)
+    for n in ("T", "p", "rho", "U", "Y"):
+        e = rel_err(glob[n], ref[n])
         assert e < 1e-9, (n, e)
