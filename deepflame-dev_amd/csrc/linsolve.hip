@@ -76,14 +76,13 @@ struct RowSet {
 };
 __device__ __forceinline__ int rows_begin() { return xcd_block() * blockDim.x + threadIdx.x; }
 template <class F> __device__ __forceinline__ void for_rows(long C, const RowSet& rs, F&& f) {
+  // one loop (the body is instantiated once: two loops measured +19 % on k_bcg_spmv2)
   const int stride = gridDim.x * blockDim.x;
-  if (rs.part == 2) {
-    for (int k = rows_begin(); k < rs.nb; k += stride) f(rs.list[k]);
-  } else {
-    for (int c = rows_begin(); c < C; c += stride) {
-      if (rs.part == 1 && rs.flag[c]) continue;
-      f(c);
-    }
+  const int n = rs.part == 2 ? rs.nb : (int)C;
+  for (int k = rows_begin(); k < n; k += stride) {
+    const int c = rs.part == 2 ? rs.list[k] : k;
+    if (rs.part == 1 && rs.flag[c]) continue;
+    f(c);
   }
 }
 
