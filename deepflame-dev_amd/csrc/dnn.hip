@@ -80,7 +80,7 @@ __device__ __forceinline__ int swz16(int row, int c) { return c ^ ((0x78 >> (2 *
 // the tile -- each fp16-rounded activation is multiplied by its output weight wo[col] and the products are
 // summed per row (fp32, fixed order: over the lane's 4 columns, then a 16-lane xor tree); the two waves of
 // a row band write separate partial sums P[z][2 tile_n + wave_n][M], which k_dnn_output adds in order.
-template <bool GELU, bool OUT, bool PRIO>
+template <bool GELU, bool OUT>
 __global__ void __launch_bounds__(256, 2)
     k_mlp_gemm(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
@@ -126,17 +126,9 @@ __global__ void __launch_bounds__(256, 2)
   const int wm = (wave >> 1) * 128, wn = (wave & 1) * 64;
   const int r = lane & 15, c = lane >> 4;
   const int nk = K / BK;
-  stage(0, 0);
-  if (nk > 1) stage(1, BK);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
-    const _Float16* la = lds + cur * STAGE;
+  auto frag_reads = [&](int buf, half8 (&af)[8], half8 (&bf)[4]) {
+    const _Float16* la = lds + buf * STAGE;
     const _Float16* lw = la + TILE_A;
-    half8 af[8], bf[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = wn + 16 * j + r;
@@ -147,16 +139,34 @@ __global__ void __launch_bounds__(256, 2)
       const int row = wm + 16 * i + r;
       af[i] = *reinterpret_cast<const half8*>(la + row * BK + swz16(row, c) * 8);
     }
-    // all 12 fragment reads issued before the first MFMA (counted lgkmcnt waits follow): left to itself the
-    // compiler re-reads A two fragments at a time behind lgkmcnt(0), exposing the LDS latency 4x per tile
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);   // MFMA phase ahead of the other wave's staging
+  };
+  // 16-column blocks of this wave that hold output columns (< N): the padded tail of the last N tile
+  // (N = 400 / 800 pad to 512 / 896) issues no MFMAs, freeing the SIMD for the co-resident block
+  const int jlive = min(4, max(0, (N - (n0 + wn) + 15) / 16));
+  auto mfmas = [&](const half8 (&af)[8], const half8 (&bf)[4]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 4; ++j)
+      if (j < jlive)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-    cur = cur == NBUF - 1 ? 0 : cur + 1;
+        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  };
+  stage(0, 0);
+  if (nk > 1) stage(1, BK);
+  {
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (kt + 2) * BK);
+      half8 af[8], bf[4];
+      frag_reads(cur, af, bf);
+      // all 12 fragment reads issued before the first MFMA (counted lgkmcnt waits follow): left to itself the
+      // compiler re-reads A two fragments at a time behind lgkmcnt(0), exposing the LDS latency 4x per tile
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(af, bf);
+      cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
   }
   // epilogue: bias + GELU in registers (C/D map col = lane & 15, row = 4 (lane >> 4) + e)
   if constexpr (OUT) {
@@ -399,8 +409,6 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   const size_t act = (size_t)d.nmod * chunk * wmax;
   if (d.h0.n < act) { d.h0.alloc(act); d.h1.alloc(act); }
   if (d.x0.n < (size_t)chunk * d.Kp[0]) d.x0.alloc((size_t)chunk * d.Kp[0]);
-  const char* ep = std::getenv("DFMI_GEMM_PRIO");   // MFMA-phase wave priority (A/B knob)
-  const bool prio = ep ? std::atoi(ep) != 0 : true;
   for (int c0 = 0; c0 < nr; c0 += chunk) {
     const int n = std::min(chunk, nr - c0);
     const int* idx = d.idx.p + c0;
@@ -421,19 +429,11 @@ void dnn_solve(Ctx& x, const char* rho_field) {
       KScope _ks(x, "k_mlp_gemm");
       if (l + 2 == L) {   // last hidden layer: the output layer fused into the epilogue
         d.gemm_flops += 2.0 * n * N * d.nmod;
-        if (prio)
-          hipLaunchKernelGGL((k_mlp_gemm<true, true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
-                             d.part.p, sP);
-        else
-          hipLaunchKernelGGL((k_mlp_gemm<true, true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
-                             d.part.p, sP);
-      } else if (prio) {
-        hipLaunchKernelGGL((k_mlp_gemm<true, false, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                           (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
+        hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+                           (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
+                           d.part.p, sP);
       } else {
-        hipLaunchKernelGGL((k_mlp_gemm<true, false, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+        hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                            (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
       }
       DFMI_HIP(hipGetLastError());

@@ -3,7 +3,7 @@
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_species53.py -x -q --timeout 120 --timeout-method thread > $R/gpurun_out/t.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_species53.py tests/test_gpu_dnn.py -x -q --timeout 120 --timeout-method thread > $R/gpurun_out/t.log 2>&1
 echo tests ok
 cd /tmp && export TMPDIR=/tmp
 i=0
