@@ -68,3 +68,48 @@ def test_full_size_steps_are_deterministic_and_conservative():
     assert abs(np.sum(rho * V) - np.sum(rho_old * V)) <= 1e-13 * np.sum(rho_old * V)
     assert np.abs(rho - rho_old).max() > 0.0           # the fluxes were not zero
     ctx.close()
+
+
+def test_config4_full_size_deterministic_and_closed():
+    """BASELINE config 4 at its full size (128^3 cells x 53 species, synthetic GRI table, the DF-ODENet
+    source of 52 nets [55,1600,800,400,1] on MFMA fp16): the large-mechanism kernels (species-chunked Y
+    assembly, cooperative thermo, batched 52-system BiCGStab, compacted DNN inference) give bitwise
+    identical fields when the same state is stepped twice, species close to 1 in every cell, T stays
+    physical and every solve meets its tolerance."""
+    sys.path.insert(0, ROOT)
+    from bench import MECHS, reference_fields
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    from dfmi.synthetic import gri53_species, gri53_smooth_fractions, gri53_dnn
+    n = 128
+    m = hex_box(n, n, n, lengths=(2 * np.pi * 1e-3,) * 3)
+    f = reference_fields(m, read_yaml_mechanism(os.path.join(GOLDEN, MECHS["burke9"][0]))["species"])
+    sp = gri53_species(os.path.join(GOLDEN, "gri30.yaml"))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_gri53_synthetic.txt"), sp)
+    ctx = Context(0)
+    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6)
+    gri53_dnn(ctx)
+    ctx.chem_set_options(2)
+    T0 = f["T"]
+    case.init_state(ctx, m, t.S, T0, f["p"], f["U"], gri53_smooth_fractions((T0 - T0.min()) / max(np.ptp(T0), 1.0)))
+    C, S = m.n_cells, t.S
+    ctx.time_step(2)
+    assert ctx.dnn_stats()[0] > 0                      # the hot kernel reacts
+    st = case.pull_state(ctx, m, S)
+    runs = []
+    for _ in range(2):
+        case.push_state(ctx, st)
+        ctx.time_step(2)
+        runs.append({k: ctx.get_field(k, (C,)) for k in ("T", "p", "rho", "he")} |
+                    {"U": ctx.get_field("U", (3, C)), "Y": ctx.get_field("Y", (S, C))})
+    for k in runs[0]:
+        assert np.array_equal(runs[0][k], runs[1][k]), k
+    T, Y = runs[0]["T"], runs[0]["Y"]
+    assert np.isfinite(T).all() and 250.0 < T.min() and T.max() < 3000.0
+    assert np.abs(Y.sum(axis=0) - 1.0).max() < 1e-12 and Y.min() >= 0.0
+    for e in ("U", "Y", "E", "p"):
+        it, r0, rel = ctx.solver_stats(e)
+        assert rel <= 1e-5 or it == 20, (e, it, rel)
+    ctx.close()
