@@ -65,6 +65,10 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
         # he, rho, rho_old, K, K_old, alpha, hDiffCorrFlux (3), dpdt, diffAlphaD, V in; diag, source out;
         # faces phi, w, dc, magSf, Sf in, lower/upper out; slots bphi, bw, bdc, bmagSf, bSf in, ic/bc out
         return C * 104.0 + C * 16.0 + F * (56.0 + 16.0) + Bc * (56.0 + 16.0) + topo
+    if kernel == "k_p_face":
+        # pEqn face fluxes (phiHbyA, rhorAUf, the laplacian's lower = upper): cells rho, rAU, rho_old, U_old (3),
+        # HbyA (3) in; faces own, nei, w, Sf (3), phi_old, deltaCoeffs, magSf in, 4 values out (no slots)
+        return C * 72.0 + F * (8.0 + 56.0 + 32.0)
     if kernel == "k_u_hbya":
         # U (3), source (3), V in; HbyA (3) out; faces lower, upper; slots internal/boundaryCoeffs (3 each)
         return C * 56.0 + C * 24.0 + F * 16.0 + Bc * 48.0 + topo
@@ -84,7 +88,7 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
 
 
 SOLVER_KERNELS = ("k_bcg_spmv", "k_cg_spmv")
-ASSEMBLY_KERNELS = ("k_y_assemble_ell", "k_y_prep", "k_u_grad", "k_u_assemble", "k_e_assemble", "k_u_hbya")
+ASSEMBLY_KERNELS = ("k_y_assemble_ell", "k_y_prep", "k_u_grad", "k_u_assemble", "k_e_assemble", "k_u_hbya", "k_p_face")
 ROOF_KERNELS = SOLVER_KERNELS + ASSEMBLY_KERNELS + ("k_thermo_cells",)
 
 
@@ -513,7 +517,8 @@ def main():
             # every instantiation of the family (k_bcg_spmv -> k_bcg_spmv1<6>, k_bcg_spmv2<6>); variants
             # moving < 1 % of the largest one's bytes are other workloads' (the 1D flame line's W = 2)
             ent = [v for key, v in tab.items()
-                   if key.split("::")[-1].split("<")[0].rstrip("12") == fam or key.split("::")[-1].startswith(fam + "<")]
+                   if key.split("::")[-1].split("<")[0].rstrip("12") == fam or key.split("::")[-1].startswith(fam + "<")
+                   or key.split("::")[-1].split("(")[0] == fam + "_cell"]   # k_p_face's cell-walk form
             if not ent:
                 continue
             top = max(v["hbm_bytes_mean"] for v in ent)
