@@ -44,6 +44,29 @@ struct Amg {
   ~Amg() { clear_graphs(); }
 };
 
+// The hierarchy as plain pointers (one workgroup runs the whole V-cycle of a small system in
+// linsolve.hip). Level 0's operator is the solver ELL (f64) or its rounded copy (f32); its right-hand
+// side is the PCG residual, so b[0] is unused.
+constexpr int AMG_MAXL = 12;
+template <class T> struct AmgView {
+  int L = 0;
+  int n[AMG_MAXL], W[AMG_MAXL];
+  const int* col[AMG_MAXL];
+  const T* val[AMG_MAXL];
+  const T* D[AMG_MAXL];
+  T* b[AMG_MAXL];
+  T* x[AMG_MAXL];
+  T* r[AMG_MAXL];
+  T* xo[AMG_MAXL];
+  const int* agg[AMG_MAXL];
+  const int* mstart[AMG_MAXL];
+  const int* members[AMG_MAXL];
+  T omega, sc;
+  int sweeps;
+};
+AmgView<float> amg_view_f32(Ctx& x, const int* col0);
+AmgView<double> amg_view_f64(Ctx& x, const double* val0, const double* D0, const int* col0);
+
 void amg_setup(Ctx& x);
 void amg_galerkin(Ctx& x, const double* val0, const double* D0);
 // z = M^-1 r with block partials of r.z written to partial[0 .. nblk) (grid of `nblk` blocks); every

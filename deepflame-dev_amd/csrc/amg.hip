@@ -577,6 +577,36 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
 
 }  // namespace
 
+namespace {
+template <class T>
+AmgView<T> amg_view_t(Ctx& x, const double* val0, const double* D0, const int* col0) {
+  constexpr bool F = std::is_same<T, float>::value;
+  Amg& a = x.amg;
+  AmgView<T> v;
+  v.L = (int)a.lv.size();
+  DFMI_CHECK(v.L <= AMG_MAXL, "AMG: too many levels for the single-workgroup V-cycle");
+  for (int l = 0; l < v.L; ++l) {
+    AmgLevel& g = a.lv[l];
+    v.n[l] = g.n; v.W[l] = g.W;
+    v.col[l] = l == 0 ? col0 : (const int*)g.col.p;
+    if constexpr (F) {
+      v.val[l] = g.fval.p; v.D[l] = g.fD.p; v.b[l] = g.fb.p; v.x[l] = g.fx.p; v.r[l] = g.fr.p; v.xo[l] = g.fxo.p;
+    } else {
+      v.val[l] = l == 0 ? val0 : (const double*)g.val.p; v.D[l] = l == 0 ? D0 : (const double*)g.D.p;
+      v.b[l] = g.b.p; v.x[l] = g.x.p; v.r[l] = g.r.p; v.xo[l] = g.xo.p;
+    }
+    v.agg[l] = g.agg.p; v.mstart[l] = g.mstart.p; v.members[l] = g.members.p;
+  }
+  v.omega = (T)a.omega; v.sc = (T)a.overcorr; v.sweeps = a.coarse_sweeps;
+  return v;
+}
+}  // namespace
+
+AmgView<float> amg_view_f32(Ctx& x, const int* col0) { return amg_view_t<float>(x, nullptr, nullptr, col0); }
+AmgView<double> amg_view_f64(Ctx& x, const double* val0, const double* D0, const int* col0) {
+  return amg_view_t<double>(x, val0, D0, col0);
+}
+
 void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
                double* partial, int nblk, const double* active) {
   Amg& a = x.amg;

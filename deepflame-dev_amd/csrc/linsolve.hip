@@ -429,6 +429,283 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
   block_partials<2>(acc, partial, 0);
 }
 
+// ============================================================== small systems: one workgroup per solve
+// A mesh of a few thousand cells (the 1D flame: 880) runs every iteration kernel at its launch floor
+// (≈ 4 µs each, ~500 per step). With one rank and C <= SMALL_C each system's whole solve runs in ONE
+// 1024-thread workgroup: the same formulas and stopping tests as the batched kernels above, phases
+// separated by workgroup barriers, dot products reduced in fixed order inside the workgroup (so the
+// sums are grouped differently from the multi-block reductions: agreement to rounding, not bitwise).
+// Vectors stay in global memory (L2-resident at these sizes); all waves of a workgroup share one CU,
+// whose L1 the barrier's workgroup-scope fence keeps coherent.
+constexpr int SMALL_C = 4096, STPB = 1024, SNW = STPB / 64;
+
+template <int NV> __device__ __forceinline__ void wg_sum(double (&v)[NV]) {
+  __shared__ double sh[SNW][NV];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) { const double t = wave_sum(v[k]); if (lane == 0) sh[wid][k] = t; }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double a = 0.0;
+    for (int w = 0; w < SNW; ++w) a += sh[w][k];
+    v[k] = a;
+  }
+  __syncthreads();
+}
+
+template <int WT>
+__global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, const int* __restrict__ col,
+                                                    const double* __restrict__ val, int max_iter, double tol,
+                                                    double abs_tol, double* scal, BV b, Sys q,
+                                                    const int* __restrict__ sys_map) {
+  const int s = blockIdx.x;
+  const int W = WT > 0 ? WT : W_;
+  double* st = scal + s * NSCAL;
+  const double* vs = val + (long)s * W * C;
+  double *r = b.r + s * Ce, *r0 = b.r0 + s * Ce, *p = b.p + s * Ce, *v = b.v + s * Ce, *t = b.t + s * Ce;
+  const double* dS = b.dS + s * Ce;
+  double* xv = q.x + (sys_map ? sys_map[s] : s) * q.xstride;
+  // r = D^-1 (b - A x); r0 = p = r (k_bcg_init)
+  double a2[2] = {0.0, 0.0};
+  for (int c = threadIdx.x; c < C; c += STPB) {
+    const double d = dS[c];
+    const double res = b.rhs[s * Ce + c] - ell_mv<WT>(W, C, col, vs, d, b.xw + s * Ce, c);
+    const double rr = res / d;
+    r[c] = rr; r0[c] = rr; p[c] = rr;
+    a2[0] += res * res;
+    a2[1] += rr * rr;
+  }
+  wg_sum<2>(a2);
+  const double res0 = sqrt(a2[0]);
+  double n2 = a2[0], rho = a2[1], omega = 1.0;
+  int it = 0;
+  for (;; ++it) {
+    const double res = sqrt(n2);
+    const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (rho == 0.0 || omega == 0.0));
+    if (threadIdx.x == 0) { st[4] = res0; st[0] = rho; st[5] = res; st[7] = it; st[6] = stop ? 0.0 : 1.0; }
+    if (stop) break;
+    // v = D^-1 A p; r0.v
+    double a1[1] = {0.0};
+    for (int c = threadIdx.x; c < C; c += STPB) {
+      const double y = scaled_mv<WT>(W, C, col, vs, dS[c], p, c);
+      v[c] = y;
+      a1[0] += r0[c] * y;
+    }
+    wg_sum<1>(a1);
+    const double alpha = a1[0] != 0.0 ? rho / a1[0] : 0.0;
+    // t = D^-1 A s, s = r - alpha v formed on the fly; (t.s, t.t, r0.t, r0.s)
+    double a4[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int c = threadIdx.x; c < C; c += STPB) {
+      const double sc = r[c] - alpha * v[c];
+      double o = 0.0;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int j = col[k * C + c];
+        o += vs[k * C + c] * (r[j] - alpha * v[j]);
+      }
+      const double y = sc + o / dS[c];
+      t[c] = y;
+      const double rz = r0[c];
+      a4[0] += y * sc; a4[1] += y * y; a4[2] += rz * y; a4[3] += rz * sc;
+    }
+    wg_sum<4>(a4);
+    omega = a4[1] != 0.0 ? a4[0] / a4[1] : 0.0;
+    const double rho_new = a4[3] - omega * a4[2];
+    const double beta = (rho != 0.0 && omega != 0.0) ? (rho_new / rho) * (alpha / omega) : 0.0;
+    // x += alpha p + omega s; r = s - omega t; p = r + beta (p - omega v); ||D r||^2
+    a1[0] = 0.0;
+    for (int c = threadIdx.x; c < C; c += STPB) {
+      const double pv = p[c], vv = v[c];
+      const double sv = r[c] - alpha * vv;
+      xv[c] = xv[c] + alpha * pv + omega * sv;
+      const double rr = sv - omega * t[c];
+      r[c] = rr;
+      p[c] = rr + beta * (pv - omega * vv);
+      const double tr = dS[c] * rr;
+      a1[0] += tr * tr;
+    }
+    wg_sum<1>(a1);
+    n2 = a1[0];
+    rho = rho_new;
+    if (threadIdx.x == 0) { st[3] = omega; st[1] = st[0]; st[8] = rho_new; }
+  }
+  if (threadIdx.x == 0) st[6] = 0.0;
+}
+
+// the AMG V-cycle of amg.hip (k_smooth_res, k_restrict, k_coarsest, k_prolong_smooth, same arithmetic
+// per cell) inside one workgroup: z = M^-1 r, returns r.z (every thread)
+template <class T>
+__device__ double vcycle_wg(const AmgView<T>& a, const double* __restrict__ r0, double* __restrict__ z) {
+  const int L = a.L;
+  const T om = a.omega, sc = a.sc;
+  if (L == 1) {   // a single level (double): Jacobi sweeps from zero straight into z (k_coarsest)
+    const int n = a.n[0], W = a.W[0];
+    const int* col = a.col[0];
+    const T *val = a.val[0], *D = a.D[0];
+    T* xa = a.x[0];
+    T* xb = a.r[0];
+    for (int c = threadIdx.x; c < n; c += STPB) xa[c] = om * (T)r0[c] / D[c];
+    __syncthreads();
+    for (int sw = 1; sw < a.sweeps; ++sw) {
+      for (int c = threadIdx.x; c < n; c += STPB) {
+        T y = D[c] * xa[c];
+        for (int k = 0; k < W; ++k) { const int j = col[k * n + c]; if (j < n) y += val[k * n + c] * xa[j]; }
+        xb[c] = xa[c] + om * ((T)r0[c] - y) / D[c];
+      }
+      __syncthreads();
+      T* tt = xa; xa = xb; xb = tt;
+    }
+    double acc[1] = {0.0};
+    for (int c = threadIdx.x; c < n; c += STPB) { z[c] = (double)xa[c]; acc[0] += r0[c] * (double)xa[c]; }
+    wg_sum<1>(acc);
+    return acc[0];
+  }
+  // down: one sweep from zero + residual, restriction
+  for (int l = 0; l + 1 < L; ++l) {
+    const int n = a.n[l], W = a.W[l];
+    const int* col = a.col[l];
+    const T *val = a.val[l], *D = a.D[l];
+    for (int c = threadIdx.x; c < n; c += STPB) {
+      const T bc = l == 0 ? (T)r0[c] : a.b[l][c];
+      const T xc = om * bc / D[c];
+      T y = D[c] * xc;
+      for (int k = 0; k < W; ++k) {
+        const int j = col[(long)k * n + c];
+        if (j < n) y += val[(long)k * n + c] * (om * (l == 0 ? (T)r0[j] : a.b[l][j]) / D[j]);
+      }
+      a.x[l][c] = xc;
+      a.r[l][c] = bc - y;
+    }
+    __syncthreads();
+    const int nc = a.n[l + 1];
+    for (int I = threadIdx.x; I < nc; I += STPB) {
+      T sm = 0;
+      for (int e = a.mstart[l][I]; e < a.mstart[l][I + 1]; ++e) sm += a.r[l][a.members[l][e]];
+      a.b[l + 1][I] = sm;
+    }
+    __syncthreads();
+  }
+  {   // coarsest: weighted-Jacobi sweeps from zero (ping-pong through x / r of that level)
+    const int l = L - 1, n = a.n[l], W = a.W[l];
+    const int* col = a.col[l];
+    const T *val = a.val[l], *D = a.D[l], *bb = a.b[l];
+    T* xa = a.x[l];
+    T* xb = a.r[l];
+    for (int c = threadIdx.x; c < n; c += STPB) xa[c] = om * bb[c] / D[c];
+    __syncthreads();
+    for (int sw = 1; sw < a.sweeps; ++sw) {
+      for (int c = threadIdx.x; c < n; c += STPB) {
+        T y = D[c] * xa[c];
+        for (int k = 0; k < W; ++k) { const int j = col[k * n + c]; if (j < n) y += val[k * n + c] * xa[j]; }
+        xb[c] = xa[c] + om * (bb[c] - y) / D[c];
+      }
+      __syncthreads();
+      T* tt = xa; xa = xb; xb = tt;
+    }
+    if (xa != a.x[l]) {   // the result in x[l]
+      for (int c = threadIdx.x; c < n; c += STPB) a.x[l][c] = xa[c];
+      __syncthreads();
+    }
+  }
+  // up: prolongate the scaled coarse correction + one sweep; levels >= 1 into xo, level 0 into z
+  for (int l = L - 2; l >= 1; --l) {
+    const int n = a.n[l], W = a.W[l];
+    const int* col = a.col[l];
+    const int* agg = a.agg[l];
+    const T *val = a.val[l], *D = a.D[l], *bb = a.b[l], *x = a.x[l];
+    const T* xc = l + 1 == L - 1 ? a.x[l + 1] : a.xo[l + 1];
+    for (int c = threadIdx.x; c < n; c += STPB) {
+      const T yc = x[c] + sc * xc[agg[c]];
+      T ay = D[c] * yc;
+      for (int k = 0; k < W; ++k) {
+        const int j = col[(long)k * n + c];
+        if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
+      }
+      a.xo[l][c] = yc + om * (bb[c] - ay) / D[c];
+    }
+    __syncthreads();
+  }
+  const int n = a.n[0], W = a.W[0];
+  const int* col = a.col[0];
+  const int* agg = a.agg[0];
+  const T *val = a.val[0], *D = a.D[0], *x = a.x[0];
+  const T* xc = L == 2 ? a.x[1] : a.xo[1];
+  double acc[1] = {0.0};
+  for (int c = threadIdx.x; c < n; c += STPB) {
+    const T yc = x[c] + sc * xc[agg[c]];
+    T ay = D[c] * yc;
+    for (int k = 0; k < W; ++k) {
+      const int j = col[(long)k * n + c];
+      if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
+    }
+    const double bc = r0[c];
+    const double o = (double)(yc + om * ((T)bc - ay) / D[c]);
+    z[c] = o;
+    acc[0] += bc * o;
+  }
+  wg_sum<1>(acc);
+  return acc[0];
+}
+
+// the whole PCG solve (k_cg_init, k_cg_spmv, k_cg_x and the preconditioner) in one workgroup; AMG:
+// the V-cycle above, otherwise Jacobi (z = r / dS)
+template <int WT, class T, bool AMG>
+__global__ void __launch_bounds__(STPB) k_pcg_small(long C, int W_, const int* __restrict__ col,
+                                                    const double* __restrict__ val, int max_iter, double tol,
+                                                    double abs_tol, double* scal, CV v, double* __restrict__ xsol,
+                                                    AmgView<T> a) {
+  const int W = WT > 0 ? WT : W_;
+  double* p = v.pa;
+  double a2[2] = {0.0, 0.0};
+  for (int c = threadIdx.x; c < C; c += STPB) {
+    const double rr = v.rhs[c] - ell_mv<WT>(W, C, col, val, v.dS[c], v.xw, c);
+    v.r[c] = rr;
+    p[c] = 0.0;
+    if (!AMG) { const double zz = rr / v.dS[c]; v.z[c] = zz; a2[0] += rr * zz; }
+    a2[1] += rr * rr;
+  }
+  wg_sum<2>(a2);
+  double rz = a2[0], rr2 = a2[1];
+  if constexpr (AMG) rz = vcycle_wg<T>(a, v.r, v.z);
+  const double res0 = sqrt(rr2);
+  double rzp = 0.0;
+  for (int it = 0;; ++it) {
+    const double res = sqrt(rr2);
+    const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && rzp == 0.0);
+    if (threadIdx.x == 0) { scal[4] = res0; scal[5] = res; scal[7] = it; scal[6] = stop ? 0.0 : 1.0; scal[0] = rz; }
+    if (stop) break;
+    const double beta = it == 0 ? 0.0 : rz / rzp;
+    for (int c = threadIdx.x; c < C; c += STPB) p[c] = v.z[c] + beta * p[c];
+    __syncthreads();
+    double a1[1] = {0.0};
+    for (int c = threadIdx.x; c < C; c += STPB) {
+      double y = v.dS[c] * p[c];
+#pragma unroll
+      for (int k = 0; k < W; ++k) y += val[k * C + c] * p[col[k * C + c]];
+      v.q[c] = y;
+      a1[0] += p[c] * y;
+    }
+    wg_sum<1>(a1);
+    const double alpha = a1[0] != 0.0 ? rz / a1[0] : 0.0;
+    a2[0] = 0.0; a2[1] = 0.0;
+    for (int c = threadIdx.x; c < C; c += STPB) {
+      xsol[c] = xsol[c] + alpha * p[c];
+      const double rr = v.r[c] - alpha * v.q[c];
+      v.r[c] = rr;
+      if (!AMG) { const double zz = rr / v.dS[c]; v.z[c] = zz; a2[0] += rr * zz; }
+      a2[1] += rr * rr;
+    }
+    wg_sum<2>(a2);
+    rzp = rz;
+    rr2 = a2[1];
+    if constexpr (AMG) rz = vcycle_wg<T>(a, v.r, v.z);
+    else rz = a2[0];
+    if (threadIdx.x == 0) { scal[2] = alpha; scal[1] = rzp; }
+  }
+  if (threadIdx.x == 0) scal[6] = 0.0;
+}
+
 // ------------------------------------------------------------------ host side
 struct Launch {
   Ctx& x;
@@ -486,6 +763,13 @@ int spmv_with_halo(Ctx& x, std::initializer_list<double*> vecs, int nsys, long C
   halo_end(x);
   launch(RowSet{2, x.ell.bflag.p, x.ell.brow.p, x.ell.nb});
   return 2 * nblk;
+}
+
+// one rank, no halo, a few thousand cells: each solve in one workgroup launch (DFMI_SMALL_SOLVE=0: off)
+bool small_solve(const Ctx& x) {
+  if (x.nranks != 1 || halo_active(x) || x.C > SMALL_C || x.C == 0) return false;
+  const char* e = std::getenv("DFMI_SMALL_SOLVE");
+  return !(e && std::atoi(e) == 0);
 }
 
 // Convergence polling without draining the stream: every `check` iterations the solver state is
@@ -726,6 +1010,17 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, smap, b.xw); }
   DFMI_HIP(hipGetLastError());
   halo_vecs(x, {b.xw}, nsys, Ce);
+  if (small_solve(x)) {
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_small");
+      hipLaunchKernelGGL(k_bcg_small<WT>, dim3(nsys), dim3(STPB), 0, x.stream, C, Ce, W, x.ell.col.p, val, cfg.max_iter,
+                         cfg.tol, cfg.abs_tol, WS.scal.p, b, q, smap);
+    });
+    DFMI_HIP(hipGetLastError());
+    record_stats(x, eqn, WS.scal.p, nsys);
+    return SolveStats{};
+  }
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
     { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, b, pR); }
@@ -797,6 +1092,26 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     amg_galerkin(x, val, v.dS);
   }
   halo_vecs(x, {v.xw}, 1, Ce);
+  if (small_solve(x)) {
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_pcg_small");
+      if (!amg) {
+        AmgView<double> none{};
+        hipLaunchKernelGGL((k_pcg_small<WT, double, false>), dim3(1), dim3(STPB), 0, x.stream, C, W, x.ell.col.p, val,
+                           cfg.max_iter, cfg.tol, cfg.abs_tol, WS.scal.p, v, xsol, none);
+      } else if (x.amg.fp32) {
+        hipLaunchKernelGGL((k_pcg_small<WT, float, true>), dim3(1), dim3(STPB), 0, x.stream, C, W, x.ell.col.p, val,
+                           cfg.max_iter, cfg.tol, cfg.abs_tol, WS.scal.p, v, xsol, amg_view_f32(x, x.ell.col.p));
+      } else {
+        hipLaunchKernelGGL((k_pcg_small<WT, double, true>), dim3(1), dim3(STPB), 0, x.stream, C, W, x.ell.col.p, val,
+                           cfg.max_iter, cfg.tol, cfg.abs_tol, WS.scal.p, v, xsol, amg_view_f64(x, val, v.dS, x.ell.col.p));
+      }
+    });
+    DFMI_HIP(hipGetLastError());
+    record_stats(x, eqn, WS.scal.p, 1);
+    return SolveStats{};
+  }
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
     KScope _ks(x, "k_cg_init");

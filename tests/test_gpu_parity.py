@@ -362,3 +362,41 @@ def test_amg_pcg_full_step(coarsest, prec, monkeypatch):
     ctx.time_step(2)
     it_jac = ctx.solver_stats("p")[0]
     assert it_amg < it_jac, (it_amg, it_jac)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_small_solves_match_batched_path(prec, monkeypatch):
+    """Systems of <= 4096 cells on one rank are solved in one workgroup per system (k_bcg_small /
+    k_pcg_small with the V-cycle inside); the batched multi-launch path (DFMI_SMALL_SOLVE=0) is what
+    larger meshes run. Same formulas and stopping tests, reductions grouped differently: the two reach
+    the same solution (tight tolerances) and the same iteration counts (within one) at production
+    tolerances."""
+    from dfmi import case
+    monkeypatch.setenv("DFMI_AMG_PREC", prec)
+    monkeypatch.setenv("DFMI_AMG_COARSEST", "64")      # a multi-level hierarchy on this mesh
+    ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
+    res = {}
+    for small in ("1", "0"):
+        monkeypatch.setenv("DFMI_SMALL_SOLVE", small)
+        out = {}
+        for tight in (True, False):
+            case.push_state(ctx, st)
+            if tight:
+                for e in ("U", "Y", "E"):
+                    ctx.set_solver(e, 300, 1e-15, 1e-300)
+                ctx.set_solver("p", 3000, 1e-14, 1e-300)
+            else:
+                for e in ("U", "Y", "E"):
+                    ctx.set_solver(e, 20, 1e-5)
+                ctx.set_solver("p", 1000, 1e-5)
+            ctx.time_step(2)
+            out[tight] = ({n: ctx.get_field(n, (m.n_cells,)) for n in ("T", "p", "rho")} |
+                          {"U": ctx.get_field("U", (3, m.n_cells)), "Y": ctx.get_field("Y", (t.S, m.n_cells))},
+                          {e: ctx.solver_stats(e)[0] for e in ("U", "Y", "E", "p")})
+        res[small] = out
+    for n in ("T", "p", "rho", "U", "Y"):
+        e = rel_err(res["1"][True][0][n], res["0"][True][0][n])
+        assert e < 1e-10, (n, e)
+    for e in ("U", "Y", "E", "p"):
+        assert abs(res["1"][False][1][e] - res["0"][False][1][e]) <= 1, (e, res["1"][False][1], res["0"][False][1])
+    case.push_state(ctx, st)
