@@ -14,7 +14,7 @@ for setting in "$@"; do
 import csv, os, sys
 d = sys.argv[1]
 rows = [r for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv")))]
-keep = [r for r in rows if any(k in r["Kernel_Name"] for k in ("thermo", "y_prep", "y_assemble", "mlp_gemm"))]
+keep = [r for r in rows if any(k in r["Kernel_Name"] for k in ("thermo", "y_prep", "y_assemble", "mlp_gemm", "bcg_", "cg_"))]
 with open(os.path.join(d, "trace_small.csv"), "w", newline="") as f:
     w = csv.DictWriter(f, fieldnames=list(rows[0].keys())); w.writeheader(); w.writerows(keep)
 os.remove(os.path.join(d, "run_kernel_trace.csv"))
