@@ -1,0 +1,130 @@
+"""Decomposed dfLowMachFoam step over the RCCL transport, one process per rank (torchrun worker).
+
+The pool's GPU boxes have one MI355X and RCCL refuses two ranks on one device ("Duplicate GPU
+detected": the check compares the host hash and the PCI bus id). Each rank therefore sets its own
+NCCL_HOSTID before RCCL initialises: the ranks look like two hosts, so RCCL connects them through its
+network transport (sockets over loopback) instead of P2P/xGMI. Everything above the wire is the
+product path the 8-GPU run takes: ncclCommInitRank from a unique id, one ncclSend/ncclRecv group per
+exchange point, ncclAllGather of the per-rank partial sums, the comm stream of the overlapped halos.
+
+Rank 0 gathers the fields (gloo), runs the undecomposed mesh on the same GPU and the oracle, and writes
+the relative errors to --out (JSON). Launched by tests/test_gpu_rccl.py:
+  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P \
+      scripts/rccl_ranks.py --decomp 2,1,1 --out gpurun_out/rccl.json
+"""
+import argparse
+import json
+import os
+import sys
+
+RANK = int(os.environ.get("RANK", "0"))
+WORLD = int(os.environ.get("WORLD_SIZE", "1"))
+# before anything loads RCCL: one "host" per rank, sockets over loopback, no InfiniBand probing
+os.environ["NCCL_HOSTID"] = f"dfmi-rccl-rank{RANK}"
+os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "deepflame-dev_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import numpy as np                      # noqa: E402
+import torch.distributed as dist        # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--decomp", default="2,1,1")
+    ap.add_argument("--mesh", default="10,8,6")
+    ap.add_argument("--overlap", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--walls", type=int, default=0)
+    ap.add_argument("--out", default="gpurun_out/rccl.json")
+    a = ap.parse_args()
+    decomp = tuple(int(x) for x in a.decomp.split(","))
+    nx, ny, nz = (int(x) for x in a.mesh.split(","))
+    assert int(np.prod(decomp)) == WORLD, "decomposition must have WORLD_SIZE blocks"
+    os.environ["DFMI_HALO_OVERLAP"] = str(a.overlap)
+
+    dist.init_process_group("gloo", rank=RANK, world_size=WORLD)
+    from dfmi.lib import Context
+    from dfmi.mesh import hex_box, global_cell_ids
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi import case
+    from conftest import GOLDEN, rel_err
+
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
+    inert = ym["species"].index("N2")
+    L = (2 * np.pi * 1e-3,) * 3
+    dt = 1e-6
+    periodic = (not a.walls,) * 3
+    grad = (1.0, 1.3, 1.0)
+    mg = hex_box(nx, ny, nz, lengths=L, gradings=grad, periodic=periodic)
+    f = case.tgv_fields(mg, ym["species"], kernel_radius=1.2e-3)
+
+    def setup(m, comm=None):
+        ctx = Context(0)
+        case.setup_context(ctx, m, t, inert, dt, case.default_patch_types(m), comm=comm)
+        for e in ("U", "Y", "E"):
+            ctx.set_solver(e, 300, 1e-14, 1e-300)
+        ctx.set_solver("p", 3000, 1e-14, 1e-300)
+        return ctx
+
+    def fields(ctx, n):
+        o = {k: ctx.get_field(k, (n,)) for k in ("T", "p", "rho", "he")}
+        o["U"] = ctx.get_field("U", (3, n))
+        o["Y"] = ctx.get_field("Y", (t.S, n))
+        return o
+
+    m = hex_box(nx, ny, nz, lengths=L, gradings=grad, periodic=periodic, decomp=decomp, rank=RANK)
+    g = global_cell_ids(m, nx, ny)
+    uid = [Context.unique_id() if RANK == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    c = setup(m, comm={"uid": uid[0], "nranks": WORLD, "rank": RANK})
+    case.init_state(c, m, t.S, f["T"][g], f["p"][g], f["U"][:, g], f["Y"][:, g])
+    c.call("pre_time_step")
+    for _ in range(a.steps):
+        c.time_step(2)
+    mine = fields(c, m.n_cells)
+    mine["gid"] = g
+    mine["p_iters"] = int(c.solver_stats("p")[0])
+    c.close()
+    allr = [None] * WORLD
+    dist.all_gather_object(allr, mine)
+    if RANK == 0:
+        glob = {}
+        for n, k in (("T", 1), ("p", 1), ("rho", 1), ("he", 1), ("U", 3), ("Y", t.S)):
+            arr = np.zeros((k, mg.n_cells))
+            for o in allr:
+                arr[:, o["gid"]] = o[n].reshape(k, -1)
+            glob[n] = arr.reshape(-1, mg.n_cells) if k > 1 else arr[0]
+        ref_ctx = setup(mg)
+        case.init_state(ref_ctx, mg, t.S, f["T"], f["p"], f["U"], f["Y"])
+        ref_ctx.call("pre_time_step")
+        res = {"world": WORLD, "decomp": list(decomp), "overlap": a.overlap, "steps": a.steps,
+               "p_iters_per_rank": [o["p_iters"] for o in allr], "vs_single_domain": {}, "vs_oracle": {}}
+        orc = None
+        if a.steps == 1:
+            import oracle as O
+            st = case.pull_state(ref_ctx, mg, t.S)
+            orc = O.Oracle(mg, t, {k: v.copy() for k, v in st.items()}, case.default_patch_types(mg), inert, 1.0 / dt)
+            orc.time_step(2)
+        for _ in range(a.steps):
+            ref_ctx.time_step(2)
+        ref = fields(ref_ctx, mg.n_cells)
+        ref_ctx.close()
+        for n in ("T", "p", "rho", "he", "U", "Y"):
+            res["vs_single_domain"][n] = float(rel_err(glob[n], ref[n]))
+            if orc is not None:
+                res["vs_oracle"][n] = float(rel_err(glob[n], orc[n]))
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as fh:
+            json.dump(res, fh, indent=1)
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
