@@ -1,7 +1,11 @@
 """Transport-fit generator (dfmi.transport_fit) pinned against the table the reference ships for
-ES80_H2-7-16 (generated there with Cantera). Tolerances are the stated difference of our collision
-integrals (Neufeld correlations + Brokaw dipole correction) from Cantera's Monchick-Mason tables:
-non-polar species <= 0.6 %, the strongly polar H2O <= 5 %, binary diffusion <= 3 %."""
+ES80_H2-7-16 (generated there with Cantera 2.6 from the Monchick-Mason collision-integral tables).
+Our tables are recomputed from the Stockmayer potential (dfmi/collision.py, scripts/gen_collision_tables.py)
+and interpolated the way Cantera's MMCollisionInt does. Tolerances (max relative difference of the fitted
+property over 300-3000 K): non-polar viscosities 2e-4; conductivities and binary diffusivities 1.2e-3,
+except the pairs with H2 (reduced temperatures up to 92, where only the published Omega22* is known:
+2.5e-3); the strongly polar H2O (delta* = 1.22) 1e-2, the orientation-averaged integrals differing from
+Monchick & Mason's 1961 numbers by up to 0.8 %. (Round 1, Neufeld correlations: 0.6 % / 5 % / 3 %.)"""
 import os
 
 import numpy as np
@@ -23,14 +27,42 @@ def test_es80_fits_match_reference_table(es80):
     for k, s in enumerate(ym["species"]):
         mu_r = _eval(ref.visc[k], T) ** 2 * np.sqrt(T); mu = _eval(t.visc[k], T) ** 2 * np.sqrt(T)
         la_r = _eval(ref.cond[k], T) * np.sqrt(T); la = _eval(t.cond[k], T) * np.sqrt(T)
-        tol = 0.05 if s == "H2O" else 0.006
-        assert np.abs(mu / mu_r - 1).max() < tol, s
-        assert np.abs(la / la_r - 1).max() < tol, s
+        polar = s == "H2O"
+        assert np.abs(mu / mu_r - 1).max() < (1e-2 if polar else 2e-4), s
+        assert np.abs(la / la_r - 1).max() < (1e-2 if polar else 1.2e-3), s
+    sp = ym["species"]
     for k in range(t.S):
         for j in range(t.S):
             d_r = _eval(ref.bdiff[k, j], T); d = _eval(t.bdiff[k, j], T)
-            assert np.abs(d / d_r - 1).max() < 0.03, (k, j)
+            tol = 1e-2 if sp[k] == sp[j] == "H2O" else (2.5e-3 if "H2" in (sp[k], sp[j]) else 1.2e-3)
+            assert np.abs(d / d_r - 1).max() < tol, (sp[k], sp[j])
             assert np.array_equal(t.bdiff[k, j], t.bdiff[j, k])
+
+
+def test_lennard_jones_integrals_match_neufeld_correlation():
+    """delta* = 0 column (computed classical integrals) against the Neufeld-Janzen-Aziz (1972) correlations
+    of the Lennard-Jones tables over 0.3 <= T* <= 20 (their stated fit accuracy is ~0.1 %)."""
+    from dfmi.collision import MMCollisionInt, TSTAR22
+    mm = MMCollisionInt()
+    for ts in TSTAR22[(TSTAR22 >= 0.3) & (TSTAR22 <= 20)]:
+        n22 = 1.16145 / ts ** 0.14874 + 0.52487 / np.exp(0.77320 * ts) + 2.16178 / np.exp(2.43787 * ts)
+        n11 = (1.06036 / ts ** 0.15610 + 0.19300 / np.exp(0.47635 * ts) + 1.03587 / np.exp(1.52996 * ts)
+               + 1.76474 / np.exp(3.89411 * ts))
+        assert abs(mm.omega22(ts) / n22 - 1) < 2e-3, ts
+        assert abs(mm.omega11(ts) / n11 - 1) < 2e-3, ts
+
+
+def test_polar_table_interpolation_is_cantera_shaped():
+    """Cantera's MMCollisionInt: exact row values at table nodes for delta* = 0, degree-6 delta* fits
+    through the 8 columns, monotone growth of Omega22* with delta* at low T*."""
+    from dfmi.collision import MMCollisionInt, TSTAR22, DELTA
+    mm = MMCollisionInt()
+    for i in (3, 9, 20):
+        assert mm.omega22(TSTAR22[i]) == mm.o22[i, 0]
+        for j in range(1, 8):   # the degree-6 fit over 8 points stays within 3e-3 of the table
+            assert abs(mm.omega22(TSTAR22[i], DELTA[j]) / mm.o22[i, j] - 1) < 3e-3
+    row = [mm.omega22(0.5, d) for d in DELTA[1:]]
+    assert np.all(np.diff(row) > 0)
 
 
 def test_burke9_table_is_reproducible_and_sane():
