@@ -113,7 +113,7 @@ def parse():
                     help="cell order (dfmi_renumber_cells): blockMesh order (default: with the owner-slot face "
                          "storage its gathers are contiguous runs and it measured fastest), 8x8x4 bricks on a Z-order "
                          "curve, plain Morton, or reverse Cuthill-McKee")
-    ap.add_argument("--traversal", default="none", choices=["bricks", "none"],
+    ap.add_argument("--traversal", default="none", choices=["bricks", "strips4", "strips8", "strips16", "none"],
                     help="visiting order of the gather kernels over the blockMesh-ordered data (dfmi_set_traversal)")
     ap.add_argument("--roof-steps", type=int, default=3, help="extra steps with per-kernel HIP events (rooflines)")
     ap.add_argument("--cpu-n", type=int, default=128, help="cells per direction of the CPU-A baseline sample")
@@ -410,6 +410,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and os.environ.get("DFMI_RCCL_SPLIT_HOSTS"):
+        # rehearsal of the multi-GPU path on a box with fewer GPUs than ranks: each rank poses as its own
+        # host (RCCL then connects the ranks through sockets instead of refusing two ranks per device);
+        # the timing of such a run says nothing about xGMI scaling
+        os.environ["NCCL_HOSTID"] = f"dfmi-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -445,6 +453,12 @@ def main():
         from dfmi.lib import renumber_cells
         ijk = np.stack(m.local_index, axis=1).astype(np.float64)
         ctx.set_traversal(renumber_cells(m.n_cells, ijk, m.owner, m.neighbour, "bricks"))
+    elif args.traversal.startswith("strips") and hasattr(m, "local_index"):
+        # y-strips of R full x-rows swept through z: the working set of a z-sweep (3 planes of one strip)
+        # stays in an XCD's L2, rows stay whole cache lines
+        i, j, k = (np.asarray(a) for a in m.local_index)
+        R = int(args.traversal[6:])
+        ctx.set_traversal(np.lexsort((i, j, k, j // R)).astype(np.int32))
     if args.chem == "ode":
         from dfmi.kinetics import parse_mechanism
         ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, yml)))

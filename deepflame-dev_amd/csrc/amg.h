@@ -17,6 +17,8 @@ struct AmgLevel {
   // work vectors, in the preconditioner's precision (one of the two sets is allocated)
   DevBuf<double> val, D, b, x, r, xo;
   DevBuf<float> fval, fD, fb, fx, fr, fxo;
+  DevBuf<double> r2, zt;                // level 0 with l0_sweeps > 1: second residual, post-sweep ping-pong
+  DevBuf<float> fr2;
 };
 
 // Precision of the V-cycle. fp32 (default) keeps every level's operator and work vectors in single
@@ -29,6 +31,7 @@ struct Amg {
   double omega = 0.85;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
+  int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;

@@ -113,6 +113,61 @@ __global__ void __launch_bounds__(TPB) k_smooth_restrict(int nc, const int* __re
   bc[I] = a;
 }
 
+// a further level-0 pre-sweep on (x, r = b - A x): x += omega r / D, r' = r - A (omega r / D)
+template <int WT, class T>
+__global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, const int* __restrict__ col,
+                                                     const T* __restrict__ val, const T* __restrict__ D,
+                                                     const T* __restrict__ r, T omega, T* __restrict__ x,
+                                                     T* __restrict__ rn, const double* act) {
+  const int W = WT > 0 ? WT : W_;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= n || (act && *act == 0.0)) return;
+  const T rc = r[c];
+  const T dc = omega * rc / D[c];
+  T y = D[c] * dc;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const int j = col[(long)k * n + c];
+    if (j < n) y += val[(long)k * n + c] * (omega * r[j] / D[j]);
+  }
+  x[c] += dc;
+  rn[c] = rc - y;
+}
+
+// a further level-0 post-sweep: out = in + omega (b - A in) / D; optional block partials of b.out
+template <int WT, class T, class TB, class TO>
+__global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, const int* __restrict__ col,
+                                                      const T* __restrict__ val, const T* __restrict__ D,
+                                                      const TB* __restrict__ b, const TO* __restrict__ in, T omega,
+                                                      TO* __restrict__ out, double* partial, const double* act) {
+  const int W = WT > 0 ? WT : W_;
+  if (act && *act == 0.0) return;
+  __shared__ double sh[TPB / 64];
+  double acc = 0.0;
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const T yc = (T)in[c];
+    T ay = D[c] * yc;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int j = col[(long)k * n + c];
+      if (j < n) ay += val[(long)k * n + c] * (T)in[j];
+    }
+    const TB bc = b[c];
+    const TO o = (TO)(yc + omega * ((T)bc - ay) / D[c]);
+    out[c] = o;
+    acc += (double)bc * (double)o;
+  }
+  if (!partial) return;
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int w = 0; w < TPB / 64; ++w) a += sh[w];
+    partial[blockIdx.x] = a;
+  }
+}
+
 template <class T>
 __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
                            const T* __restrict__ r, T* __restrict__ bc, const double* act) {
@@ -347,6 +402,7 @@ void amg_setup(Ctx& x) {
   }   // measured: 19.5 -> 19.9 ms/step with graphs (GPU-side latency, not host launches, bounds the coarse levels)
   a.omega = env_d("DFMI_AMG_OMEGA", 0.85);
   a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
+  a.l0_sweeps = std::max(1, (int)env_d("DFMI_AMG_L0_SWEEPS", 1));
   a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
   a.overcorr = env_d("DFMI_AMG_OVERCORR", 1.35);
   // fused smoothing + restriction per level: measured slower (19.7 -> 21.8 ms/step with levels >= 1 fused,
@@ -411,10 +467,13 @@ void amg_setup(Ctx& x) {
       v.fval.alloc(ne); v.fD.alloc(nv);
       if (l > 0) v.fb.alloc(nv);
       v.fx.alloc(nv); v.fr.alloc(nv); v.fxo.alloc(nv);
+      if (l == 0 && a.l0_sweeps > 1) v.fr2.alloc(nv);
     } else {
       if (l > 0) { v.val.alloc(ne); v.D.alloc(nv); v.b.alloc(nv); }
       v.x.alloc(nv); v.r.alloc(nv); v.xo.alloc(nv);
+      if (l == 0 && a.l0_sweeps > 1) v.r2.alloc(nv);
     }
+    if (l == 0 && a.l0_sweeps > 1) v.zt.alloc(nv);
   }
   a.ready = true;
 }
@@ -526,6 +585,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
                            f.members.p, f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
       continue;
     }
+    T* rcur = RV(l);
     {
       KScope _ks(x, "k_smooth_res");
       if (l == 0)
@@ -535,10 +595,20 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, T>, k_smooth_res<6, T, T>, f.n, f.W, COL(l), VAL(l), DD(l),
                  (const T*)BV(l), om, XV(l), RV(l), act);
     }
+    if (l == 0 && a.l0_sweeps > 1) {   // further pre-sweeps, the residual carried along
+      T* ralt;
+      if constexpr (F) ralt = f.fr2.p; else ralt = f.r2.p;
+      for (int s = 1; s < a.l0_sweeps; ++s) {
+        KScope _ks(x, "k_smooth_step");
+        launch_w(f.W, g, x.stream, k_smooth_step<0, T>, k_smooth_step<6, T>, f.n, f.W, COL(0), VAL(0), DD(0),
+                 (const T*)rcur, om, XV(0), ralt, act);
+        std::swap(rcur, ralt);
+      }
+    }
     {
       KScope _ks(x, "k_restrict");
       hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
-                         f.mstart.p, f.members.p, (const T*)RV(l), BV(l + 1), act);
+                         f.mstart.p, f.members.p, (const T*)rcur, BV(l + 1), act);
     }
   }
   // coarsest
@@ -561,9 +631,18 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
     AmgLevel& f = a.lv[l];
     KScope _ks(x, "k_prolong_smooth");
     if (l == 0) {
+      // with ns post-sweeps the outputs alternate zt / z so that the last one lands in z
+      const int ns = a.l0_sweeps;
+      auto outk = [&](int k) { return ((ns - k) % 2 == 0) ? z : f.zt.p; };   // k = 1 .. ns
       launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
-               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, (const T*)XV(1), om, sc, z,
-               partial, act);
+               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, (const T*)XV(1), om, sc,
+               outk(1), ns == 1 ? partial : (double*)nullptr, act);
+      for (int k = 2; k <= ns; ++k) {
+        KScope _ks2(x, "k_jacobi_sweep");
+        launch_w(f.W, dim3(nblk), x.stream, k_jacobi_sweep<0, T, double, double>, k_jacobi_sweep<6, T, double, double>,
+                 f.n, f.W, COL(0), VAL(0), DD(0), r, (const double*)outk(k - 1), om, outk(k),
+                 k == ns ? partial : (double*)nullptr, act);
+      }
     } else {
       launch_w(f.W, dim3(blocks_for(f.n, TPB)), x.stream, k_prolong_smooth<0, T, T, T>, k_prolong_smooth<6, T, T, T>,
                f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), (const T*)XV(l), (const int*)f.agg.p,
