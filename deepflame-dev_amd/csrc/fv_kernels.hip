@@ -180,12 +180,15 @@ __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __rest
   double s[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) s[k] = 0.0;
+  const double Uc[3] = {U[c], U[C + c], U[2 * C + c]};   // own-cell values in registers
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
     const double w = m.w[f];
     double uf[3], sf[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) uf[j] = interp_f(w, U[j * C + o], U[j * C + n]);
+    for (int j = 0; j < 3; ++j) {
+      const double un = U[j * C + o2];
+      uf[j] = own ? interp_f(w, Uc[j], un) : interp_f(w, un, Uc[j]);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) sf[i] = m.Sf[i * F + f];
 #pragma unroll
@@ -246,24 +249,33 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
   double dT[3] = {0.0, 0.0, 0.0}, gp[3] = {0.0, 0.0, 0.0};
+  // the cell's own tensor, mu and p stay in registers; each face gathers only the other cell's values
+  // (interp_f keeps its owner-first argument order, so the arithmetic is unchanged)
+  double Tc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
+  const double muc = mu[c], pcc = p[c];
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
     const double w = m.w[f], ph = phi[f];
     const double L1 = -w * ph;
     const double U1 = L1 + ph;
-    const double UL = m.dc[f] * (interp_f(w, mu[o], mu[n]) * m.magSf[f]);
+    const double mun = mu[o2];
+    const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
     if (own) { d1 -= L1; lower[f] = L1 + (-UL); upper[f] = U1 + (-UL); }
     else d1 -= U1;
     dL -= UL;
     const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+    double Tn[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Tn[k] = T[k * C + o2];
+    auto fi = [&](int k) { return own ? interp_f(w, Tc[k], Tn[k]) : interp_f(w, Tn[k], Tc[k]); };
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const double v = sf0 * interp_f(w, T[(0 + j) * C + o], T[(0 + j) * C + n]) +
-                       sf1 * interp_f(w, T[(3 + j) * C + o], T[(3 + j) * C + n]) +
-                       sf2 * interp_f(w, T[(6 + j) * C + o], T[(6 + j) * C + n]);
+      const double v = sf0 * fi(0 + j) + sf1 * fi(3 + j) + sf2 * fi(6 + j);
       if (own) dT[j] += v; else dT[j] -= v;
     }
-    const double pf = interp_f(w, p[o], p[n]);
+    const double pn = p[o2];
+    const double pf = own ? interp_f(w, pcc, pn) : interp_f(w, pn, pcc);
     const double g0 = sf0 * pf, g1 = sf1 * pf, g2 = sf2 * pf;
     if (own) { gp[0] += g0; gp[1] += g1; gp[2] += g2; } else { gp[0] -= g0; gp[1] -= g1; gp[2] -= g2; }
   });
@@ -329,6 +341,14 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
+  // one pass over the faces for the three components (each face's coefficient loaded once; every
+  // component still sums its faces in order)
+  double Hl[3] = {0.0, 0.0, 0.0};
+  each_face<WT>(m, c, [&](int f, int oc, bool own) {
+    const double a = own ? upper[f] : lower[f];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Hl[k] -= a * U[k * C + oc];
+  });
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const double* Uk = U + k * C;
@@ -336,11 +356,7 @@ __global__ void __launch_bounds__(TPB) k_u_hbya(MeshView m, const int8_t* __rest
     each_slot(m, tyU, c, [&](int b, int) { bd += ic[k * B + b]; });
     bd = -bd;
     each_slot(m, tyU, c, [&](int b, int) { bd += (ic[b] + ic[B + b] + ic[2 * B + b]) / 3; });
-    double Hl = 0.0;
-    each_face<WT>(m, c, [&](int f, int oc, bool own) {
-      if (own) Hl -= upper[f] * Uk[oc]; else Hl -= lower[f] * Uk[oc];
-    });
-    double h = bd * Uk[c] + (Hl + src[k * C + c]);
+    double h = bd * Uk[c] + (Hl[k] + src[k * C + c]);
     each_slot(m, tyU, c, [&](int b, int t) {
       h += bc_coupled(t) ? bc[k * B + b] * nbrv(m, Uk, bU + k * B, b) : bc[k * B + b];
     });
@@ -542,9 +558,10 @@ __global__ void k_p_cell_post(MeshView m, const int8_t* __restrict__ tyP, const 
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double g[3] = {0.0, 0.0, 0.0};
+  const double pcc = p[c];
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
-    const double pf = interp_f(m.w[f], p[o], p[n]);
+    const double pn = p[o2];
+    const double pf = own ? interp_f(m.w[f], pcc, pn) : interp_f(m.w[f], pn, pcc);
 #pragma unroll
     for (int k = 0; k < 3; ++k) { const double v = m.Sf[k * F + f] * pf; if (own) g[k] += v; else g[k] -= v; }
   });
@@ -661,6 +678,141 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
   for (int s = 0; s < S; ++s) dad = dad + lap[s] / vol;
   dAD[c] = dad;
   // boundary fields of the non-coupled slots (coupled slots interpolate cell values downstream)
+  each_slot(m, tyY, c, [&](int b, int t) {
+    if (bc_coupled(t)) return;
+    const double ms = m.bmagSf[b];
+    const double nv[3] = {m.bSf[b] / ms, m.bSf[B + b] / ms, m.bSf[2 * B + b] / ms};
+    double bg[S][3];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
+      const double corr = sn - (nv[0] * g[s][0] + nv[1] * g[s][1] + nv[2] * g[s][2]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) bg[s][k] = g[s][k] + nv[k] * corr;
+    }
+    double bse[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s) a += brhoD[s * B + b] * bg[s][k];
+      bse[k] = a;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        a += bhai[s * B + b] * (brhoD[s * B + b] * bg[s][k] - bY[s * B + b] * bse[k]);
+      bsumE[k * B + b] = bse[k];
+      bhD[k * B + b] = a;
+    }
+  });
+}
+
+// k_y_prep, species-outer over the solver's gather rows (hex meshes, W = 6): the cell's six faces'
+// indices, geometry and neighbour alpha are loaded once up front, then each species loads its twelve
+// neighbour values (Y, hai at the six neighbours) together -- two dependent memory levels per cell instead
+// of the face walk's two to three per face, so a thread keeps up to twelve gathers in flight. Per species
+// the faces are summed in the same sequential order (then the cell's boundary slots), so every
+// accumulator is bitwise the face walk's.
+template <int S>
+__global__ void __launch_bounds__(TPB) k_y_prep_rows(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
+    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
+    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
+    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
+  constexpr int WT = 6;
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  int es[WT], cs[WT];
+#pragma unroll
+  for (int k = 0; k < WT; ++k) { es[k] = m.esrc[k * C + c]; cs[k] = m.ecol[k * C + c]; }
+  double fw[WT], f0[WT], f1[WT], f2[WT], fms[WT], fdc[WT], fan[WT];
+#pragma unroll
+  for (int k = 0; k < WT; ++k) {
+    const bool live = es[k] >= 0;
+    const int f = live ? es[k] >> 1 : 0;
+    const int o2 = live ? cs[k] : c;
+    fw[k] = m.w[f]; f0[k] = m.Sf[f]; f1[k] = m.Sf[F + f]; f2[k] = m.Sf[2 * F + f];
+    fms[k] = m.magSf[f]; fdc[k] = m.dc[f]; fan[k] = alpha[o2];
+  }
+  const double ac = alpha[c];
+  const double vol = m.V[c];
+  const int sb0 = m.cbStart[c], sb1 = m.cbStart[c + 1];
+  double g[S][3];
+  double dad = 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const double yc = Y[s * C + c];
+    const double ahc = ac * hai[s * C + c];
+    double yn[WT], hn[WT];
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      const int o2 = es[k] >= 0 ? cs[k] : c;
+      yn[k] = Y[s * C + o2];
+      hn[k] = hai[s * C + o2];
+    }
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0, lap = 0.0;
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      if (es[k] < 0) continue;
+      const bool own = (es[k] & 1) != 0;
+      const double w = fw[k];
+      const double ahn = fan[k] * hn[k];
+      const double yf = own ? interp_f(w, yc, yn[k]) : interp_f(w, yn[k], yc);
+      const double v0 = f0[k] * yf, v1 = f1[k] * yf, v2 = f2[k] * yf;
+      const double gam = own ? interp_f(w, ahc, ahn) : interp_f(w, ahn, ahc);
+      const double dy = own ? yn[k] - yc : yc - yn[k];
+      const double v = gam * fms[k] * (fdc[k] * dy);
+      if (own) { g0 += v0; g1 += v1; g2 += v2; lap += v; }
+      else { g0 -= v0; g1 -= v1; g2 -= v2; lap -= v; }
+    }
+    for (int kk = sb0; kk < sb1; ++kk) {
+      const int b = m.cbSlot[kk];
+      const int t = tyY[b];
+      if (t == EMPTY) continue;
+      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
+      g0 += m.bSf[b] * yf; g1 += m.bSf[B + b] * yf; g2 += m.bSf[2 * B + b] * yf;
+      double v;
+      if (bc_coupled(t)) {
+        const int pc = m.partner[b];
+        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+        v = interp_b(m.bw[b], ahc, an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc));
+      } else {
+        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc) : 0.0;
+        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+      }
+      lap += v;
+    }
+    g[s][0] = g0 / vol; g[s][1] = g1 / vol; g[s][2] = g2 / vol;
+    dad = dad + lap / vol;
+  }
+  if (gout) {
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gout[(3L * s + k) * C + c] = g[s][k];
+  }
+  double se[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const double rd = rhoD[s * C + c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) se[k] += rd * g[s][k];
+  }
+  double hd[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const double rd = rhoD[s * C + c], h = hai[s * C + c], yc = Y[s * C + c];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hd[k] += h * (rd * g[s][k] - yc * se[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { sumE[k * C + c] = se[k]; hD[k * C + c] = hd[k]; }
+  dAD[c] = dad;
+  // boundary fields of the non-coupled slots (as k_y_prep)
   each_slot(m, tyY, c, [&](int b, int t) {
     if (bc_coupled(t)) return;
     const double ms = m.bmagSf[b];
@@ -1224,17 +1376,18 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0, divK = 0.0, divh = 0.0;
+  const double ac = alpha[c], Kc = K[c], hc0 = hD[c], hc1 = hD[C + c], hc2 = hD[2 * C + c];   // own cell
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const int o = own ? c : o2, n = own ? o2 : c;
     const double ph = phi[f], w = m.w[f];
+    auto fi = [&](double vc, double vn) { return own ? interp_f(w, vc, vn) : interp_f(w, vn, vc); };
     const double wu = ph >= 0 ? 1.0 : 0.0;
     const double L1 = -wu * ph, U1 = L1 + ph;
-    const double UL = m.dc[f] * (interp_f(w, alpha[o], alpha[n]) * m.magSf[f]);
+    const double UL = m.dc[f] * (fi(ac, alpha[o2]) * m.magSf[f]);
     if (own) { d1 -= L1; lower[f] = L1 - UL; upper[f] = U1 - UL; } else d1 -= U1;
     dL -= UL;
-    const double vk = ph * interp_f(w, K[o], K[n]);
-    const double vh = m.Sf[f] * interp_f(w, hD[o], hD[n]) + m.Sf[F + f] * interp_f(w, hD[C + o], hD[C + n]) +
-                      m.Sf[2 * F + f] * interp_f(w, hD[2 * C + o], hD[2 * C + n]);
+    const double vk = ph * fi(Kc, K[o2]);
+    const double vh = m.Sf[f] * fi(hc0, hD[o2]) + m.Sf[F + f] * fi(hc1, hD[C + o2]) +
+                      m.Sf[2 * F + f] * fi(hc2, hD[2 * C + o2]);
     if (own) { divK += vk; divh += vh; } else { divK -= vk; divh -= vh; }
   });
   each_slot(m, tyK, c, [&](int b, int t) { divK += bphi[b] * bface(m, t, K, bK, b, c); });
@@ -1304,6 +1457,10 @@ template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim
 // ====================================================================== launchers
 #define LAUNCH(kernel, n, ...) \
   do { KScope _ks(x, #kernel); if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
+       DFMI_HIP(hipGetLastError()); } while (0)
+// a launch timed under another kernel's name (a variant of that kernel: the bench rooflines key on the name)
+#define LAUNCH_AS(name, kernel, n, ...) \
+  do { KScope _ks(x, name); if ((n) > 0) hipLaunchKernelGGL(kernel, dim3(blocks_for((n), TPB)), dim3(TPB), 0, x.stream, __VA_ARGS__); \
        DFMI_HIP(hipGetLastError()); } while (0)
 
 // kernels templated on the ELL width: the unrolled path for hex meshes (W = 6), the CSR walk otherwise
@@ -1459,10 +1616,22 @@ void y_prep(Ctx& x) {
   double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
 // (k_y_prep: the CSR walk measured faster than the gather rows -- 667 vs 848 us on the 2M box; its
 // 243 VGPRs leave no room for the up-front row loads)
-#define CALL(NS) LAUNCH((k_y_prep<NS, 0>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
-                        x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),    \
-                        x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"),         \
-                        x.f("diffAlphaD"), gout)
+// (DFMI_YPREP_ROWS=1: the species-outer row kernel k_y_prep_rows on hex meshes)
+  const char* erows = std::getenv("DFMI_YPREP_ROWS");
+  const bool prep_rows = face_rows(x) && erows && std::atoi(erows) != 0;
+#define CALL(NS)                                                                                                     \
+  do {                                                                                                               \
+    if (prep_rows)                                                                                                   \
+      LAUNCH_AS("k_y_prep", (k_y_prep_rows<NS>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
+             x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
+             x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
+             gout);                                                                                                  \
+    else                                                                                                             \
+      LAUNCH((k_y_prep<NS, 0>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"),   \
+             x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
+             x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
+             gout);                                                                                                  \
+  } while (0)
 #define GEN(CH) LAUNCH_SWG(k_y_prep_gen, CH, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),     \
                        x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
                        x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                  \
