@@ -132,9 +132,11 @@ struct Sys {
 
 // per system: ELL values, dS = diag + sum internalCoeffs, rhs = source + non-coupled boundaryCoeffs
 // (fvMatrix::addBoundaryDiag / addBoundarySource(source, false)), slot order as the sequential code
+// vshared: the systems share one operator (U's components: one LDU, and the coupled-slot coefficients of
+// translational cyclic / processor patches do not depend on the component), so only system 0 writes val
 __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, const int* __restrict__ sys_map, int W,
                             const int* __restrict__ esrc, long Ce, double* __restrict__ val, double* __restrict__ dS,
-                            double* __restrict__ rhs) {
+                            double* __restrict__ rhs, int vshared = 0) {
   const int s = blockIdx.y;
   const int ms = sys_map ? sys_map[s] : s;
   const long C = m.C;
@@ -143,8 +145,9 @@ __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, co
   const double* ic = q.ic + ms * q.bstride;
   const double* bc = q.bc + ms * q.bstride;
   double* vs = val + (long)s * W * C;
+  const bool wv = !(vshared && s > 0);
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
-    for (int k = 0; k < W; ++k) {
+    for (int k = 0; wv && k < W; ++k) {
       const int e = esrc[k * C + c];
       double v;
       if (e == PAD) v = 0.0;
@@ -190,7 +193,7 @@ __global__ void k_copy_x(long C, long Ce, Sys q, const int* __restrict__ sys_map
 // scal[s*16 + k]: 0 rho, 1 rho_old, 2 alpha, 3 omega, 4 res0, 5 res, 6 active, 7 iters, 8 rho_new (the
 // update kernel writes it, the next SpMV publishes it as rho: no scalar is rewritten by the kernel whose
 // other blocks read it)
-struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; };
+struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; int vshared; };
 constexpr int BCG_VECS = 9;
 
 // y = (A in)_c / D_c = in_c + (sum_k val in_j) / D_c
@@ -209,7 +212,7 @@ template <int WT>
 __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const int* __restrict__ col,
                                                   const double* __restrict__ val, BV b, double* partial) {
   const int s = blockIdx.y;
-  const double* vs = val + (long)s * W * C;
+  const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
@@ -245,7 +248,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const
     st[6] = stop ? 0.0 : 1.0;
   }
   if (stop) return;
-  const double* vs = val + (long)s * W * C;
+  const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
   double acc[1] = {0.0};
   for_rows(C, rs, [&](int c) {
     const long i = s * Ce + c;
@@ -286,7 +289,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, cons
   const double alpha = v1[0] != 0.0 ? st[0] / v1[0] : 0.0;
   if (leader() && rows.part != 2) st[2] = alpha;
   const int W = WT > 0 ? WT : W_;
-  const double* vs = val + (long)s * W * C;
+  const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
   const double* rs = b.r + s * Ce;
   const double* ws = b.v + s * Ce;
   const double* hs = b.sv + s * Ce;
@@ -462,7 +465,7 @@ __global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, con
   const int s = blockIdx.x;
   const int W = WT > 0 ? WT : W_;
   double* st = scal + s * NSCAL;
-  const double* vs = val + (long)s * W * C;
+  const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
   double *r = b.r + s * Ce, *r0 = b.r0 + s * Ce, *p = b.p + s * Ce, *v = b.v + s * Ce, *t = b.t + s * Ce;
   const double* dS = b.dS + s * Ce;
   double* xv = q.x + (sys_map ? sys_map[s] : s) * q.xstride;
@@ -921,7 +924,7 @@ void bicg_rows_from_ldu_Y(Ctx& x) {
   Sys q{A.lower, A.upper, A.diag, A.source, A.ic, A.bc, x.Fs, x.Fs, C, C, x.B, x.f("Y"), C};
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   hipLaunchKernelGGL(k_ell_build, dim3(nblk, nsys), dim3(TPB), 0, x.stream, x.view(), x.st("Y"), q,
-                     (const int*)x.ws.sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs);
+                     (const int*)x.ws.sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs, 0);
   DFMI_HIP(hipGetLastError());
 }
 
@@ -991,8 +994,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   }
   const long N = nsys * Ce;
   double* base = WS.buf.p;
+  // U's three components share one operator: built and read once (k_ell_build vshared)
+  const int vshared = (!prebuilt && nsys > 1 && lstride == 0 && ustride == 0 && std::string(eqn) == "U") ? 1 : 0;
   BV b{base, base + N, base + 2 * N, base + 3 * N, base + 4 * N, base + 5 * N, base + 6 * N, base + 7 * N,
-       base + 8 * N};
+       base + 8 * N, vshared};
   double* val = base + BCG_VECS * N;
   // one partial buffer per reduction site (a converged system's last sums stay intact)
   double* pR = val + (size_t)nsys * W * C;          // (||D r||^2, rho0 | 0): init, xp
@@ -1005,7 +1010,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   Launch L{x, nblk, nsys};
   if (!prebuilt) {
     KScope _ks(x, "k_ell_build");
-    hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, smap, W, x.ell.src.p, Ce, val, b.dS, b.rhs);
+    hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, smap, W, x.ell.src.p, Ce, val, b.dS, b.rhs, vshared);
   }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, smap, b.xw); }
   DFMI_HIP(hipGetLastError());
@@ -1084,7 +1089,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   dim3 g(nblk), bl(TPB);
   Launch L{x, nblk, 1};
   const bool amg = cfg.precond == 1;
-  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs); }
+  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, 0); }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());
   if (amg) {
