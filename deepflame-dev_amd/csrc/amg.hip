@@ -450,7 +450,7 @@ void amg_setup(Ctx& x) {
     AmgLevel c;
     std::vector<int> ccol;
     Graph cg;
-    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, a.lv.size() == 1 ? (int)env_d("DFMI_AMG_L0_PASSES", 3) : 3);
+    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, a.lv.size() == 1 ? (int)env_d("DFMI_AMG_L0_PASSES", 3) : (int)env_d("DFMI_AMG_LN_PASSES", 3));
     DFMI_HIP(hipStreamSynchronize(x.stream));
     const bool stalled = c.n * 2 > a.lv.back().n;
     a.lv.push_back(std::move(c));
