@@ -7,8 +7,10 @@ network transport (sockets over loopback) instead of P2P/xGMI. Everything above 
 product path the 8-GPU run takes: ncclCommInitRank from a unique id, one ncclSend/ncclRecv group per
 exchange point, ncclAllGather of the per-rank partial sums, the comm stream of the overlapped halos.
 
-Rank 0 gathers the fields (gloo), runs the undecomposed mesh on the same GPU and the oracle, and writes
-the relative errors to --out (JSON). Launched by tests/test_gpu_rccl.py:
+Rank 0 gathers the fields (through files), runs the undecomposed mesh on the same GPU and the oracle
+(--no-oracle for meshes beyond its reach), and writes the relative errors to --out (JSON). Launched by
+tests/test_gpu_rccl.py and, at BASELINE config 5's size (256^3 = 16.8M cells, 8 ranks 2x2x2), by
+scripts/rccl_config5.sh:
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P \
       scripts/rccl_ranks.py --decomp 2,1,1 --out gpurun_out/rccl.json
 """
@@ -40,6 +42,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--walls", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/rccl.json")
+    ap.add_argument("--no-oracle", action="store_true", help="skip the oracle (meshes too large for it)")
+    ap.add_argument("--tol", type=float, default=1e-14, help="relative solver tolerance of every equation")
     a = ap.parse_args()
     decomp = tuple(int(x) for x in a.decomp.split(","))
     nx, ny, nz = (int(x) for x in a.mesh.split(","))
@@ -60,15 +64,16 @@ def main():
     dt = 1e-6
     periodic = (not a.walls,) * 3
     grad = (1.0, 1.3, 1.0)
-    mg = hex_box(nx, ny, nz, lengths=L, gradings=grad, periodic=periodic)
-    f = case.tgv_fields(mg, ym["species"], kernel_radius=1.2e-3)
+    # the undecomposed mesh only on rank 0 (its reference run); every rank's initial state is the same
+    # analytic TGV field evaluated at its own cell centres
+    mg = hex_box(nx, ny, nz, lengths=L, gradings=grad, periodic=periodic) if RANK == 0 else None
 
     def setup(m, comm=None):
         ctx = Context(0)
         case.setup_context(ctx, m, t, inert, dt, case.default_patch_types(m), comm=comm)
         for e in ("U", "Y", "E"):
-            ctx.set_solver(e, 300, 1e-14, 1e-300)
-        ctx.set_solver("p", 3000, 1e-14, 1e-300)
+            ctx.set_solver(e, 300, a.tol, 1e-300)
+        ctx.set_solver("p", 3000, a.tol, 1e-300)
         return ctx
 
     def fields(ctx, n):
@@ -82,7 +87,9 @@ def main():
     uid = [Context.unique_id() if RANK == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     c = setup(m, comm={"uid": uid[0], "nranks": WORLD, "rank": RANK})
-    case.init_state(c, m, t.S, f["T"][g], f["p"][g], f["U"][:, g], f["Y"][:, g])
+    fl = case.tgv_fields(m, ym["species"], kernel_radius=1.2e-3)
+    case.init_state(c, m, t.S, fl["T"], fl["p"], fl["U"], fl["Y"])
+    del fl
     c.call("pre_time_step")
     for _ in range(a.steps):
         c.time_step(2)
@@ -90,9 +97,15 @@ def main():
     mine["gid"] = g
     mine["p_iters"] = int(c.solver_stats("p")[0])
     c.close()
-    allr = [None] * WORLD
-    dist.all_gather_object(allr, mine)
+    # fields travel through files (a 16M-cell run would push GBs through the object collectives)
+    import tempfile
+    xdir = [tempfile.mkdtemp(prefix="dfmi_rccl_") if RANK == 0 else None]
+    dist.broadcast_object_list(xdir, src=0)
+    np.savez(os.path.join(xdir[0], f"rank{RANK}.npz"), **{k: np.asarray(v) for k, v in mine.items()})
+    del mine
+    dist.barrier()
     if RANK == 0:
+        allr = [dict(np.load(os.path.join(xdir[0], f"rank{r}.npz"))) for r in range(WORLD)]
         glob = {}
         for n, k in (("T", 1), ("p", 1), ("rho", 1), ("he", 1), ("U", 3), ("Y", t.S)):
             arr = np.zeros((k, mg.n_cells))
@@ -100,12 +113,15 @@ def main():
                 arr[:, o["gid"]] = o[n].reshape(k, -1)
             glob[n] = arr.reshape(-1, mg.n_cells) if k > 1 else arr[0]
         ref_ctx = setup(mg)
+        f = case.tgv_fields(mg, ym["species"], kernel_radius=1.2e-3)
         case.init_state(ref_ctx, mg, t.S, f["T"], f["p"], f["U"], f["Y"])
+        del f
         ref_ctx.call("pre_time_step")
-        res = {"world": WORLD, "decomp": list(decomp), "overlap": a.overlap, "steps": a.steps,
-               "p_iters_per_rank": [o["p_iters"] for o in allr], "vs_single_domain": {}, "vs_oracle": {}}
+        res = {"world": WORLD, "decomp": list(decomp), "mesh": [nx, ny, nz], "cells": mg.n_cells,
+               "overlap": a.overlap, "steps": a.steps, "tol": a.tol,
+               "p_iters_per_rank": [int(o["p_iters"]) for o in allr], "vs_single_domain": {}, "vs_oracle": {}}
         orc = None
-        if a.steps == 1:
+        if a.steps == 1 and not a.no_oracle:
             import oracle as O
             st = case.pull_state(ref_ctx, mg, t.S)
             orc = O.Oracle(mg, t, {k: v.copy() for k, v in st.items()}, case.default_patch_types(mg), inert, 1.0 / dt)

@@ -52,3 +52,15 @@ def test_rccl_four_ranks_walls_two_steps(tmp_path):
     assert len(set(r["p_iters_per_rank"])) == 1, r
     for n, e in r["vs_single_domain"].items():
         assert e < 1e-9, (n, e, r)
+
+
+def test_rccl_eight_ranks_config5_layout(tmp_path):
+    """BASELINE config 5's decomposition (2x2x2 blocks, 8 ranks, processorCyclic wrap-around) at a small
+    mesh: eight RCCL processes vs the single-domain run and the oracle. (The full 256^3 = 16.8M-cell run
+    of the same script is scripts/rccl_config5.sh, recorded in profiles/.)"""
+    r = _launch(tmp_path, "2,2,2", 0, mesh="16,16,16")
+    assert r["world"] == 8 and len(set(r["p_iters_per_rank"])) == 1, r
+    for n, e in r["vs_single_domain"].items():
+        assert e < 1e-9, (n, e, r)
+    for n, e in r["vs_oracle"].items():
+        assert e < 1e-9, ("oracle", n, e, r)
