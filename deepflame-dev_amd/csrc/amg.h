@@ -31,7 +31,8 @@ struct Amg {
   double omega = 0.85;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
-  int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
+  int l0_sweeps = 1;
+  bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)       // weighted-Jacobi sweeps before and after the coarse correction on level 0
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;

@@ -55,7 +55,7 @@ __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, co
       a += src >= 0 ? (double)fval[src] : (double)fD[-src - 1];
     }
     if (s < slots - 1) cval[(long)s * nc + I] = (TC)a;
-    else cD[I] = (TC)a;
+    else cD[I] = e0 == e1 ? (TC)1 : (TC)a;   // an empty (padding) cell of a padded level: unit diagonal
   }
 }
 
@@ -166,6 +166,33 @@ __global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, const int* 
     for (int w = 0; w < TPB / 64; ++w) a += sh[w];
     partial[blockIdx.x] = a;
   }
+}
+
+// padded coarse levels (pad_levels): first sweep from zero + residual as k_smooth_res, and the restriction
+// to the next level summed over the 8 lanes of the aggregate (in member order, as k_restrict) -- n is a
+// multiple of 8 and every aligned group of 8 threads is one aggregate, so a group exits or runs together
+template <int WT, class T>
+__global__ void __launch_bounds__(TPB) k_smooth_res_r8(int n, int W_, const int* __restrict__ col,
+                                                       const T* __restrict__ val, const T* __restrict__ D,
+                                                       const T* __restrict__ b, T omega, T* __restrict__ x,
+                                                       T* __restrict__ bnext, const double* act) {
+  const int W = WT > 0 ? WT : W_;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= n || (act && *act == 0.0)) return;
+  const T bc = b[c];
+  const T xc = omega * bc / D[c];
+  T y = D[c] * xc;
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const int j = col[(long)k * n + c];
+    if (j < n) y += val[(long)k * n + c] * (omega * b[j] / D[j]);
+  }
+  x[c] = xc;
+  const T r = bc - y;
+  T s = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) s += __shfl(r, m, 8);
+  if ((threadIdx.x & 7) == 0) bnext[c >> 3] = s;
 }
 
 template <class T>
@@ -366,8 +393,9 @@ __global__ void __launch_bounds__(CTPB) k_amg_coarse(CoarseArgs<T> a) {
 // ---------------------------------------------------------------- host: hierarchy
 // (aggregation in amg_graph.h, shared with the CPU-A baseline; here the result is uploaded)
 void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLevel& c, std::vector<int>& ccol,
-                Graph& cg, hipStream_t st, int passes) {
+                Graph& cg, hipStream_t st, int passes, std::vector<int>& agg_host) {
   AmgCoarse k = amg_coarsen(fcol, f.W, f.n, g, passes);
+  agg_host = k.agg;
   f.agg.upload(k.agg, st);
   f.mstart.upload(k.mstart, st);
   f.members.upload(k.members, st);
@@ -381,6 +409,61 @@ void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLe
 }
 
 double env_d(const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; }
+
+// Levels 1 .. L-2 renumbered so that the (at most 8) members of every aggregate sit in one aligned group
+// of 8 consecutive cells: level l's cell of parent J, sibling m (members in their previous order) gets
+// index 8 J' + m, J' the parent's new index (numbered the same way from the coarsest level down). Unused
+// slots are empty cells (no couplings, unit diagonal, zero right-hand side). The restriction of such a
+// level is then a sum over 8 adjacent lanes inside the smoothing kernel (k_smooth_res_r8), so levels
+// 1 .. L-2 need one launch on the way down instead of two. Level 0 keeps the mesh order. Member order
+// inside an aggregate is unchanged, so every restriction sums the same values in the same order.
+void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vector<int>>& aggs) {
+  Amg& a = x.amg;
+  const int L = (int)a.lv.size();
+  if (L < 3) return;
+  // new index of every level-l cell, from the coarsest level down (level L-1 keeps its numbering)
+  std::vector<std::vector<int>> pi(L);
+  std::vector<int> nn(L);
+  nn[L - 1] = a.lv[L - 1].n;
+  pi[L - 1].resize(nn[L - 1]);
+  std::iota(pi[L - 1].begin(), pi[L - 1].end(), 0);
+  for (int l = L - 2; l >= 1; --l) {
+    const std::vector<int>& ag = aggs[l];   // level l -> level l + 1 (old numbering)
+    std::vector<int> cnt(a.lv[l + 1].n, 0);
+    pi[l].resize(a.lv[l].n);
+    for (int v = 0; v < a.lv[l].n; ++v) {
+      const int m = cnt[ag[v]]++;
+      if (m >= 8) return;                    // an aggregate of more than 8 cells: keep the plain levels
+      pi[l][v] = 8 * pi[l + 1][ag[v]] + m;
+    }
+    nn[l] = 8 * nn[l + 1];
+  }
+  // rebuild the member lists, coarse columns and Galerkin lists in the new numbering
+  std::vector<int> fcol = col0;
+  int Wf = a.lv[0].W, nf = a.lv[0].n;
+  for (int l = 0; l + 1 < L; ++l) {
+    AmgCoarse r;
+    r.agg.resize(nf);
+    if (l == 0) for (int v = 0; v < nf; ++v) r.agg[v] = pi[1][aggs[0][v]];
+    else for (int v = 0; v < nf; ++v) r.agg[v] = v >> 3;
+    amg_level_data(fcol, Wf, nf, nn[l + 1], r);
+    AmgLevel& f = a.lv[l];
+    AmgLevel& c = a.lv[l + 1];
+    f.agg.upload(r.agg, x.stream);
+    f.mstart.upload(r.mstart, x.stream);
+    f.members.upload(r.members, x.stream);
+    f.gstart.upload(r.gstart, x.stream);
+    f.gsrc.upload(r.gsrc, x.stream);
+    c.n = r.nc;
+    c.W = r.Wc;
+    c.col.upload(r.ccol, x.stream);
+    fcol.swap(r.ccol);
+    Wf = c.W;
+    nf = c.n;
+  }
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  a.padded = true;
+}
 
 }  // namespace
 
@@ -445,12 +528,15 @@ void amg_setup(Ctx& x) {
   a.lv[0].n = C;
   a.lv[0].W = x.ell.W;
   std::vector<int> fcol = col;
+  std::vector<std::vector<int>> aggs;   // host copies of each level's fine -> coarse map
   auto too_big = [&](const AmgLevel& l) { return l.n > a.coarsest || (size_t)l.n * l.W > 6144; };
   while (too_big(a.lv.back())) {
     AmgLevel c;
     std::vector<int> ccol;
     Graph cg;
-    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, a.lv.size() == 1 ? (int)env_d("DFMI_AMG_L0_PASSES", 3) : (int)env_d("DFMI_AMG_LN_PASSES", 3));
+    aggs.emplace_back();
+    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, a.lv.size() == 1 ? (int)env_d("DFMI_AMG_L0_PASSES", 3) : (int)env_d("DFMI_AMG_LN_PASSES", 3),
+               aggs.back());
     DFMI_HIP(hipStreamSynchronize(x.stream));
     const bool stalled = c.n * 2 > a.lv.back().n;
     a.lv.push_back(std::move(c));
@@ -459,6 +545,8 @@ void amg_setup(Ctx& x) {
     if (stalled) break;
   }
   DFMI_CHECK(!too_big(a.lv.back()) || a.lv.back().n <= 8, "AMG coarsening stalled above the coarsest-level capacity");
+  a.padded = false;
+  if (env_d("DFMI_AMG_PADDED", 1) != 0) pad_levels(x, col, aggs);
   if (a.lv.size() == 1) a.fp32 = false;   // a single level writes z directly: keep it in double
   for (size_t l = 0; l < a.lv.size(); ++l) {
     AmgLevel& v = a.lv[l];
@@ -583,6 +671,12 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
       else
         hipLaunchKernelGGL((k_smooth_restrict<T, T>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
                            f.members.p, f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
+      continue;
+    }
+    if (l > 0 && a.padded) {   // aggregates in aligned groups of 8: smoothing and restriction in one launch
+      KScope _ks(x, "k_smooth_res");
+      launch_w(f.W, g, x.stream, k_smooth_res_r8<0, T>, k_smooth_res_r8<6, T>, f.n, f.W, COL(l), VAL(l), DD(l),
+               (const T*)BV(l), om, XV(l), BV(l + 1), act);
       continue;
     }
     T* rcur = RV(l);

@@ -101,32 +101,12 @@ struct AmgCoarse {
   Graph cg;
 };
 
-inline AmgCoarse amg_coarsen(const std::vector<int>& fcol, int Wf, int nf, const Graph& g, int passes = 3) {
-  AmgCoarse r;
-  // `passes` pairwise passes -> aggregates of up to 2^passes cells (3: 2x2x2 on a hex mesh)
-  std::vector<int>& agg = r.agg;
-  agg.resize(nf);
-  std::iota(agg.begin(), agg.end(), 0);
-  Graph cur = g;
-  int ng = nf;
-  for (int pass = 0; pass < passes; ++pass) {
-    std::vector<int> grp;
-    ng = pair_match(cur, grp);
-    for (int v = 0; v < nf; ++v) agg[v] = grp[agg[v]];
-    cur = collapse(cur, grp, ng);
-  }
-  // renumber coarse cells by their first fine member (locality)
-  std::vector<int> first(ng, INT32_MAX);
-  for (int v = 0; v < nf; ++v) first[agg[v]] = std::min(first[agg[v]], v);
-  std::vector<int> ord(ng);
-  std::iota(ord.begin(), ord.end(), 0);
-  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return first[a] < first[b]; });
-  std::vector<int> ren(ng);
-  for (int i = 0; i < ng; ++i) ren[ord[i]] = i;
-  for (int v = 0; v < nf; ++v) agg[v] = ren[agg[v]];
-  const int nc = ng;
+// the member lists, coarse ELL columns and Galerkin contribution lists of a coarse level, given the
+// fine -> coarse map r.agg (any numbering of the nc coarse cells; a coarse cell may have no members:
+// its row is all padding and its diagonal list is empty)
+inline void amg_level_data(const std::vector<int>& fcol, int Wf, int nf, int nc, AmgCoarse& r) {
+  const std::vector<int>& agg = r.agg;
   r.nc = nc;
-  r.cg = collapse(g, agg, nc);   // coarse strength graph (same collapse, renumbered)
   r.mstart.assign(nc + 1, 0);
   r.members.resize(nf);
   for (int v = 0; v < nf; ++v) r.mstart[agg[v] + 1]++;
@@ -182,6 +162,34 @@ inline AmgCoarse amg_coarsen(const std::vector<int>& fcol, int Wf, int nf, const
     r.gstart[s + 1] = (int)r.gsrc.size();
   }
   if (r.gsrc.empty()) r.gsrc.push_back(0);
+}
+
+inline AmgCoarse amg_coarsen(const std::vector<int>& fcol, int Wf, int nf, const Graph& g, int passes = 3) {
+  AmgCoarse r;
+  // `passes` pairwise passes -> aggregates of up to 2^passes cells (3: 2x2x2 on a hex mesh)
+  std::vector<int>& agg = r.agg;
+  agg.resize(nf);
+  std::iota(agg.begin(), agg.end(), 0);
+  Graph cur = g;
+  int ng = nf;
+  for (int pass = 0; pass < passes; ++pass) {
+    std::vector<int> grp;
+    ng = pair_match(cur, grp);
+    for (int v = 0; v < nf; ++v) agg[v] = grp[agg[v]];
+    cur = collapse(cur, grp, ng);
+  }
+  // renumber coarse cells by their first fine member (locality)
+  std::vector<int> first(ng, INT32_MAX);
+  for (int v = 0; v < nf; ++v) first[agg[v]] = std::min(first[agg[v]], v);
+  std::vector<int> ord(ng);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return first[a] < first[b]; });
+  std::vector<int> ren(ng);
+  for (int i = 0; i < ng; ++i) ren[ord[i]] = i;
+  for (int v = 0; v < nf; ++v) agg[v] = ren[agg[v]];
+  const int nc = ng;
+  r.cg = collapse(g, agg, nc);   // coarse strength graph (same collapse, renumbered)
+  amg_level_data(fcol, Wf, nf, nc, r);
   return r;
 }
 
