@@ -40,23 +40,23 @@ constexpr int CTPB = 1024;
 // Value type T is the V-cycle precision (double, or float in the default mixed mode); TB the type
 // of a level's right-hand side (level 0: the PCG residual, always double); TO the type written out.
 
-// coarse values: out[s * nc + I] = sum (in double) of the fine sources listed for (slot s, cell I)
+// coarse values: out[s * nc + I] = sum (in double) of the fine sources listed for (slot s, cell I); one
+// thread per (slot, cell) entry, so a cell's lists are walked in parallel rather than one after another
 template <class TF, class TC>
 __global__ void k_galerkin(int nc, int slots, const int* __restrict__ gstart, const int* __restrict__ gsrc,
                            const TF* __restrict__ fval, const TF* __restrict__ fD, TC* __restrict__ cval,
                            TC* __restrict__ cD) {
-  const int I = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I >= nc) return;
-  for (int s = 0; s < slots; ++s) {
-    const long e0 = gstart[(long)s * nc + I], e1 = gstart[(long)s * nc + I + 1];
-    double a = 0.0;
-    for (long e = e0; e < e1; ++e) {
-      const int src = gsrc[e];
-      a += src >= 0 ? (double)fval[src] : (double)fD[-src - 1];
-    }
-    if (s < slots - 1) cval[(long)s * nc + I] = (TC)a;
-    else cD[I] = e0 == e1 ? (TC)1 : (TC)a;   // an empty (padding) cell of a padded level: unit diagonal
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)nc * slots) return;
+  const int s = (int)(t / nc), I = (int)(t % nc);
+  const long e0 = gstart[t], e1 = gstart[t + 1];
+  double a = 0.0;
+  for (long e = e0; e < e1; ++e) {
+    const int src = gsrc[e];
+    a += src >= 0 ? (double)fval[src] : (double)fD[-src - 1];
   }
+  if (s < slots - 1) cval[t] = (TC)a;
+  else cD[I] = e0 == e1 ? (TC)1 : (TC)a;   // an empty (padding) cell of a padded level: unit diagonal
 }
 
 // level-0 operator rounded to the V-cycle precision (once per solve)
@@ -580,7 +580,7 @@ void amg_galerkin(Ctx& x, const double* val0, const double* D0) {
     AmgLevel& f = a.lv[l];
     AmgLevel& c = a.lv[l + 1];
     KScope _ks(x, "k_galerkin");
-    const dim3 g(blocks_for(c.n, TPB));
+    const dim3 g(blocks_for((long)c.n * (c.W + 1), TPB));
     if (!a.fp32)
       hipLaunchKernelGGL((k_galerkin<double, double>), g, dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p, f.gsrc.p,
                          l == 0 ? val0 : (const double*)f.val.p, l == 0 ? D0 : (const double*)f.D.p, c.val.p, c.D.p);
