@@ -605,7 +605,7 @@ void launch_w(int W, dim3 g, hipStream_t st, K0 k0, K6 k6, A... a) {
 // z = M^-1 r in precision T; block partials of r.z (one per block of the level-0 grid) into `partial`
 template <class T>
 void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-             double* partial, int nblk, const double* act) {
+             double* partial, int nblk, const double* act, bool l0_done) {
   constexpr bool F = std::is_same<T, float>::value;
   Amg& a = x.amg;
   const int L = (int)a.lv.size();
@@ -680,7 +680,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
       continue;
     }
     T* rcur = RV(l);
-    {
+    if (!(l == 0 && l0_done)) {
       KScope _ks(x, "k_smooth_res");
       if (l == 0)
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
@@ -780,16 +780,23 @@ AmgView<double> amg_view_f64(Ctx& x, const double* val0, const double* D0, const
   return amg_view_t<double>(x, val0, D0, col0);
 }
 
+bool amg_l0_fusable(const Ctx& x) {
+  const Amg& a = x.amg;
+  return a.fp32 && a.lv.size() >= 2 && a.l0_sweeps == 1 && a.fused_coarse == 0 &&
+         !(a.coop_blocks > 0 && a.lv.size() >= 3);
+}
+
 void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
-               double* partial, int nblk, const double* active) {
+               double* partial, int nblk, const double* active, bool l0_done) {
   Amg& a = x.amg;
+  DFMI_CHECK(!l0_done || amg_l0_fusable(x), "AMG: level-0 sweep fused on an unsupported configuration");
   auto direct = [&] {
-    if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active);
-    else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active);
+    if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
+    else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
   };
   if (!a.use_graph || !x.ktimer.targets.empty()) { direct(); return; }
   const std::array<uintptr_t, 8> key{(uintptr_t)val0, (uintptr_t)D0, (uintptr_t)col0, (uintptr_t)r, (uintptr_t)z,
-                                     (uintptr_t)partial, (uintptr_t)nblk, (uintptr_t)active};
+                                     (uintptr_t)partial, (uintptr_t)nblk * 2 + (l0_done ? 1 : 0), (uintptr_t)active};
   auto it = a.graphs.find(key);
   if (it == a.graphs.end()) {
     hipGraph_t g;

@@ -432,6 +432,45 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
   block_partials<2>(acc, partial, 0);
 }
 
+// k_cg_x<false> fused with the AMG's level-0 first sweep (one rank): the updated residual r (written to
+// rnew, the dead z buffer; the host then swaps the r and z roles) is also the
+// V-cycle's right-hand side, so the same pass forms x0 = omega r / D and res = r - A x0 in the V-cycle's
+// precision T; a neighbour's r_j is re-formed as r_j - alpha q_j (the expression the update stores), so
+// x0 and res are bitwise those of k_smooth_res on the stored r. Partials (0, r.r) as k_cg_x<false>.
+template <int WT, class T>
+__global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, const int* __restrict__ col, Red red,
+                                                     double* scal, double* __restrict__ x, CV v,
+                                                     const double* __restrict__ pnew, double* __restrict__ rnew,
+                                                     double* partial, const T* __restrict__ val0,
+                                                     const T* __restrict__ D0, T omega, T* __restrict__ x0,
+                                                     T* __restrict__ res0) {
+  if (scal[6] == 0.0) return;
+  double pv[1];
+  red_sum<1>(red, 0, pv);
+  const double rz = scal[0];
+  const double alpha = pv[0] != 0.0 ? rz / pv[0] : 0.0;
+  if (leader()) { scal[2] = alpha; scal[1] = rz; }
+  const int W = WT > 0 ? WT : W_;
+  double acc[2] = {0.0, 0.0};
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    x[c] = x[c] + alpha * pnew[c];
+    const double rr = v.r[c] - alpha * v.q[c];
+    rnew[c] = rr;   // not in place: neighbours read the old r
+    acc[1] += rr * rr;
+    const T bc = (T)rr;
+    const T xc = omega * bc / D0[c];
+    T y = D0[c] * xc;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int j = col[(long)k * C + c];
+      if (j < C) y += val0[(long)k * C + c] * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
+    }
+    x0[c] = xc;
+    res0[c] = bc - y;
+  }
+  block_partials<2>(acc, partial, 0);
+}
+
 // ============================================================== small systems: one workgroup per solve
 // A mesh of a few thousand cells (the 1D flame: 880) runs every iteration kernel at its launch floor
 // (≈ 4 µs each, ~500 per step). With one rank and C <= SMALL_C each system's whole solve runs in ONE
@@ -1154,6 +1193,9 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   const int check = amg ? 2 : 8;
   double* pold = v.pa;
   double* pnew = v.pb;
+  // one rank: the update kernel also does the V-cycle's level-0 first sweep (DFMI_CG_FUSE=0: separate)
+  const bool fuse_l0 = amg && x.nranks == 1 && !halo_active(x) && amg_l0_fusable(x) && [] {
+    const char* e = std::getenv("DFMI_CG_FUSE"); return !(e && std::atoi(e) == 0); }();
   for (int it = 0;; ++it) {
     const int np = spmv_with_halo(x, {v.z, pold}, 1, Ce, nblk, [&](RowSet rs) {
       dispatch_W(W, [&](auto wt) {
@@ -1165,6 +1207,25 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     });
     if (it >= cfg.max_iter) break;
     Red red = L.after(q1, 1, 0, np);
+    if (fuse_l0) {
+      AmgLevel& l0 = x.amg.lv[0];
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_cg_x");
+        hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.col.p, red, WS.scal.p, xsol, v,
+                           pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
+                           l0.fx.p, l0.fr.p);
+      });
+      DFMI_HIP(hipGetLastError());
+      std::swap(v.r, v.z);   // z was dead (k_cg_spmv has read it); the V-cycle writes the new z over the old r
+      Red r2 = L.after(q2, 2, 0);
+      red_rr = r2; red_rr.p += 1;
+      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, WS.scal.p + 6, true);
+      red_rz = L.after(q3, 1, 1);
+      std::swap(pold, pnew);
+      if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
+      continue;
+    }
     {
       KScope _ks(x, "k_cg_x");
       if (amg) hipLaunchKernelGGL(k_cg_x<false>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
