@@ -57,6 +57,7 @@ int orc_e_assemble();
 int orc_thermo_correct(int from_T);
 int orc_energy_gradient();
 int orc_correct_bc(const char* field, const char* bfield, const char* ptype, int ncomp);
+int orc_conv_weights();
 }
 
 struct dfmi_ctx;
@@ -97,6 +98,9 @@ struct Ctx {
   std::map<std::string, Field> fields;                  // user-visible fields (SoA [ncomp][n])
   std::map<std::string, std::vector<double>> work;      // oracle inputs/outputs that are not fields
   std::vector<double> rdt_v;
+  // schemes (dfmi_set_scheme; the oracle's "schemes" / "scheme_k" layout)
+  std::vector<int> schemes{0, 1, 1};
+  std::vector<double> scheme_k{1.0, 1.0};
   // thermo
   std::vector<double> W, nasa, visc, cond, bdiff;
   // solvers
@@ -158,6 +162,8 @@ void allocate_fields(Ctx& x) {
   for (auto n : {"lower", "upper"}) { wk(std::string("ueqn_") + n, F); wk(std::string("peqn_") + n, F); }
   wk("ueqn_source", 3 * C); wk("ueqn_internal_coeffs", 3 * B); wk("ueqn_boundary_coeffs", 3 * B);
   wk("peqn_internal_coeffs", B); wk("peqn_boundary_coeffs", B); wk("peqn_phiHbyA", F); wk("peqn_boundary_phiHbyA", B);
+  wk("conv_w", F); wk("boundary_conv_w", B);   // div(phi,Yi_h) weights (start of YEqn, reused by EEqn)
+  if (!x.work.count("boundary_delta")) wk("boundary_delta", 3 * B);
   for (auto e : {"U", "Y", "E"}) if (!x.solver.count(e)) x.solver[e] = SolverCfg{20, 1e-5, 0.0, 0};   // amgxUOptions
   if (!x.solver.count("p")) x.solver["p"] = SolverCfg{1000, 1e-5, 0.0, 1};                            // amgxpOptions
 }
@@ -177,6 +183,8 @@ void bind(Ctx& x) {
   for (auto& kv : x.ptype) orc_set_i(("ptype_" + kv.first).c_str(), kv.second.data());
   x.rdt_v = {x.rdt};
   orc_set_d("rdelta_t", x.rdt_v.data());
+  orc_set_i("schemes", x.schemes.data());
+  orc_set_d("scheme_k", x.scheme_k.data());
   for (auto& kv : x.fields) orc_set_d(kv.first.c_str(), kv.second.v.data());
   for (auto& kv : x.work) orc_set_d(kv.first.c_str(), kv.second.data());
   orc(orc_set_thermo(x.S, x.W.data(), x.nasa.data(), x.visc.data(), x.cond.data(), x.bdiff.data()), "thermo");
@@ -666,6 +674,7 @@ void do_U(Ctx& x) {
 void do_Y(Ctx& x) {
   if (x.mode == 1) chem_solve(x, 1.0 / x.rdt, "rho_old");   // thermo density of the step start (chem.hip)
   CHECK(x.mode != 2, "DNN chemistry is a GPU-path feature");
+  orc(orc_conv_weights(), "div(phi,Yi_h) weights");
   orc(orc_y_prep(), "YEqn prep");
   orc(orc_y_assemble(), "YEqn");
   const long C = x.C, F = x.F, B = x.B;
@@ -822,14 +831,16 @@ int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighb
   });
 }
 int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const double* mag_sf, const double* weight,
-                                       const double* delta_coeffs, const double* volume, const double*) {
+                                       const double* delta_coeffs, const double* volume, const double* mesh_distance) {
   return guard([&] {
     Ctx& x = ctx->x;
     CHECK(x.have_topo, "call dfmi_set_constant_indexes first");
     const long F = x.F;
-    std::vector<double> s(3 * std::max(F, 1L));
+    std::vector<double> s(3 * std::max(F, 1L)), md(3 * std::max(F, 1L), 0.0);
     for (long f = 0; f < F; ++f) for (int k = 0; k < 3; ++k) s[k * F + f] = sf[f * 3 + k];
+    if (mesh_distance) for (long f = 0; f < F; ++f) for (int k = 0; k < 3; ++k) md[k * F + f] = mesh_distance[f * 3 + k];
     x.work["sf"] = s;
+    x.work["mesh_distance"] = md;   // the limited schemes' d (LimitedScheme::calcLimiter)
     x.work["mag_sf"].assign(mag_sf, mag_sf + F);
     x.work["weight"].assign(weight, weight + F);
     x.work["delta_coeffs"].assign(delta_coeffs, delta_coeffs + F);
@@ -891,6 +902,48 @@ int dfmi_renumber_faces(int, int, const int*, const int*, const int*, int*, int*
 }
 
 int dfmi_set_traversal(dfmi_ctx*, const int*) { return 0; }   // a GPU visiting order: nothing to do here
+
+int dfmi_init_boundary_delta(dfmi_ctx* ctx, const double* bd) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    CHECK(x.have_bgeom, "call dfmi_init_constant_fields_boundary first");
+    std::vector<double> s(3 * std::max(x.B, 1), 0.0);
+    for (long b = 0; b < x.B; ++b) for (int k = 0; k < 3; ++k) s[k * x.B + b] = bd[b * 3 + k];
+    x.work["boundary_delta"] = s;
+  });
+}
+
+// the same selection as the HIP library (include/dfmi.h dfmi_set_scheme); the arithmetic is the oracle's
+int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    const std::string t(term ? term : "");
+    std::vector<std::string> tok;
+    std::string cur;
+    for (char ch : std::string(scheme ? scheme : "") + " ") {
+      if (ch == ' ' || ch == '\t') { if (!cur.empty()) tok.push_back(cur); cur.clear(); } else cur += ch;
+    }
+    if (!tok.empty() && tok[0] == "Gauss") tok.erase(tok.begin());
+    CHECK(!tok.empty(), t + ": empty scheme");
+    int kind = -1;
+    double k = 1.0;
+    if (tok[0] == "upwind") kind = 0;
+    else if (tok[0] == "linear") kind = 1;
+    else if (tok[0] == "limitedLinear") kind = 2;
+    else if (tok[0] == "limitedLinear01") kind = 3;
+    else if (tok[0] == "cubic") kind = 4;
+    CHECK(kind >= 0, t + ": unsupported scheme");
+    if (kind == 2 || kind == 3) {
+      CHECK(tok.size() == 2, t + ": limitedLinear needs its coefficient k");
+      k = std::stod(tok[1]);
+      CHECK(k >= 0 && k <= 1, t + ": limitedLinear coefficient must be in [0, 1]");
+    } else CHECK(tok.size() == 1, t + ": unexpected arguments");
+    if (t == "div(phi,Yi_h)") { CHECK(kind == 0 || kind == 2 || kind == 3, t + ": upwind or limitedLinear(01)"); x.schemes[0] = kind; x.scheme_k[0] = k; }
+    else if (t == "div(phi,K)") { CHECK(kind <= 3, t + ": upwind, linear or limitedLinear(01)"); x.schemes[1] = kind; x.scheme_k[1] = k; }
+    else if (t == "div(hDiffCorrFlux)") { CHECK(kind == 1 || kind == 4, t + ": linear or cubic"); x.schemes[2] = kind; }
+    else throw Error("dfmi (CPU-A): unknown scheme term '" + t + "'");
+  });
+}
 
 int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* pt) {
   return guard([&] {

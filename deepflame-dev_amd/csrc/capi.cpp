@@ -8,6 +8,7 @@
 #include "dfmi_ctx.h"
 #include "../../include/dfmi.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <numeric>
@@ -332,18 +333,21 @@ int dfmi_set_constant_indexes(dfmi_ctx* ctx, const int* owner, const int* neighb
 
 int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const double* mag_sf, const double* weight,
                                        const double* delta_coeffs, const double* volume, const double* mesh_distance) {
-  (void)mesh_distance;   // used by limitedLinear only (disabled in the reference, dfMatrixOpBase.cu:2540-2600)
+  // mesh_distance (C[nei] - C[own]) is the d the limited schemes' limiter reads (LimitedScheme::calcLimiter);
+  // the reference's GPU path uploads it for its disabled limitedLinear (dfMatrixOpBase.cu:2540-2600)
   return guard([&] {
     Ctx& x = ctx->x;
     DFMI_CHECK(x.have_topo, "call dfmi_set_constant_indexes first");
     const long F = x.F, Fs = x.Fs;
     std::vector<double> soa(3 * std::max(Fs, 1L), 0.0), ms(std::max(Fs, 1L), 0.0), ww(std::max(Fs, 1L), 0.0),
-        dd(std::max(Fs, 1L), 0.0);
+        dd(std::max(Fs, 1L), 0.0), mdv(3 * std::max(Fs, 1L), 0.0);
     for (long f = 0; f < F; ++f) {   // AoS -> SoA, OpenFOAM face order -> face storage
       const long s = x.h_fst[f];
       for (int k = 0; k < 3; ++k) soa[k * Fs + s] = sf[f * 3 + k];
+      if (mesh_distance) for (int k = 0; k < 3; ++k) mdv[k * Fs + s] = mesh_distance[f * 3 + k];
       ms[s] = mag_sf[f]; ww[s] = weight[f]; dd[s] = delta_coeffs[f];
     }
+    x.md.upload(mdv, x.stream);
     x.Sf.upload(soa, x.stream);
     x.magSf.upload(ms, x.stream);
     x.w.upload(ww, x.stream);
@@ -403,6 +407,68 @@ int dfmi_set_patch_types(dfmi_ctx* ctx, const char* field, const int* patch_type
     }
     set_ptype(x, f, patch_type);
     DFMI_HIP(hipStreamSynchronize(x.stream));
+  });
+}
+
+int dfmi_init_boundary_delta(dfmi_ctx* ctx, const double* boundary_delta) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_CHECK(x.have_bgeom, "call dfmi_init_constant_fields_boundary first");
+    const long B = x.B;
+    std::vector<double> soa(3 * std::max(B, 1L), 0.0);
+    for (long b = 0; b < B; ++b) for (int k = 0; k < 3; ++k) soa[k * B + b] = boundary_delta[b * 3 + k];
+    x.bdv.upload(soa, x.stream);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.have_bdelta = true;
+  });
+}
+
+// "limitedLinear01 1" -> (kind, k); a leading "Gauss" accepted (system/fvSchemes divSchemes syntax)
+static void parse_scheme(const std::string& term, const std::string& text, int& kind, double& k) {
+  std::vector<std::string> tok;
+  std::string cur;
+  for (char ch : text + " ") {
+    if (ch == ' ' || ch == '\t') { if (!cur.empty()) tok.push_back(cur); cur.clear(); }
+    else cur += ch;
+  }
+  if (!tok.empty() && tok[0] == "Gauss") tok.erase(tok.begin());
+  DFMI_CHECK(!tok.empty(), term + ": empty scheme");
+  const std::string& n = tok[0];
+  k = 1.0;
+  if (n == "upwind") kind = SCH_UPWIND;
+  else if (n == "linear") kind = SCH_LINEAR;
+  else if (n == "cubic") kind = SCH_CUBIC;
+  else if (n == "limitedLinear" || n == "limitedLinear01") {
+    kind = n == "limitedLinear" ? SCH_LL : SCH_LL01;
+    DFMI_CHECK(tok.size() == 2, term + ": " + n + " needs its coefficient k");
+    char* end = nullptr;
+    k = std::strtod(tok[1].c_str(), &end);
+    DFMI_CHECK(end && *end == 0 && k >= 0 && k <= 1, term + ": limitedLinear coefficient must be a number in [0, 1]");
+    return;
+  } else throw Error("dfmi: " + term + ": unsupported scheme '" + text + "'");
+  DFMI_CHECK(tok.size() == 1, term + ": unexpected arguments in '" + text + "'");
+}
+
+int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    const std::string t(term ? term : ""), s(scheme ? scheme : "");
+    int kind;
+    double k;
+    parse_scheme(t, s, kind, k);
+    if (t == "div(phi,Yi_h)") {
+      DFMI_CHECK(kind == SCH_UPWIND || kind == SCH_LL || kind == SCH_LL01, t + ": upwind, limitedLinear or limitedLinear01");
+      bool proc = false;
+      for (int p : x.pkind) proc |= p == 2;
+      DFMI_CHECK(kind == SCH_UPWIND || !proc, t + ": limited schemes on decomposed meshes (processor patches) are not supported");
+      x.sch.yh = kind; x.sch.k_yh = k;
+    } else if (t == "div(phi,K)") {
+      DFMI_CHECK(kind != SCH_CUBIC, t + ": upwind, linear, limitedLinear or limitedLinear01");
+      x.sch.K = kind; x.sch.k_K = k;
+    } else if (t == "div(hDiffCorrFlux)") {
+      DFMI_CHECK(kind == SCH_LINEAR || kind == SCH_CUBIC, t + ": linear or cubic");
+      x.sch.hD = kind;
+    } else throw Error("dfmi: unknown scheme term '" + t + "' (div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux))");
   });
 }
 
@@ -623,7 +689,7 @@ int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
     } else if (e == "Y_ell_ref") {    // LDU assembly folded by the generic solver gather
       y_prep(x); y_assemble(x);
       bicg_rows_from_ldu_Y(x);
-    } else if (e == "E") e_assemble(x);
+    } else if (e == "E") { conv_weights(x); e_assemble(x); }   // EEqn inspected on its own: fresh div(phi,Yi_h) weights
     else if (e == "p") p_assemble(x);
     else if (e == "HbyA") u_hbya(x);
     else if (e == "p_post") p_post_solve(x);

@@ -36,6 +36,15 @@ struct MeshView {
   int W;
   double rdt;
   const int* trav;          // optional traversal order of the per-cell gather kernels (thread t -> cell)
+  const double *md, *bdv;   // C[nei] - C[own] [3][F] (face storage) and patch delta vectors [3][B] (limited schemes)
+};
+
+// interpolation / convection schemes of the terms the reference GPU path hard-wires (dfmi_set_scheme;
+// dfmi/schemes.py): div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux)
+enum SchemeKind { SCH_UPWIND = 0, SCH_LINEAR = 1, SCH_LL = 2, SCH_LL01 = 3, SCH_CUBIC = 4 };
+struct Schemes {
+  int yh = SCH_UPWIND, K = SCH_LINEAR, hD = SCH_LINEAR;
+  double k_yh = 1.0, k_K = 1.0;
 };
 
 struct Field {
@@ -153,6 +162,9 @@ struct Ctx {
   DevBuf<int8_t> sprim;
   // geometry
   DevBuf<double> Sf, magSf, w, dc, V, bSf, bmagSf, bw, bdc;
+  DevBuf<double> md, bdv;        // mesh_distance [3][Fs], boundary delta [3][B] (dfmi_init_boundary_delta)
+  bool have_bdelta = false;
+  Schemes sch;
   // per-field patch types (host, per patch) and per-slot device copies
   std::map<std::string, std::vector<int>> ptype;
   std::map<std::string, DevBuf<int8_t>> stype;
@@ -209,6 +221,7 @@ struct Ctx {
     m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
     m.rdt = rdt;
     m.trav = trav.n ? trav.p : nullptr;
+    m.md = md.p; m.bdv = bdv.p;
     return m;
   }
   double* f(const std::string& name) {
@@ -220,6 +233,18 @@ struct Ctx {
     auto it = stype.find(field);
     DFMI_CHECK(it != stype.end(), "patch types not set for field '" + field + "'");
     return it->second.p;
+  }
+  // scheme buffers (fv_kernels.hip scheme launchers): 0/1 div(phi,Yi_h) weights (faces / slots), 2/3
+  // div(phi,K) weights, 4/5 cubic flux correction of div(hDiffCorrFlux); nullptr where the term keeps
+  // the reference GPU path's scheme (upwind / linear / linear)
+  const double* sch_w(int i) {
+    static const char* names[6] = {"conv_w", "boundary_conv_w", "K_w", "boundary_K_w", "cubic_flux",
+                                   "boundary_cubic_flux"};
+    const bool on = i < 2 ? sch.yh != SCH_UPWIND : i < 4 ? sch.K != SCH_LINEAR : sch.hD == SCH_CUBIC;
+    if (!on) return nullptr;
+    auto it = fields.find(names[i]);
+    DFMI_CHECK(it != fields.end(), std::string("scheme buffer '") + names[i] + "' not computed");
+    return it->second.buf.p;
   }
   const std::vector<int>& pt(const std::string& field) {
     auto it = ptype.find(field);
@@ -267,6 +292,7 @@ void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs
 void y_post_solve(Ctx& x);
 void e_assemble(Ctx& x);
 void e_post_solve(Ctx& x);
+void conv_weights(Ctx& x);   // div(phi,Yi_h) weights (start of YEqn; EEqn reuses them)
 void copy_old(Ctx& x);
 void zero_d_step(Ctx& x, double dt);   // df0DFoam loop body for every cell
 void thermo_rho_from_psi(Ctx& x);

@@ -132,6 +132,243 @@ __global__ void k_bc_correct(MeshView m, const int8_t* __restrict__ ty, const do
   }
 }
 
+// ------------------------------------------------------------------ limited / cubic schemes
+// The terms the reference GPU path hard-wires (upwind Yi/ha, linear K and hDiffCorrFlux; dfYEqn.cu:543,
+// 587-593, dfEEqn.cu:166-174) with the schemes the reference's own cases select (system/fvSchemes:
+// div(phi,Yi_h) Gauss limitedLinear01 1 -- multivariate over every Y_i and he, YEqn.H:6-14; div(phi,K)
+// Gauss limitedLinear 1; div(hDiffCorrFlux) Gauss cubic), OpenFOAM-7 semantics as restated in
+// oracle/df_oracle.cpp (limited_weights, conv_weights, k_weights, cubic_flux) -- the same operations in
+// the same order, so the weights and fluxes are bitwise the oracle's.
+__device__ __forceinline__ double pos0(double x) { return x >= 0 ? 1.0 : 0.0; }
+__device__ __forceinline__ double sgn(double x) { return x >= 0 ? 1.0 : -1.0; }
+
+// limitedLinearLimiter<NVDTVD>::limiter (+ Limited01Limiter's bounds when b01); g = the upwind cell's gradient
+__device__ __forceinline__ double ll_limiter(double twoByk, double faceFlux, double phiP, double phiN,
+                                             const double* g, const double* dv) {
+  const double gradf = phiN - phiP;
+  const double gradcf = dv[0] * g[0] + dv[1] * g[1] + dv[2] * g[2];
+  double r;
+  if (fabs(gradcf) >= 1000 * fabs(gradf)) r = 2 * 1000 * sgn(gradcf) * sgn(gradf) - 1;
+  else r = 2 * (gradcf / gradf) - 1;
+  return fmax(fmin(twoByk * r, 1.0), 0.0);
+}
+__device__ __forceinline__ bool out01(double faceFlux, double phiP, double phiN) {
+  return (faceFlux > 0 && (phiP < 0 || phiN > 1)) || (faceFlux < 0 && (phiN < 0 || phiP > 1));
+}
+
+// Gauss linear gradient of a scalar at cell c (fvc::grad; the oracle's grad_scalar: faces in
+// increasing index, then the cell's boundary slots, / V)
+__device__ __forceinline__ void cell_grad(const MeshView& m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
+                                          const double* __restrict__ bvf, int c, double* g) {
+  const long F = m.F, B = m.B;
+  const double vc = vf[c];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  each_face<0>(m, c, [&](int f, int o2, bool own) {
+    const double w = m.w[f], vn = vf[o2];
+    const double yf = own ? interp_f(w, vc, vn) : interp_f(w, vn, vc);
+    const double v0 = m.Sf[f] * yf, v1 = m.Sf[F + f] * yf, v2 = m.Sf[2 * F + f] * yf;
+    if (own) { s0 += v0; s1 += v1; s2 += v2; } else { s0 -= v0; s1 -= v1; s2 -= v2; }
+  });
+  each_slot(m, ty, c, [&](int b, int t) {
+    const double yf = bface(m, t, vf, bvf, b, c);
+    s0 += m.bSf[b] * yf; s1 += m.bSf[B + b] * yf; s2 += m.bSf[2 * B + b] * yf;
+  });
+  const double vol = m.V[c];
+  g[0] = s0 / vol; g[1] = s1 / vol; g[2] = s2 / vol;
+}
+
+// multivariate limited weights of div(phi,Yi_h) over {Y_0 .. Y_{S-1}, he} on the internal faces (face
+// storage order). Limited01's bounds are checked first for every field (he of a real mixture leaves
+// [0, 1] almost everywhere, which makes the minimum 0 without any gradient); only faces where every
+// field passes evaluate the limiters, each from the upwind cell's Gauss gradient formed on the fly.
+__global__ void k_conv_w_face(MeshView m, int S, const int8_t* __restrict__ tyY, const int8_t* __restrict__ tyH,
+                              int b01, double twoByk, const double* __restrict__ phi, const double* __restrict__ Y,
+                              const double* __restrict__ bY, const double* __restrict__ he,
+                              const double* __restrict__ bhe, double* __restrict__ wout) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const int o = m.own[f];
+  if (o < 0) return;   // owner-slot padding
+  const int n = m.nei[f];
+  const long C = m.C, Fs = m.F, B = m.B;
+  const double ph = phi[f];
+  double lim = 0.0;
+  bool zero = false;
+  if (b01) {
+    zero = out01(ph, he[o], he[n]);
+    for (int s = 0; s < S && !zero; ++s) zero = out01(ph, Y[s * C + o], Y[s * C + n]);
+  }
+  if (!zero) {
+    const double dv[3] = {m.md[f], m.md[Fs + f], m.md[2 * Fs + f]};
+    const int cu = ph > 0 ? o : n;   // NVDTVD::r reads the upwind cell's gradient
+    for (int s = 0; s <= S; ++s) {
+      const double* v = s < S ? Y + s * C : he;
+      const double* bv = s < S ? bY + s * B : bhe;
+      double g[3];
+      cell_grad(m, s < S ? tyY : tyH, v, bv, cu, g);
+      const double l = ll_limiter(twoByk, ph, v[o], v[n], g, dv);
+      lim = s == 0 ? l : fmin(lim, l);
+    }
+  }
+  wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+}
+
+// the same on the boundary slots: coupled (cyclic) slots with the partner cell as N and the patch delta;
+// every other slot takes limiter 1 (calcLimiter's non-coupled branch), i.e. its CD weight
+__global__ void k_conv_w_slot(MeshView m, int S, const int8_t* __restrict__ tyY, const int8_t* __restrict__ tyH,
+                              int b01, double twoByk, const double* __restrict__ bphi, const double* __restrict__ Y,
+                              const double* __restrict__ bY, const double* __restrict__ he,
+                              const double* __restrict__ bhe, double* __restrict__ bwout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = tyY[b];
+  const double ph = bphi[b];
+  double lim = 1.0;
+  if (bc_coupled(t) && m.sprim[b]) {
+    const int c = m.bfc[b], pc = m.partner[b];   // processor slots are rejected at setup (no pc < 0 here)
+    lim = 0.0;
+    bool zero = false;
+    if (b01) {
+      zero = out01(ph, he[c], he[pc]);
+      for (int s = 0; s < S && !zero; ++s) zero = out01(ph, Y[s * C + c], Y[s * C + pc]);
+    }
+    if (!zero) {
+      const double dv[3] = {m.bdv[b], m.bdv[B + b], m.bdv[2 * B + b]};
+      const int cu = ph > 0 ? c : pc;
+      for (int s = 0; s <= S; ++s) {
+        const double* v = s < S ? Y + s * C : he;
+        const double* bv = s < S ? bY + s * B : bhe;
+        double g[3];
+        cell_grad(m, s < S ? tyY : tyH, v, bv, cu, g);
+        const double l = ll_limiter(twoByk, ph, v[c], v[pc], g, dv);
+        lim = s == 0 ? l : fmin(lim, l);
+      }
+    }
+  }
+  bwout[b] = lim * m.bw[b] + (1 - lim) * pos0(ph);
+}
+
+// Gauss linear gradients of ncomp scalar components (component k at vf + k*C, boundary bvf + k*B)
+// -> g [(3k + dir)][C] (fvc::grad of each vf.component(k))
+__global__ void k_grad_cells(MeshView m, const int8_t* __restrict__ ty, int ncomp, const double* __restrict__ vf,
+                             const double* __restrict__ bvf, double* __restrict__ g) {
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
+  if (c >= m.C) return;
+  const long C = m.C, B = m.B;
+  for (int k = 0; k < ncomp; ++k) {
+    double gg[3];
+    cell_grad(m, ty, vf + k * C, bvf + k * B, c, gg);
+    g[(3 * k + 0) * C + c] = gg[0]; g[(3 * k + 1) * C + c] = gg[1]; g[(3 * k + 2) * C + c] = gg[2];
+  }
+}
+
+// single-field limited weights (LimitedScheme: div(phi,K)) from a precomputed gradient g [3][C]
+__global__ void k_lim_w_face(MeshView m, int b01, double twoByk, const double* __restrict__ phi,
+                             const double* __restrict__ v, const double* __restrict__ g, double* __restrict__ wout) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const int o = m.own[f];
+  if (o < 0) return;
+  const int n = m.nei[f];
+  const long C = m.C, Fs = m.F;
+  const double ph = phi[f];
+  double lim = 0.0;
+  if (!(b01 && out01(ph, v[o], v[n]))) {
+    const double dv[3] = {m.md[f], m.md[Fs + f], m.md[2 * Fs + f]};
+    const int cu = ph > 0 ? o : n;
+    const double gu[3] = {g[cu], g[C + cu], g[2 * C + cu]};
+    lim = ll_limiter(twoByk, ph, v[o], v[n], gu, dv);
+  }
+  wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+}
+// boundary slots; bg = the neighbour-side gradient on processor slots ([3][B], halo), cyclic: partner cell
+__global__ void k_lim_w_slot(MeshView m, const int8_t* __restrict__ ty, int b01, double twoByk,
+                             const double* __restrict__ bphi, const double* __restrict__ v, const double* __restrict__ bv,
+                             const double* __restrict__ g, const double* __restrict__ bg, double* __restrict__ bwout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = ty[b];
+  const double ph = bphi[b];
+  double lim = 1.0;
+  if (bc_coupled(t) && m.sprim[b]) {
+    const int c = m.bfc[b], pc = m.partner[b];
+    const double vn = nbrv(m, v, bv, b);
+    lim = 0.0;
+    if (!(b01 && out01(ph, v[c], vn))) {
+      const double dv[3] = {m.bdv[b], m.bdv[B + b], m.bdv[2 * B + b]};
+      double gu[3];
+      for (int q = 0; q < 3; ++q) gu[q] = ph > 0 ? g[q * C + c] : (pc >= 0 ? g[q * C + pc] : bg[q * B + b]);
+      lim = ll_limiter(twoByk, ph, v[c], vn, gu, dv);
+    }
+  }
+  bwout[b] = lim * m.bw[b] + (1 - lim) * pos0(ph);
+}
+
+__global__ void k_upwind_w_face(MeshView m, const double* __restrict__ phi, double* __restrict__ wout) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F || m.own[f] < 0) return;
+  wout[f] = pos0(phi[f]);
+}
+__global__ void k_upwind_w_slot(MeshView m, const double* __restrict__ bphi, double* __restrict__ bwout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  bwout[b] = pos0(bphi[b]);
+}
+
+// cubic::correction of a vector field (3 components), dotted with Sf: the flux cubic adds to the linear
+// face flux (surfaceInterpolationScheme::dotInterpolate + Sf & correction); g = its gradients [9][C]
+__device__ __forceinline__ double cubic_corr(double lam, const double* S, double ms, double dc, const double* vP,
+                                             const double* vN, const double* gP, const double* gN) {
+  const double kSc = lam * (1 - lam * (3 - 2 * lam));
+  const double kVecP = ((1 - lam) * (1 - lam)) * lam;
+  const double kVecN = (lam * lam) * (lam - 1);
+  double cr[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double v = kSc * vP[c] + (-kSc) * vN[c];
+    double gi[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) gi[q] = kVecP * gP[3 * c + q] + kVecN * gN[3 * c + q];
+    cr[c] = v + (((gi[0] * S[0] + gi[1] * S[1] + gi[2] * S[2]) / ms) / dc);
+  }
+  return S[0] * cr[0] + S[1] * cr[1] + S[2] * cr[2];
+}
+__global__ void k_cubic_face(MeshView m, const double* __restrict__ vf, const double* __restrict__ g,
+                             double* __restrict__ cf) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const int o = m.own[f];
+  if (o < 0) return;
+  const int n = m.nei[f];
+  const long C = m.C, Fs = m.F;
+  const double S[3] = {m.Sf[f], m.Sf[Fs + f], m.Sf[2 * Fs + f]};
+  double vP[3], vN[3], gP[9], gN[9];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { vP[c] = vf[c * C + o]; vN[c] = vf[c * C + n]; }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) { gP[q] = g[q * C + o]; gN[q] = g[q * C + n]; }
+  cf[f] = cubic_corr(m.w[f], S, m.magSf[f], m.dc[f], vP, vN, gP, gN);
+}
+__global__ void k_cubic_slot(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
+                             const double* __restrict__ bvf, const double* __restrict__ g, const double* __restrict__ bg,
+                             double* __restrict__ bcf) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = ty[b];
+  if (!bc_coupled(t) || !m.sprim[b]) { bcf[b] = 0.0; return; }
+  const int c0 = m.bfc[b], pc = m.partner[b];
+  const double S[3] = {m.bSf[b], m.bSf[B + b], m.bSf[2 * B + b]};
+  double vP[3], vN[3], gP[9], gN[9];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { vP[c] = vf[c * C + c0]; vN[c] = nbrv(m, vf + c * C, bvf + c * B, b); }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) { gP[q] = g[q * C + c0]; gN[q] = pc >= 0 ? g[q * C + pc] : bg[q * B + b]; }
+  bcf[b] = cubic_corr(m.bw[b], S, m.bmagSf[b], m.bdc[b], vP, vN, gP, gN);
+}
+
 // ------------------------------------------------------------------ old <- new (preTimeStep)
 // every pair in one launch (grid.y = pair) instead of one copy launch per field
 constexpr int MAXCOPY = 12;
@@ -880,7 +1117,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
-    double* __restrict__ bc, MixBC mxY) {
+    double* __restrict__ bc, MixBC mxY, const double* __restrict__ wY, const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -890,7 +1127,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
   for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double ph = phi[f], pu = phiUc[f];
-    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
     const double L1 = -wu * ph, U1 = L1 + ph;
     const double L2 = -wu * pu, U2 = L2 + pu;
     if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
@@ -915,7 +1152,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
     src[s * C + c] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
   }
   each_slot(m, tyY, c, [&](int b, int t) {
-    const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+    const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
 #pragma unroll
     for (int s = 0; s < S; ++s) {
       if (s == inert) continue;
@@ -940,7 +1177,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
-    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
+    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY, const double* __restrict__ wY,
+    const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
@@ -951,7 +1189,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
   int k = 0;
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double ph = phi[f], pu = phiUc[f];
-    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
     const double L1 = -wu * ph, U1 = L1 + ph;
     const double L2 = -wu * pu, U2 = L2 + pu;
     if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
@@ -978,7 +1216,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     sr[s] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
   }
   each_slot(m, tyY, c, [&](int b, int t) {
-    const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+    const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
     const bool cp = bc_coupled(t);
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -1208,7 +1446,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, double* __restrict__ lower,
     double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic,
-    double* __restrict__ bc, MixBC mxY) {
+    double* __restrict__ bc, MixBC mxY, const double* __restrict__ wY, const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -1220,7 +1458,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
     for (int j = 0; j < CH; ++j) { dL[j] = 0.0; rc[j] = s0 + j < S ? rhoD[(s0 + j) * C + c] : 0.0; }
     each_face<WT>(m, c, [&](int f, int o2, bool own) {
       const double ph = phi[f], pu = phiUc[f];
-      const double wu = ph >= 0 ? 1.0 : 0.0;
+      const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
       const double L1 = -wu * ph, U1 = L1 + ph;
       const double L2 = -wu * pu, U2 = L2 + pu;
       if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
@@ -1248,7 +1486,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
       src[s * C + c] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
     }
     each_slot(m, tyY, c, [&](int b, int t) {
-      const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+      const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const int s = s0 + j;
@@ -1272,7 +1510,8 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
-    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY) {
+    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY, const double* __restrict__ wY,
+    const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
@@ -1285,7 +1524,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
     int k = 0;
     each_face<WT>(m, c, [&](int f, int o2, bool own) {
       const double ph = phi[f], pu = phiUc[f];
-      const double wu = ph >= 0 ? 1.0 : 0.0;
+      const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
       const double L1 = -wu * ph, U1 = L1 + ph;
       const double L2 = -wu * pu, U2 = L2 + pu;
       if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
@@ -1314,7 +1553,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
       sr[j] = s < S ? ro * Y[s * C + c] * vol + vol * RR[s * C + c] : 0.0;
     }
     each_slot(m, tyY, c, [&](int b, int t) {
-      const double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+      const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
       const bool cp = bc_coupled(t);
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
@@ -1371,7 +1610,9 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
     const double* __restrict__ alpha, const double* __restrict__ balpha, const double* __restrict__ hD,
     const double* __restrict__ bhD, const double* __restrict__ dpdt, const double* __restrict__ dAD,
     const double* __restrict__ egrad, double* __restrict__ lower, double* __restrict__ upper,
-    double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic, double* __restrict__ bc) {
+    double* __restrict__ diag, double* __restrict__ src, double* __restrict__ ic, double* __restrict__ bc,
+    const double* __restrict__ wY, const double* __restrict__ bwY, const double* __restrict__ wK,
+    const double* __restrict__ bwK, const double* __restrict__ cf, const double* __restrict__ bcf) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -1380,22 +1621,29 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double ph = phi[f], w = m.w[f];
     auto fi = [&](double vc, double vn) { return own ? interp_f(w, vc, vn) : interp_f(w, vn, vc); };
-    const double wu = ph >= 0 ? 1.0 : 0.0;
+    const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
     const double L1 = -wu * ph, U1 = L1 + ph;
     const double UL = m.dc[f] * (fi(ac, alpha[o2]) * m.magSf[f]);
     if (own) { d1 -= L1; lower[f] = L1 - UL; upper[f] = U1 - UL; } else d1 -= U1;
     dL -= UL;
-    const double vk = ph * fi(Kc, K[o2]);
-    const double vh = m.Sf[f] * fi(hc0, hD[o2]) + m.Sf[F + f] * fi(hc1, hD[C + o2]) +
-                      m.Sf[2 * F + f] * fi(hc2, hD[2 * C + o2]);
+    const double wk = wK ? wK[f] : w;   // div(phi,K): limited weights, or linear
+    const double vk = ph * (own ? interp_f(wk, Kc, K[o2]) : interp_f(wk, K[o2], Kc));
+    double vh = m.Sf[f] * fi(hc0, hD[o2]) + m.Sf[F + f] * fi(hc1, hD[C + o2]) +
+                m.Sf[2 * F + f] * fi(hc2, hD[2 * C + o2]);
+    if (cf) vh = vh + cf[f];            // div(hDiffCorrFlux) cubic: + Sf & correction
     if (own) { divK += vk; divh += vh; } else { divK -= vk; divh -= vh; }
   });
-  each_slot(m, tyK, c, [&](int b, int t) { divK += bphi[b] * bface(m, t, K, bK, b, c); });
+  each_slot(m, tyK, c, [&](int b, int t) {
+    const double kb = (wK && bc_coupled(t)) ? interp_b(bwK[b], Kc, nbrv(m, K, bK, b)) : bface(m, t, K, bK, b, c);
+    divK += bphi[b] * kb;
+  });
   each_slot(m, tyH, c, [&](int b, int t) {
     double h[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) h[k] = bface(m, t, hD + k * C, bhD + k * B, b, c);
-    divh += m.bSf[b] * h[0] + m.bSf[B + b] * h[1] + m.bSf[2 * B + b] * h[2];
+    double v = m.bSf[b] * h[0] + m.bSf[B + b] * h[1] + m.bSf[2 * B + b] * h[2];
+    if (bcf && bc_coupled(t)) v = v + bcf[b];
+    divh += v;
   });
   const double vol = m.V[c];
   diag[c] = (m.rdt * rho[c] * vol + d1) - dL;
@@ -1408,7 +1656,7 @@ __global__ void __launch_bounds__(TPB) k_e_assemble(MeshView m, const int8_t* __
   src[c] = sL - sR;
   each_slot(m, tyH, c, [&](int b, int t) {
     const double eg = egrad ? egrad[b] : 0.0;
-    const BCoef qc = bcoef(t, bhe[b], bphi[b] >= 0 ? 1.0 : 0.0, m.bdc[b], eg);
+    const BCoef qc = bcoef(t, bhe[b], bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0), m.bdc[b], eg);
     const BCoef ql = bcoef(t, bhe[b], m.bw[b], m.bdc[b], eg);
     const double gam = bc_coupled(t) ? interp_b(m.bw[b], alpha[c], nbrv(m, alpha, balpha, b)) : balpha[b];
     const double pG = gam * m.bmagSf[b];
@@ -1611,7 +1859,86 @@ bool species_generic(int S) {
     default: throw Error("dfmi: species count " + std::to_string(S) + " not supported");          \
   }
 
+// ---- schemes (dfmi_set_scheme): buffers allocated on first use
+static double* scheme_buf(Ctx& x, const char* name, long n, int ncomp, bool face = false) {
+  auto it = x.fields.find(name);
+  if (it == x.fields.end() || it->second.n != n || it->second.ncomp != ncomp) {
+    Field& f = x.fields[name];
+    f.n = n; f.ncomp = ncomp; f.boundary = std::string(name).rfind("boundary_", 0) == 0; f.face = face;
+    f.buf.alloc((size_t)n * ncomp);
+    f.buf.zero(x.stream);
+    return f.buf.p;
+  }
+  return it->second.buf.p;
+}
+static void scheme_checks(Ctx& x, bool limited) {
+  bool proc = false, coupled = false;
+  for (int p = 0; p < x.P; ++p) { proc |= x.pkind[p] == 2; coupled |= x.pkind[p] != 0; }
+  DFMI_CHECK(!proc || !limited, "limited convection schemes on decomposed meshes (processor patches) are not supported");
+  DFMI_CHECK(!limited || !coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
+  DFMI_CHECK(!limited || x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
+}
+
+// div(phi,Yi_h) weights from this step's Y, he and phi (YEqn.H:6-14: the multivariate scheme is built at the
+// start of YEqn and EEqn reuses it)
+void conv_weights(Ctx& x) {
+  if (x.sch.yh == SCH_UPWIND) return;
+  scheme_checks(x, true);
+  double* w = scheme_buf(x, "conv_w", x.Fs, 1, true);
+  double* bw = scheme_buf(x, "boundary_conv_w", x.B, 1);
+  const int b01 = x.sch.yh == SCH_LL01;
+  const double twoByk = 2.0 / std::max(x.sch.k_yh, 1e-15);
+  MeshView m = x.view();
+  LAUNCH(k_conv_w_face, x.Fs, m, x.S, x.st("Y"), x.st("he"), b01, twoByk, x.f("phi"), x.f("Y"), x.f("boundary_Y"),
+         x.f("he"), x.f("boundary_he"), w);
+  LAUNCH(k_conv_w_slot, x.B, m, x.S, x.st("Y"), x.st("he"), b01, twoByk, x.f("boundary_phi"), x.f("Y"),
+         x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), bw);
+}
+
+// div(phi,K) weights and div(hDiffCorrFlux)'s cubic correction (EEqn.H's fvc::div(phi, K), fvc::div(hDiffCorrFlux))
+static void e_scheme_terms(Ctx& x) {
+  MeshView m = x.view();
+  if (x.sch.K != SCH_LINEAR) {
+    const bool lim = x.sch.K == SCH_LL || x.sch.K == SCH_LL01;
+    scheme_checks(x, false);
+    double* w = scheme_buf(x, "K_w", x.Fs, 1, true);
+    double* bw = scheme_buf(x, "boundary_K_w", x.B, 1);
+    double* g = scheme_buf(x, "gradK", x.C, 3);
+    double* bg = scheme_buf(x, "boundary_gradK", x.B, 3);
+    if (lim) {
+      DFMI_CHECK(x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
+      bool coupled = false;
+      for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
+      DFMI_CHECK(!coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
+      LAUNCH(k_grad_cells, x.C, m, x.st("K"), 1, x.f("K"), x.f("boundary_K"), g);
+      halo_fields(x, {"gradK"});   // the neighbour cell's gradient on processor faces (patchNeighbourField)
+    }
+    // upwind: limiter 0 everywhere (Limited01 with bounds that reject every face)
+    const int b01 = lim ? (x.sch.K == SCH_LL01) : 1;
+    const double twoByk = 2.0 / std::max(x.sch.k_K, 1e-15);
+    if (lim) {
+      LAUNCH(k_lim_w_face, x.Fs, m, b01, twoByk, x.f("phi"), x.f("K"), g, w);
+      LAUNCH(k_lim_w_slot, x.B, m, x.st("K"), b01, twoByk, x.f("boundary_phi"), x.f("K"), x.f("boundary_K"), g, bg, bw);
+    } else {
+      LAUNCH(k_upwind_w_face, x.Fs, m, x.f("phi"), w);
+      LAUNCH(k_upwind_w_slot, x.B, m, x.f("boundary_phi"), bw);
+    }
+  }
+  if (x.sch.hD == SCH_CUBIC) {
+    double* cf = scheme_buf(x, "cubic_flux", x.Fs, 1, true);
+    double* bcf = scheme_buf(x, "boundary_cubic_flux", x.B, 1);
+    double* g = scheme_buf(x, "gradHD", x.C, 9);
+    scheme_buf(x, "boundary_gradHD", x.B, 9);
+    LAUNCH(k_grad_cells, x.C, m, x.st("calculated"), 3, x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
+    halo_fields(x, {"gradHD"});
+    LAUNCH(k_cubic_face, x.Fs, m, x.f("hDiffCorrFlux"), g, cf);
+    LAUNCH(k_cubic_slot, x.B, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g,
+           x.f("boundary_gradHD"), bcf);
+  }
+}
+
 void y_prep(Ctx& x) {
+  conv_weights(x);   // div(phi,Yi_h) weights of this step (before Y changes)
   MeshView m = x.view();
   double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
 // (k_y_prep: the CSR walk measured faster than the gather rows -- 667 vs 848 us on the 2M box; its
@@ -1657,11 +1984,11 @@ void y_assemble(Ctx& x) {
   MeshView m = x.view();
 #define CALL(NS) LAUNCH_SW(k_y_assemble, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),   \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), \
-                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y"))
+                        x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
   DFMI_SWITCH_S(x.S, CALL,
                 LAUNCH_SWG(k_y_assemble_gen, YCH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),
                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), x.f("boundary_phi"),
-                       x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y")))
+                       x.f("phiUc"), x.f("boundary_phiUc"), A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1)))
 #undef CALL
 }
 
@@ -1669,10 +1996,10 @@ void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs
   MeshView m = x.view();
 #define CALL(NS) LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
                         x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
-                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"))
+                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
 #define GEN(CH) LAUNCH_SWG(k_y_assemble_ell_gen, CH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), \
                        x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),     \
-                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"))
+                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
   const char* ech = std::getenv("DFMI_YASM_CH");   // species per chunk, A/B knob (default 8)
   const int ch = ech ? std::atoi(ech) : 8;
   DFMI_SWITCH_S(x.S, CALL, if (ch == 4) GEN(4); else GEN(8))
@@ -1693,11 +2020,13 @@ void e_assemble(Ctx& x) {
   MeshView m = x.view();
   thermo_energy_gradient(x);   // eeqn_calculate_energy_gradient (dfEEqn.cu:148, :266-287)
   k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
+  e_scheme_terms(x);
   const double* eg = x.f("boundary_heGradient");
   LAUNCH_W(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
          x.f("K"), x.f("K_old"), x.f("boundary_K"), x.f("phi"), x.f("boundary_phi"), x.f("alpha"),
          x.f("boundary_alpha"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("dpdt"), x.f("diffAlphaD"),
-         eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p);
+         eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, x.sch_w(0), x.sch_w(1), x.sch_w(2),
+         x.sch_w(3), x.sch_w(4), x.sch_w(5));
 }
 
 void e_post_solve(Ctx& x) {

@@ -48,6 +48,8 @@ SIGNATURES = {
     "dfmi_set_inert_index": [_P, C.c_int],
     "dfmi_set_patch_param": [_P, C.c_char_p, C.c_int, C.c_char_p, C.c_double],
     "dfmi_set_traversal": [_P, _IP],
+    "dfmi_init_boundary_delta": [_P, _DP],
+    "dfmi_set_scheme": [_P, C.c_char_p, C.c_char_p],
     "dfmi_thermo_set_coeffs": [_P, C.c_int, _DP, _DP, _DP, _DP, _DP],
     "dfmi_thermo_load": [_P, C.c_char_p],
     "dfmi_set_field": [_P, C.c_char_p, _DP, C.c_long, C.c_int],
@@ -224,6 +226,16 @@ class Context:
         fc = _i32(bfc) if np.size(bfc) else np.zeros(1, np.int32)
         pc, pe = _i32(ptype_calc), _i32(ptype_extrap)
         self._call("dfmi_init_constant_fields_boundary", self.h, *[_dp(a) for a in arrs], _ip(fc), _ip(pc), _ip(pe))
+
+    def init_boundary_delta(self, bdelta):
+        a = _f64(bdelta)
+        if a.size == 0:
+            a = np.zeros(3)
+        self._call("dfmi_init_boundary_delta", self.h, _dp(a))
+
+    def set_scheme(self, term, scheme):
+        """fvSchemes divSchemes entry for div(phi,Yi_h) / div(phi,K) / div(hDiffCorrFlux) (include/dfmi.h)"""
+        self._call("dfmi_set_scheme", self.h, term.encode(), scheme.encode())
 
     def set_patch_types(self, field, types):
         a = _i32(types); self._call("dfmi_set_patch_types", self.h, field.encode(), _ip(a))

@@ -61,6 +61,10 @@ class Patch:
     peer_rank: int = -1           # processor neighbour rank
     peer_patch: int = -1          # index of the matching patch on peer_rank
     nbr_cells_global: np.ndarray | None = None  # procCols (global ids of cells across the patch)
+    # [n,3] patch delta vectors (fvPatch::delta; coupled: (Cf - C) - (Cf' - C'), cyclicFvPatch::delta /
+    # processorFvPatch::delta), the d the limited schemes' limiter reads across a coupled face
+    # (LimitedScheme::calcLimiter); None: the patch-normal n/deltaCoeffs of an orthogonal patch
+    delta: np.ndarray | None = None
 
     @property
     def size(self) -> int:
@@ -127,6 +131,19 @@ class Mesh:
             return np.zeros((0, 3)), z, z, z, np.zeros(0, np.int32)
         return (np.concatenate(sf), np.concatenate(mag), np.concatenate(dc),
                 np.concatenate(w), np.concatenate(fc).astype(np.int32))
+
+    def boundary_delta(self) -> np.ndarray:
+        """[B,3] patch delta vectors per boundary slot (processor patches: both halves)"""
+        out = []
+        for p in self.patches:
+            reps = 2 if p.kind in ("processor", "processorCyclic") else 1
+            if p.delta is not None:
+                dv = np.asarray(p.delta, dtype=np.float64).reshape(-1, 3)
+            else:
+                nf = p.sf / np.maximum(p.mag_sf, 1e-300)[:, None] if p.size else np.zeros((0, 3))
+                dv = nf / p.delta_coeffs[:, None] if p.size else np.zeros((0, 3))
+            out += [dv] * reps
+        return np.concatenate(out) if out else np.zeros((0, 3))
 
     def proc_rows_cols(self):
         """procRows/procCols for processor interfaces (createGPUSolver.H:205-243)."""
@@ -316,7 +333,9 @@ def hex_box(nx: int, ny: int, nz: int, lengths=(6.283185307179586e-3,) * 3,
             wgt = np.ones(fc.shape[0])
             dc = 1.0 / d_own
         name_to_idx[name] = len(patches)
-        patches.append(Patch(name, kind, fc.astype(np.int32), s, a, wgt, dc))
+        dv = np.zeros((fc.shape[0], 3))
+        dv[:, axis] = side * (d_own + d_nbr) if kind == "cyclic" else side * d_own
+        patches.append(Patch(name, kind, fc.astype(np.int32), s, a, wgt, dc, delta=dv))
     for p in patches:
         if p.kind == "cyclic":
             osi = {"front": "back", "back": "front", "left": "right", "right": "left", "top": "down", "down": "top"}[p.name]
@@ -340,8 +359,10 @@ def hex_box(nx: int, ny: int, nz: int, lengths=(6.283185307179586e-3,) * 3,
         d_nbr = np.abs(d_nbr)
         wgt = d_nbr / (d_own + d_nbr)
         dc = 1.0 / (d_own + d_nbr)
+        dv = np.zeros((fc.shape[0], 3))
+        dv[:, axis] = side * (d_own + d_nbr)
         p = Patch(f"procBoundary{rank}to{peer}_{name}", kind, fc.astype(np.int32), s, a, wgt, dc,
-                  peer_rank=peer)
+                  peer_rank=peer, delta=dv)
         p.nbr_cells_global = gids.astype(np.int32)
         p.side = (axis, side)
         patches.append(p)

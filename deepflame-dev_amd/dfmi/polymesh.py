@@ -195,10 +195,11 @@ def read_polymesh(directory: str) -> Mesh:
             wgt = dni / (di + dni)
             # cyclicFvPatch::delta: the full own-side (Cf - C) minus the partner's (translational cyclic)
             dc = 1.0 / np.linalg.norm(dfull - geo[q][5], axis=1)
-            p = Patch(name, "cyclic", fc.astype(np.int32), sf, mag, wgt, dc)
+            p = Patch(name, "cyclic", fc.astype(np.int32), sf, mag, wgt, dc, delta=dfull - geo[q][5])
             p.neighbour_patch = q
         else:
-            p = Patch(name, "wall", fc.astype(np.int32), sf, mag, np.ones(fc.size), 1.0 / np.linalg.norm(delta, axis=1))
+            p = Patch(name, "wall", fc.astype(np.int32), sf, mag, np.ones(fc.size), 1.0 / np.linalg.norm(delta, axis=1),
+                      delta=delta)
         patches.append(p)
     return Mesh(n_cells=C, owner=owner[:Fi].astype(np.int32), neighbour=neighbour.astype(np.int32), sf=sfi,
                 mag_sf=magsf, weight=w, delta_coeffs=dcoef, volume=vol, cell_centres=cc, mesh_distance=mdist,

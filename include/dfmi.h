@@ -73,6 +73,26 @@ int dfmi_init_constant_fields_boundary(dfmi_ctx* ctx, const double* boundary_sf,
                                        const int* boundary_face_cell, const int* patch_type_calculated,
                                        const int* patch_type_extrapolated);
 
+/* patch delta vectors [B][3] (AoS, processor patches both halves like the other boundary arrays):
+ * fvPatch::delta, on coupled patches (Cf - C) - (Cf' - C') (cyclicFvPatch::delta / processorFvPatch::delta).
+ * The d a limited scheme's limiter reads across a coupled face (OpenFOAM-7 LimitedScheme::calcLimiter,
+ * patch().delta()); required before a time step when a limited scheme is selected and the mesh has
+ * coupled patches. No reference counterpart (its limitedLinear is disabled, dfMatrixOpBase.cu:2540-2600). */
+int dfmi_init_boundary_delta(dfmi_ctx* ctx, const double* boundary_delta);
+
+/* ---- convection / interpolation schemes -------------------------------------------------------------
+ * The reference GPU path hard-wires upwind for Yi and ha and linear for K and hDiffCorrFlux
+ * (dfYEqn.cu:543,587-593; dfEEqn.cu:166-174) whatever system/fvSchemes says; the CPU dfLowMachFoam runs
+ * the case's schemes (YEqn.H:6-14 multivariate convection over every Y_i and he, createFields.H:118-129;
+ * EEqn.H). term (the fvSchemes divSchemes key) / scheme:
+ *   "div(phi,Yi_h)"       "upwind" (default) | "limitedLinear <k>" | "limitedLinear01 <k>"  (Yi and he)
+ *   "div(phi,K)"          "linear" (default) | "upwind" | "limitedLinear <k>" | "limitedLinear01 <k>"
+ *   "div(hDiffCorrFlux)"  "linear" (default) | "cubic"
+ * a leading "Gauss" is accepted, e.g. the reference cases' "Gauss limitedLinear01 1" / "Gauss cubic"
+ * (test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver/system/fvSchemes:32-40). Limited schemes on
+ * decomposed meshes (processor patches) are an error for div(phi,Yi_h). */
+int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme);
+
 /* ---- cell renumbering (the role of OpenFOAM's renumberMesh; run once on the host before
  * dfmi_set_constant_indexes, then permute the mesh and field data with the returned maps) -------- */
 /* new_to_old[num_cells]: method "bricks" (structured blocks: cell_centres holds the integer (i, j, k) of

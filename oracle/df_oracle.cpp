@@ -244,6 +244,190 @@ inline double bface(const M& m, int t, const double* vf, const double* bvf, int 
   return is_coupled(t) ? interp_b(m.bw[b], vf[c], nbr(m, vf, bvf, b)) : bvf[b];
 }
 
+// ---------------------------------------------------------------- convection / interpolation schemes
+// The reference GPU path hard-wires upwind for Yi and ha and linear for K and hDiffCorrFlux
+// (dfYEqn.cu:543,587-593, dfEEqn.cu:166-174); its own cases ask for (system/fvSchemes of
+// examples/dfLowMachFoam/notorch/threeD_reactingTGV/H2/cvodeIntegrator and
+// test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver):
+//   div(phi,Yi_h)       Gauss limitedLinear01 1   (the multivariate scheme YEqn.H:6-14 builds over the
+//                                                  table createFields.H:118-129 = every Y_i plus he; EEqn.H
+//                                                  reuses it for he)
+//   div(phi,K)          Gauss limitedLinear 1     (fvc::div(phi, K), EEqn.H)
+//   div(hDiffCorrFlux)  Gauss cubic               (fvc::div(hDiffCorrFlux), EEqn.H)
+// Restated from OpenFOAM-7 (LimitedScheme::calcLimiter, Limited01.H / LimitedLimiter::limiter,
+// limitedLinearLimiter, NVDTVD::r, multivariateScheme's min over the table's limiters,
+// limitedSurfaceInterpolationScheme::weights, cubic::correction).
+// "schemes" (int[3]): div(phi,Yi_h) 0 upwind | 2 limitedLinear | 3 limitedLinear01; div(phi,K) 0 upwind |
+// 1 linear | 2 limitedLinear | 3 limitedLinear01; div(hDiffCorrFlux) 1 linear | 4 cubic. "scheme_k"
+// (double[2]): the limiters' k for Yi_h and K. Absent: the GPU reference's schemes (0, 1, 1).
+enum Scheme { S_UPWIND = 0, S_LINEAR = 1, S_LL = 2, S_LL01 = 3, S_CUBIC = 4 };
+int scheme(int term) {
+  static const int dflt[3] = {S_UPWIND, S_LINEAR, S_LINEAR};
+  auto it = I.find("schemes");
+  return it == I.end() ? dflt[term] : it->second[term];
+}
+double scheme_k(int term) { return has("scheme_k") ? d("scheme_k")[term] : 1.0; }
+inline double pos0(double x) { return x >= 0 ? 1.0 : 0.0; }
+inline double sgn(double x) { return x >= 0 ? 1.0 : -1.0; }   // OpenFOAM sign()
+
+// limitedLinearLimiter<NVDTVD>::limiter, wrapped in Limited01Limiter (bounded01) when asked
+double ll_limiter(double twoByk, bool bounded01, double faceFlux, double phiP, double phiN, const double* gP,
+                  const double* gN, const double* dv) {
+  if (bounded01 && ((faceFlux > 0 && (phiP < 0 || phiN > 1)) || (faceFlux < 0 && (phiN < 0 || phiP > 1)))) return 0;
+  const double gradf = phiN - phiP;
+  const double* g = faceFlux > 0 ? gP : gN;
+  const double gradcf = dv[0] * g[0] + dv[1] * g[1] + dv[2] * g[2];
+  double r;
+  if (std::fabs(gradcf) >= 1000 * std::fabs(gradf)) r = 2 * 1000 * sgn(gradcf) * sgn(gradf) - 1;
+  else r = 2 * (gradcf / gradf) - 1;
+  return std::max(std::min(twoByk * r, 1.0), 0.0);
+}
+
+// per-field data the limiter reads at a face: values and Gauss-linear gradients [3][C] of the cells,
+// and on coupled slots the neighbour-side value and gradient
+struct LimField { const double *v, *bv, *g; const double* bg; };   // bg: neighbour-side gradient [3][B] (processor)
+
+// weights of a limited scheme over `fields` (one field: LimitedScheme; several: multivariateScheme's min)
+// -> w[F], bw[B]; every limiter evaluated in the same order, min over the table
+void limited_weights(const M& m, const int* type, const std::vector<LimField>& fl, int kind, double k,
+                     const double* phi, const double* bphi, double* w, double* bw) {
+  const double twoByk = 2.0 / std::max(k, 1e-15);
+  const bool b01 = kind == S_LL01;
+  const double* md = d("mesh_distance");
+  #pragma omp parallel for schedule(static)
+  for (int f = 0; f < m.F; ++f) {
+    const int o = m.own[f], n = m.nei[f];
+    const double dv[3] = {md[f], md[(long)m.F + f], md[2L * m.F + f]};
+    double lim = 1.0;
+    for (size_t i = 0; i < fl.size(); ++i) {
+      const LimField& x = fl[i];
+      const double gP[3] = {x.g[o], x.g[(long)m.C + o], x.g[2L * m.C + o]};
+      const double gN[3] = {x.g[n], x.g[(long)m.C + n], x.g[2L * m.C + n]};
+      const double l = ll_limiter(twoByk, b01, phi[f], x.v[o], x.v[n], gP, gN, dv);
+      lim = i == 0 ? l : std::min(lim, l);
+    }
+    w[f] = lim * m.w[f] + (1 - lim) * pos0(phi[f]);
+  }
+  const double* bd = d("boundary_delta");
+  #pragma omp parallel for schedule(static)
+  for (int b = 0; b < m.B; ++b) {
+    const int t = type[m.slot_patch[b]];
+    double lim = 1.0;
+    if (is_coupled(t) && m.primary[b]) {
+      const int c = m.bfc[b], pc = m.partner_cell[b];
+      const double dv[3] = {bd[b], bd[(long)m.B + b], bd[2L * m.B + b]};
+      for (size_t i = 0; i < fl.size(); ++i) {
+        const LimField& x = fl[i];
+        const double gP[3] = {x.g[c], x.g[(long)m.C + c], x.g[2L * m.C + c]};
+        double gN[3];
+        for (int q = 0; q < 3; ++q) gN[q] = pc >= 0 ? x.g[(long)q * m.C + pc] : x.bg[(long)q * m.B + b];
+        const double l = ll_limiter(twoByk, b01, bphi[b], x.v[c], nbr(m, x.v, x.bv, b), gP, gN, dv);
+        lim = i == 0 ? l : std::min(lim, l);
+      }
+    }
+    bw[b] = lim * m.bw[b] + (1 - lim) * pos0(bphi[b]);
+  }
+}
+
+void grad_scalar(const M& m, const int* type, const double* vf, const double* bvf, double* g, double* bg);
+
+// convection weights of div(phi,Yi_h): upwind (pos0(phi)), or the multivariate limited scheme over
+// every Y_i and he (YEqn.H:6-14) -> "conv_w" [F], "boundary_conv_w" [B]; computed once per step at the
+// start of YEqn and reused by EEqn (the same mvConvection object)
+void conv_weights(const M& m) {
+  const int* tY = ia("ptype_Y");
+  const int* the = ia("ptype_he");
+  double *phi = d("phi"), *bphi = d("boundary_phi"), *w = d("conv_w"), *bw = d("boundary_conv_w");
+  const int kind = scheme(0);
+  if (kind == S_UPWIND) {
+    for (int f = 0; f < m.F; ++f) w[f] = pos0(phi[f]);
+    for (int b = 0; b < m.B; ++b) bw[b] = pos0(bphi[b]);
+    return;
+  }
+  if (kind != S_LL && kind != S_LL01) throw std::runtime_error("oracle: div(phi,Yi_h) scheme must be upwind or limitedLinear(01)");
+  for (int b = 0; b < m.B; ++b)
+    if (is_proc(tY[m.slot_patch[b]]) && !has("boundary_conv_grad"))
+      throw std::runtime_error("oracle: limited div(phi,Yi_h) on processor patches needs boundary_conv_grad");
+  const double *Y = d("Y"), *bY = d("boundary_Y"), *he = d("he"), *bhe = d("boundary_he");
+  const double* bgx = has("boundary_conv_grad") ? d("boundary_conv_grad") : nullptr;   // [S+1][3][B]
+  std::vector<double> g(3L * (m.S + 1) * m.C);
+  std::vector<LimField> fl;
+  for (int s = 0; s <= m.S; ++s) {
+    const double* v = s < m.S ? Y + (long)s * m.C : he;
+    const double* bv = s < m.S ? bY + (long)s * m.B : bhe;
+    double* gs = g.data() + 3L * s * m.C;
+    grad_scalar(m, s < m.S ? tY : the, v, bv, gs, nullptr);
+    fl.push_back({v, bv, gs, bgx ? bgx + 3L * s * m.B : nullptr});
+  }
+  limited_weights(m, tY, fl, kind, scheme_k(0), phi, bphi, w, bw);
+}
+
+// interpolation weights of fvc::div(phi, K): linear (the mesh weights), upwind, or limitedLinear(01)
+// from K's own Gauss gradient -> "K_w" [F], "boundary_K_w" [B]
+void k_weights(const M& m, double* w, double* bw) {
+  const int* tK = ia("ptype_K");
+  double *phi = d("phi"), *bphi = d("boundary_phi");
+  const int kind = scheme(1);
+  if (kind == S_LINEAR) { std::copy(m.w, m.w + m.F, w); std::copy(m.bw, m.bw + m.B, bw); return; }
+  if (kind == S_UPWIND) {
+    for (int f = 0; f < m.F; ++f) w[f] = pos0(phi[f]);
+    for (int b = 0; b < m.B; ++b) bw[b] = pos0(bphi[b]);
+    return;
+  }
+  const double *K = d("K"), *bK = d("boundary_K");
+  std::vector<double> g(3L * m.C);
+  grad_scalar(m, tK, K, bK, g.data(), nullptr);
+  const double* bg = has("boundary_gradK") ? d("boundary_gradK") : nullptr;
+  limited_weights(m, tK, {LimField{K, bK, g.data(), bg}}, kind, scheme_k(1), phi, bphi, w, bw);
+}
+
+// cubic::correction of a vector field vf [3][C] (boundary bvf [3][B]) dotted with Sf: the face flux
+// the scheme adds to the linear one (surfaceInterpolationScheme::dotInterpolate: + Sf & correction) ->
+// cf [F], bcf [B] (0 on non-coupled slots, whose correction cubic zeroes)
+void cubic_flux(const M& m, const int* type, const double* vf, const double* bvf, double* cf, double* bcf) {
+  std::vector<double> g(9L * m.C);   // [3 comp][3 dir][C]: fvc::grad(vf.component(c))
+  for (int c = 0; c < 3; ++c) grad_scalar(m, type, vf + (long)c * m.C, bvf + (long)c * m.B, g.data() + 3L * c * m.C, nullptr);
+  const double* bgn = has("boundary_gradHD") ? d("boundary_gradHD") : nullptr;   // processor neighbour gradients [9][B]
+  auto corr = [&](double lam, const double* S, double ms, double dc, const double* vP, const double* vN,
+                  const double* gP, const double* gN) {
+    const double kSc = lam * (1 - lam * (3 - 2 * lam));
+    const double kVecP = ((1 - lam) * (1 - lam)) * lam;
+    const double kVecN = (lam * lam) * (lam - 1);
+    double cr[3];
+    for (int c = 0; c < 3; ++c) {
+      double v = kSc * vP[c] + (-kSc) * vN[c];
+      double gi[3];
+      for (int q = 0; q < 3; ++q) gi[q] = kVecP * gP[3 * c + q] + kVecN * gN[3 * c + q];
+      cr[c] = v + (((gi[0] * S[0] + gi[1] * S[1] + gi[2] * S[2]) / ms) / dc);
+    }
+    return S[0] * cr[0] + S[1] * cr[1] + S[2] * cr[2];
+  };
+  #pragma omp parallel for schedule(static)
+  for (int f = 0; f < m.F; ++f) {
+    const int o = m.own[f], n = m.nei[f];
+    const double S[3] = {m.sf(0, f), m.sf(1, f), m.sf(2, f)};
+    double vP[3], vN[3], gP[9], gN[9];
+    for (int c = 0; c < 3; ++c) { vP[c] = vf[(long)c * m.C + o]; vN[c] = vf[(long)c * m.C + n]; }
+    for (int q = 0; q < 9; ++q) { gP[q] = g[(long)q * m.C + o]; gN[q] = g[(long)q * m.C + n]; }
+    cf[f] = corr(m.w[f], S, m.magSf[f], m.dc[f], vP, vN, gP, gN);
+  }
+  #pragma omp parallel for schedule(static)
+  for (int b = 0; b < m.B; ++b) {
+    bcf[b] = 0.0;
+    const int t = type[m.slot_patch[b]];
+    if (!is_coupled(t) || !m.primary[b]) continue;
+    const int c0 = m.bfc[b], pc = m.partner_cell[b];
+    const double S[3] = {m.bsf(0, b), m.bsf(1, b), m.bsf(2, b)};
+    double vP[3], vN[3], gP[9], gN[9];
+    for (int c = 0; c < 3; ++c) { vP[c] = vf[(long)c * m.C + c0]; vN[c] = nbr(m, vf + (long)c * m.C, bvf + (long)c * m.B, b); }
+    for (int q = 0; q < 9; ++q) {
+      gP[q] = g[(long)q * m.C + c0];
+      gN[q] = pc >= 0 ? g[(long)q * m.C + pc] : bgn[(long)q * m.B + b];
+    }
+    bcf[b] = corr(m.bw[b], S, m.bmagSf[b], m.bdc[b], vP, vN, gP, gN);
+  }
+}
+
 // ---------------------------------------------------------------- rhoEqn (rhoEqn.H:33-45; dfRhoEqn.cu:41-92)
 void rho_eqn(const M& m) {
   const int* trho = ia("ptype_rho");
@@ -657,11 +841,15 @@ void y_assemble(const M& m) {
     bphiUc[b] = m.bsf(0, b) * e[0] + m.bsf(1, b) * e[1] + m.bsf(2, b) * e[2];
   });
   if (has("out_phiUc")) { std::copy(phiUc.begin(), phiUc.end(), d("out_phiUc")); std::copy(bphiUc.begin(), bphiUc.end(), d("out_boundary_phiUc")); }
-  // multivariate Gauss upwind: weights pos0(phi) for both fluxes
+  // multivariate Gauss convection: the same weights (upwind pos0(phi), or the limited scheme's from
+  // conv_weights) for both fluxes -- multivariateGaussConvectionScheme::fvmDiv(phiUc, Yi) interpolates
+  // with the weights the scheme computed from phi
+  const double* cw = has("conv_w") ? d("conv_w") : nullptr;
+  const double* bcw = has("conv_w") ? d("boundary_conv_w") : nullptr;
   std::vector<double> L1(F), U1(F), L2(F), U2(F), UL(F);
   #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) {
-    double w = phi[f] >= 0 ? 1.0 : 0.0;
+    double w = cw ? cw[f] : (phi[f] >= 0 ? 1.0 : 0.0);
     L1[f] = -w * phi[f]; U1[f] = L1[f] + phi[f];
     L2[f] = -w * phiUc[f]; U2[f] = L2[f] + phiUc[f];
   }
@@ -688,7 +876,7 @@ void y_assemble(const M& m) {
       sr[(long)s * C + c] = m.rdt * rho_old[c] * y[c] * m.V[c] + m.V[c] * RR[(long)s * C + c];
     }
     for_slots(m, tY, [&](int b, int t, int c) {
-      double wu = bphi[b] >= 0 ? 1.0 : 0.0;
+      double wu = bcw ? bcw[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
       BCoef qc = bcoef_f(t, by[b], wu, m.bdc[b], mxY, b, B, s);
       BCoef ql = bcoef_f(t, by[b], m.bw[b], m.bdc[b], mxY, b, B, s);
       double gam = is_coupled(t) ? interp_b(m.bw[b], rd[c], nbr(m, rd, brd, b)) : brd[b];
@@ -733,23 +921,39 @@ void e_assemble(const M& m) {
   double *lower = d("out_lower"), *upper = d("out_upper"), *diag = d("out_diag"), *src = d("out_source");
   double *ic = d("out_internal_coeffs"), *bc = d("out_boundary_coeffs");
   const double* egrad = has("boundary_heGradient") ? d("boundary_heGradient") : nullptr;
+  // he convection: mvConvection->fvmDiv(phi, he) (EEqn.H), the weights YEqn's scheme computed
+  const double* cw = has("conv_w") ? d("conv_w") : nullptr;
+  const double* bcw = has("conv_w") ? d("boundary_conv_w") : nullptr;
   std::vector<double> L1(F), U1(F), UL(F);
   #pragma omp parallel for schedule(static)
-  for (int f = 0; f < F; ++f) { double w = phi[f] >= 0 ? 1.0 : 0.0; L1[f] = -w * phi[f]; U1[f] = L1[f] + phi[f]; }
+  for (int f = 0; f < F; ++f) { double w = cw ? cw[f] : (phi[f] >= 0 ? 1.0 : 0.0); L1[f] = -w * phi[f]; U1[f] = L1[f] + phi[f]; }
   auto d1 = neg_sum_diag(m, L1.data(), U1.data());
   #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) UL[f] = m.dc[f] * (interp_f(m.w[f], alpha[m.own[f]], alpha[m.nei[f]]) * m.magSf[f]);
   auto dL = neg_sum_diag(m, UL.data(), UL.data());
-  auto divK = integrate(m, tK, [&](int f) { return phi[f] * interp_f(m.w[f], K[m.own[f]], K[m.nei[f]]); },
-                        [&](int b, int t, int c) { return bphi[b] * bface(m, t, K, bK, b, c); });
+  // fvc::div(phi, K): interpolation weights of div(phi,K) (linear: the mesh weights)
+  std::vector<double> kw(m.w, m.w + F), bkw(m.bw, m.bw + B);
+  if (scheme(1) != S_LINEAR) k_weights(m, kw.data(), bkw.data());
+  auto divK = integrate(m, tK, [&](int f) { return phi[f] * interp_f(kw[f], K[m.own[f]], K[m.nei[f]]); },
+                        [&](int b, int t, int c) {
+                          return bphi[b] * (is_coupled(t) ? interp_b(bkw[b], K[c], nbr(m, K, bK, b)) : bK[b]); });
+  // fvc::div(hDiffCorrFlux): linear, plus cubic's explicit correction (Sf & correction)
+  const bool cubic = scheme(2) == S_CUBIC;
+  std::vector<double> cf, bcf;
+  if (cubic) {
+    cf.assign(F, 0.0); bcf.assign(B, 0.0);
+    cubic_flux(m, ia("ptype_calculated"), hD, bhD, cf.data(), bcf.data());
+  }
   auto divh = integrate(m, the,
       [&](int f) { int o = m.own[f], n = m.nei[f]; double w = m.w[f];
-                   return m.sf(0, f) * interp_f(w, hD[o], hD[n]) + m.sf(1, f) * interp_f(w, hD[C + o], hD[C + n]) +
-                          m.sf(2, f) * interp_f(w, hD[2L * C + o], hD[2L * C + n]); },
+                   double v = m.sf(0, f) * interp_f(w, hD[o], hD[n]) + m.sf(1, f) * interp_f(w, hD[C + o], hD[C + n]) +
+                              m.sf(2, f) * interp_f(w, hD[2L * C + o], hD[2L * C + n]);
+                   return cubic ? v + cf[f] : v; },
       [&](int b, int t, int c) {
         double h[3];
         for (int k = 0; k < 3; ++k) h[k] = bface(m, t, hD + (long)k * C, bhD + (long)k * B, b, c);
-        return m.bsf(0, b) * h[0] + m.bsf(1, b) * h[1] + m.bsf(2, b) * h[2]; });
+        double v = m.bsf(0, b) * h[0] + m.bsf(1, b) * h[1] + m.bsf(2, b) * h[2];
+        return (cubic && is_coupled(t)) ? v + bcf[b] : v; });
   #pragma omp parallel for schedule(static)
   for (int f = 0; f < F; ++f) { lower[f] = L1[f] - UL[f]; upper[f] = U1[f] - UL[f]; }
   #pragma omp parallel for schedule(static)
@@ -767,7 +971,7 @@ void e_assemble(const M& m) {
   std::fill(ic, ic + B, 0.0); std::fill(bc, bc + B, 0.0);
   for_slots(m, the, [&](int b, int t, int c) {
     double eg = egrad ? egrad[b] : 0.0;
-    BCoef qc = bcoef(t, bhe[b], bphi[b] >= 0 ? 1.0 : 0.0, m.bdc[b], eg);
+    BCoef qc = bcoef(t, bhe[b], bcw ? bcw[b] : (bphi[b] >= 0 ? 1.0 : 0.0), m.bdc[b], eg);
     BCoef ql = bcoef(t, bhe[b], m.bw[b], m.bdc[b], eg);
     double gam = is_coupled(t) ? interp_b(m.bw[b], alpha[c], nbr(m, alpha, balpha, b)) : balpha[b];
     double pG = gam * m.bmagSf[b];
@@ -950,6 +1154,13 @@ int orc_y_inert() { ORC_CALL(y_inert(m)) }
 int orc_e_assemble() { ORC_CALL(e_assemble(m)) }
 int orc_thermo_correct(int from_T) { ORC_CALL(thermo_correct(m, from_T != 0)) }
 int orc_energy_gradient() { ORC_CALL(energy_gradient(m)) }
+// convection weights of div(phi,Yi_h) -> "conv_w" / "boundary_conv_w" (start of YEqn, reused by EEqn)
+int orc_conv_weights() { ORC_CALL(conv_weights(m)) }
+// inspection: cubic's explicit flux correction of hDiffCorrFlux -> "out_cubic_flux" [F], "out_boundary_cubic_flux" [B];
+// the div(phi,K) weights -> "out_K_w" [F], "out_boundary_K_w" [B]
+int orc_cubic_flux() { ORC_CALL(cubic_flux(m, ia("ptype_calculated"), d("hDiffCorrFlux"), d("boundary_hDiffCorrFlux"),
+                                           d("out_cubic_flux"), d("out_boundary_cubic_flux"))) }
+int orc_k_weights() { ORC_CALL(k_weights(m, d("out_K_w"), d("out_boundary_K_w"))) }
 int orc_correct_bc(const char* field, const char* bfield, const char* ptype, int ncomp) {
   const Mix mx = mix_for(field);
   ORC_CALL(correct_bc_vec(m, ia(ptype), d(field), d(bfield), ncomp, &mx))

@@ -53,8 +53,12 @@ def _dp(a):
 class Oracle:
     """Holds contiguous copies of every array the restatement reads or writes."""
 
-    def __init__(self, mesh, table, state: dict, ptypes: dict, inert: int, rdt: float):
+    def __init__(self, mesh, table, state: dict, ptypes: dict, inert: int, rdt: float, schemes: dict | None = None):
+        """schemes: {fvSchemes divSchemes key: scheme} for the terms the reference GPU path hard-wires
+        (dfmi.schemes.TERMS; default upwind / linear / linear), e.g. the reference cases'
+        {"div(phi,Yi_h)": "limitedLinear01 1", "div(phi,K)": "limitedLinear 1", "div(hDiffCorrFlux)": "cubic"}"""
         from dfmi.case import patch_kind
+        from dfmi.schemes import scheme_codes
         self.m = mesh
         self.S = table.S
         self.L = lib()
@@ -74,6 +78,14 @@ class Oracle:
         self._d("boundary_sf", bsf.T.copy() if bsf.size else np.zeros(3)); self._d("boundary_mag_sf", bmag)
         self._d("boundary_weight", bw); self._d("boundary_delta_coeffs", bdc)
         self._d("rdelta_t", [rdt])
+        self._d("mesh_distance", np.asarray(m.mesh_distance).T.copy() if m.n_faces else np.zeros(3))
+        bd = m.boundary_delta()
+        self._d("boundary_delta", bd.T.copy() if bd.size else np.zeros(3))
+        codes, ks = scheme_codes(schemes or {})
+        self._i("schemes", codes)
+        self._d("scheme_k", ks)
+        self._d("conv_w", np.zeros(max(m.n_faces, 1)))
+        self._d("boundary_conv_w", np.zeros(max(m.n_boundary_slots, 1)))
         self.rdt = rdt
         self.inert = inert
         self.ptypes = ptypes
@@ -165,6 +177,7 @@ class Oracle:
         self.out("out_gradY", 3 * self.S * m.n_cells)
         for k in ("sumYDiffError", "hDiffCorrFlux"):
             self.set(k, np.zeros((3, m.n_cells)) if self.arr.get(k) is None else self.arr[k])
+        self._run("orc_conv_weights")   # div(phi,Yi_h) weights from this step's Y, he, phi (YEqn.H:6-14)
         self._run("orc_y_prep")
 
     def y_assemble(self):
@@ -178,7 +191,11 @@ class Oracle:
     def y_inert(self):
         self._run("orc_y_inert")
 
-    def e_assemble(self):
+    def e_assemble(self, fresh_weights=False):
+        """fresh_weights: recompute the div(phi,Yi_h) weights first (an EEqn inspected on its own); in
+        the time step EEqn reuses the weights YEqn computed (EEqn.H's mvConvection)"""
+        if fresh_weights:
+            self._run("orc_conv_weights")
         o = self.matrix_outputs(1, 1, 1)
         self._run("orc_e_assemble")
         self.eeqn = {k: v.copy() for k, v in o.items()}

@@ -47,7 +47,7 @@ def _distorted_mesh(nx, ny, nz, lengths, seed=5, amp=0.15):
 
 
 def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0), mech="es80", distorted=False,
-          renumber=None, mixed=False, traversal=False):
+          renumber=None, mixed=False, traversal=False, schemes=None):
     from dfmi.mesh import hex_box, FIXED_VALUE, ZERO_GRADIENT
     from dfmi.lib import Context
     from dfmi import case
@@ -66,7 +66,7 @@ def _case(nx=6, ny=5, nz=4, periodic=True, walls=None, gradings=(1.0, 1.4, 1.0),
         pt.update(walls(m))
     inert = ym["species"].index("N2")
     dt = 1e-6
-    case.setup_context(ctx, m, t, inert, dt, pt)
+    case.setup_context(ctx, m, t, inert, dt, pt, schemes=schemes)
     if traversal:     # gather kernels visit the cells in 8x8x4 bricks (dfmi_set_traversal); data order unchanged
         from dfmi.lib import renumber_cells
         ijk = np.stack(m.local_index, axis=1).astype(np.float64)

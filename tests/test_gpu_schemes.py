@@ -1,0 +1,174 @@
+"""The reference cases' convection schemes on the GPU, bitwise against the oracle (MI355X).
+
+div(phi,Yi_h) limitedLinear01 1 (multivariate over every Y_i and he), div(phi,K) limitedLinear 1 and
+div(hDiffCorrFlux) cubic -- the schemes of the reference's own dfLowMachFoam cases
+(test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver/system/fvSchemes:32-40), which its GPU path replaces
+by upwind / linear (dfYEqn.cu:543,587-593, dfEEqn.cu:166-174). The "ll" variant selects limitedLinear 1
+for Yi_h (no [0, 1] bounds, so every face's limiter comes from the on-the-fly upwind-cell gradients of all
+S + 1 fields) and limitedLinear01 1 for K. YEqn / EEqn matrices at 0 ulp, the production ELL rows at 0 ulp
+against the LDU fold, one outer iteration vs the oracle's exact solves at the parity suite's tolerances.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import rel_err, ulp_diff
+from test_gpu_parity import _case, _cmp_matrix, _ell_width
+
+pytestmark = pytest.mark.gpu
+
+REF = {"div(phi,Yi_h)": "Gauss limitedLinear01 1", "div(phi,K)": "Gauss limitedLinear 1",
+       "div(hDiffCorrFlux)": "Gauss cubic"}
+LL = {"div(phi,Yi_h)": "Gauss limitedLinear 1", "div(phi,K)": "Gauss limitedLinear01 1",
+      "div(hDiffCorrFlux)": "Gauss cubic"}
+
+
+def _walls(mixed=False):
+    from dfmi.mesh import FIXED_VALUE, FIXED_ENERGY, GRADIENT_ENERGY, INLET_OUTLET, WAVE_TRANSMISSIVE
+
+    def walls(m):
+        fv = {}
+        names = ("left",) if mixed else ("left", "right")
+        fixed = [i for i, p in enumerate(m.patches) if p.name in names]
+        for f in ("U", "T", "Y"):
+            t = m.patch_types(0).copy()
+            t[fixed] = FIXED_VALUE
+            fv[f] = t
+        t = m.patch_types(GRADIENT_ENERGY).copy()
+        t[fixed] = FIXED_ENERGY
+        fv["he"] = t
+        if mixed:
+            out = [i for i, p in enumerate(m.patches) if p.name == "right"]
+            fv["U"][out] = INLET_OUTLET
+            fv["Y"][out] = INLET_OUTLET
+            fv["p"] = m.patch_types(0).copy()
+            fv["p"][out] = WAVE_TRANSMISSIVE
+        return fv
+    return walls
+
+
+@pytest.fixture(scope="module", params=["ref-periodic", "ll-periodic", "ll-walls", "ref-distorted", "ll-mixed",
+                                        "ll-periodic-generic", "ll-walls-csr", "ref-gri53"])
+def sc(request):
+    p = request.param
+    if p.endswith("-generic"):
+        os.environ["DFMI_SPECIES_GENERIC"] = "1"
+        request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
+    if p.endswith("-csr"):
+        os.environ["DFMI_FACE_CSR"] = "1"
+        request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
+    schemes = REF if p.startswith("ref") else LL
+    kind = p.split("-")[1]
+    if kind == "periodic":
+        out = _case(mech="burke9", schemes=schemes)
+    elif kind == "gri53":
+        out = _case(mech="gri53", schemes=schemes)
+    else:
+        out = _case(periodic=False, walls=_walls(kind == "mixed"), mech="burke9", distorted=kind == "distorted",
+                    mixed=kind == "mixed", schemes=schemes)
+    return out + (schemes,)
+
+
+def _oracle(m, t, st, pt, inert, dt, schemes):
+    import oracle as O
+    return O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt, schemes=schemes)
+
+
+def test_y_eqn_assembly_bitwise(sc):
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    o = _oracle(m, t, st, pt, inert, dt, schemes)
+    o.y_prep()
+    ref = o.y_assemble()
+    ctx.assemble("Y")
+    res = _cmp_matrix(ctx, "Y", ref, ["lower", "upper", "diag", "source", "internal_coeffs", "boundary_coeffs"],
+                      m.n_boundary_slots)
+    bad = {k: v for k, v in res.items() if v[0] != 0}
+    assert not bad, bad
+    # the limited weights differ from upwind somewhere (the "ll" schemes), the reference's limitedLinear01
+    # over a table holding he is upwind wherever he leaves [0, 1]
+    up = (st["phi"] >= 0).astype(float)
+    frac = float(np.mean(o["conv_w"][:m.n_faces] != up))
+    if schemes is LL:
+        assert frac > 0.05, frac
+
+
+def test_y_ell_rows_bitwise(sc):
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    W = _ell_width(m)
+    n = t.S - 1
+    ctx.assemble("Y_ell")
+    got = {p: ctx.get_solver_rows("Y", p, n * (W if p == "val" else 1) * m.n_cells) for p in ("val", "dS", "rhs")}
+    ctx.assemble("Y_ell_ref")
+    for p in ("val", "dS", "rhs"):
+        assert ulp_diff(got[p], ctx.get_solver_rows("Y", p, got[p].size)) == 0, p
+
+
+def test_e_eqn_assembly_bitwise(sc):
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    o = _oracle(m, t, st, pt, inert, dt, schemes)
+    o.y_prep()
+    o.energy_gradient()
+    o.correct_bc("he", "he", 1)
+    ref = o.e_assemble(fresh_weights=True)
+    ctx.assemble("Y")
+    ctx.assemble("E")
+    res = _cmp_matrix(ctx, "E", ref, ["lower", "upper", "diag", "source", "internal_coeffs", "boundary_coeffs"],
+                      m.n_boundary_slots)
+    bad = {k: v for k, v in res.items() if v[0] != 0}
+    assert not bad, bad
+
+
+def test_schemes_change_the_matrices(sc):
+    """the selected schemes are live: the E source differs from the reference GPU path's upwind/linear one"""
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    o1 = _oracle(m, t, st, pt, inert, dt, schemes)
+    o1.y_prep(); o1.energy_gradient(); o1.correct_bc("he", "he", 1)
+    r1 = o1.e_assemble(fresh_weights=True)["source"].copy()
+    o0 = _oracle(m, t, st, pt, inert, dt, None)
+    o0.y_prep(); o0.energy_gradient(); o0.correct_bc("he", "he", 1)
+    r0 = o0.e_assemble(fresh_weights=True)["source"].copy()
+    assert rel_err(r1, r0) > 1e-12
+
+
+def test_full_outer_iteration(sc):
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    for e in ("U", "Y", "E"):
+        ctx.set_solver(e, 200, 1e-15, 1e-300)
+    ctx.set_solver("p", 2000, 1e-15, 1e-300)
+    o = _oracle(m, t, st, pt, inert, dt, schemes)
+    o.time_step(2)
+    ctx.time_step(2)
+    for n, tl in {"T": 1e-10, "p": 1e-11, "rho": 1e-10, "he": 1e-10}.items():
+        got = ctx.get_field(n, (m.n_cells,))
+        assert rel_err(got, o[n]) < tl, (n, rel_err(got, o[n]))
+    assert rel_err(ctx.get_field("U", (3, m.n_cells)), o["U"]) < 1e-9
+    assert rel_err(ctx.get_field("Y", (t.S, m.n_cells)), o["Y"]) < 1e-9
+    assert rel_err(ctx.get_field("phi", (m.n_faces,)), o["phi"]) < 1e-9
+    for e in ("U", "Y", "E"):
+        ctx.set_solver(e, 20, 1e-5)
+    ctx.set_solver("p", 1000, 1e-5)
+    case.push_state(ctx, st)
+
+
+def test_limited_schemes_rejected_on_processor_patches():
+    """div(phi,Yi_h) limited on a decomposed mesh is an explicit error (not silently upwind)"""
+    from dfmi.lib import Context, DfmiError
+    from dfmi.mesh import hex_box
+    from dfmi import case
+    from test_gpu_parity import _mech
+    ym, t = _mech("burke9")
+    m = hex_box(8, 4, 4, decomp=(2, 1, 1), rank=0)
+    ctx = Context(0)
+    with pytest.raises(DfmiError, match="decomposed"):
+        case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, schemes=REF)
