@@ -371,6 +371,7 @@ def hex_box(nx: int, ny: int, nz: int, lengths=(6.283185307179586e-3,) * 3,
              weight=w, delta_coeffs=dcoef, volume=vol, cell_centres=cc, mesh_distance=mdist, patches=patches,
              global_offset=rank * C, n_total_cells=C * nranks)
     m.local_index = (ii, jj, kk)
+    m.nodes = (xs, ys, zs)
     m.block = (rx, ry, rz)
     m.block_dims = (lnx, lny, lnz)
     return m
