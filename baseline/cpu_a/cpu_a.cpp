@@ -99,8 +99,8 @@ struct Ctx {
   std::map<std::string, std::vector<double>> work;      // oracle inputs/outputs that are not fields
   std::vector<double> rdt_v;
   // schemes (dfmi_set_scheme; the oracle's "schemes" / "scheme_k" layout)
-  std::vector<int> schemes{0, 1, 1};
-  std::vector<double> scheme_k{1.0, 1.0};
+  std::vector<int> schemes{0, 1, 1, 1};
+  std::vector<double> scheme_k{1.0, 1.0, 1.0};
   // thermo
   std::vector<double> W, nasa, visc, cond, bdiff;
   // solvers
@@ -932,8 +932,9 @@ int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
     else if (tok[0] == "limitedLinear") kind = 2;
     else if (tok[0] == "limitedLinear01") kind = 3;
     else if (tok[0] == "cubic") kind = 4;
+    else if (tok[0] == "limitedLinearV") kind = 5;
     CHECK(kind >= 0, t + ": unsupported scheme");
-    if (kind == 2 || kind == 3) {
+    if (kind == 2 || kind == 3 || kind == 5) {
       CHECK(tok.size() == 2, t + ": limitedLinear needs its coefficient k");
       k = std::stod(tok[1]);
       CHECK(k >= 0 && k <= 1, t + ": limitedLinear coefficient must be in [0, 1]");
@@ -941,6 +942,7 @@ int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
     if (t == "div(phi,Yi_h)") { CHECK(kind == 0 || kind == 2 || kind == 3, t + ": upwind or limitedLinear(01)"); x.schemes[0] = kind; x.scheme_k[0] = k; }
     else if (t == "div(phi,K)") { CHECK(kind <= 3, t + ": upwind, linear or limitedLinear(01)"); x.schemes[1] = kind; x.scheme_k[1] = k; }
     else if (t == "div(hDiffCorrFlux)") { CHECK(kind == 1 || kind == 4, t + ": linear or cubic"); x.schemes[2] = kind; }
+    else if (t == "div(phi,U)") { CHECK(kind == 1 || kind == 5, t + ": linear or limitedLinearV"); x.schemes[3] = kind; x.scheme_k[2] = k; }
     else throw Error("dfmi (CPU-A): unknown scheme term '" + t + "'");
   });
 }

@@ -438,8 +438,8 @@ static void parse_scheme(const std::string& term, const std::string& text, int& 
   if (n == "upwind") kind = SCH_UPWIND;
   else if (n == "linear") kind = SCH_LINEAR;
   else if (n == "cubic") kind = SCH_CUBIC;
-  else if (n == "limitedLinear" || n == "limitedLinear01") {
-    kind = n == "limitedLinear" ? SCH_LL : SCH_LL01;
+  else if (n == "limitedLinear" || n == "limitedLinear01" || n == "limitedLinearV") {
+    kind = n == "limitedLinear" ? SCH_LL : n == "limitedLinear01" ? SCH_LL01 : SCH_LLV;
     DFMI_CHECK(tok.size() == 2, term + ": " + n + " needs its coefficient k");
     char* end = nullptr;
     k = std::strtod(tok[1].c_str(), &end);
@@ -468,7 +468,13 @@ int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
     } else if (t == "div(hDiffCorrFlux)") {
       DFMI_CHECK(kind == SCH_LINEAR || kind == SCH_CUBIC, t + ": linear or cubic");
       x.sch.hD = kind;
-    } else throw Error("dfmi: unknown scheme term '" + t + "' (div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux))");
+    } else if (t == "div(phi,U)") {
+      DFMI_CHECK(kind == SCH_LINEAR || kind == SCH_LLV, t + ": linear or limitedLinearV");
+      bool proc = false;
+      for (int p : x.pkind) proc |= p == 2;
+      DFMI_CHECK(kind == SCH_LINEAR || !proc, t + ": limited schemes on decomposed meshes (processor patches) are not supported");
+      x.sch.U = kind; x.sch.k_U = k;
+    } else throw Error("dfmi: unknown scheme term '" + t + "' (div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux), div(phi,U))");
   });
 }
 

@@ -41,10 +41,10 @@ struct MeshView {
 
 // interpolation / convection schemes of the terms the reference GPU path hard-wires (dfmi_set_scheme;
 // dfmi/schemes.py): div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux)
-enum SchemeKind { SCH_UPWIND = 0, SCH_LINEAR = 1, SCH_LL = 2, SCH_LL01 = 3, SCH_CUBIC = 4 };
+enum SchemeKind { SCH_UPWIND = 0, SCH_LINEAR = 1, SCH_LL = 2, SCH_LL01 = 3, SCH_CUBIC = 4, SCH_LLV = 5 };
 struct Schemes {
-  int yh = SCH_UPWIND, K = SCH_LINEAR, hD = SCH_LINEAR;
-  double k_yh = 1.0, k_K = 1.0;
+  int yh = SCH_UPWIND, K = SCH_LINEAR, hD = SCH_LINEAR, U = SCH_LINEAR;
+  double k_yh = 1.0, k_K = 1.0, k_U = 1.0;
 };
 
 struct Field {
@@ -236,11 +236,12 @@ struct Ctx {
   }
   // scheme buffers (fv_kernels.hip scheme launchers): 0/1 div(phi,Yi_h) weights (faces / slots), 2/3
   // div(phi,K) weights, 4/5 cubic flux correction of div(hDiffCorrFlux); nullptr where the term keeps
-  // the reference GPU path's scheme (upwind / linear / linear)
+  // the reference GPU path's scheme (upwind / linear / linear); 6/7 div(phi,U) limitedLinearV weights
   const double* sch_w(int i) {
-    static const char* names[6] = {"conv_w", "boundary_conv_w", "K_w", "boundary_K_w", "cubic_flux",
-                                   "boundary_cubic_flux"};
-    const bool on = i < 2 ? sch.yh != SCH_UPWIND : i < 4 ? sch.K != SCH_LINEAR : sch.hD == SCH_CUBIC;
+    static const char* names[8] = {"conv_w", "boundary_conv_w", "K_w", "boundary_K_w", "cubic_flux",
+                                   "boundary_cubic_flux", "U_w", "boundary_U_w"};
+    const bool on = i < 2 ? sch.yh != SCH_UPWIND : i < 4 ? sch.K != SCH_LINEAR : i < 6 ? sch.hD == SCH_CUBIC
+                                                                                     : sch.U == SCH_LLV;
     if (!on) return nullptr;
     auto it = fields.find(names[i]);
     DFMI_CHECK(it != fields.end(), std::string("scheme buffer '") + names[i] + "' not computed");

@@ -317,6 +317,59 @@ __global__ void k_upwind_w_slot(MeshView m, const double* __restrict__ bphi, dou
   bwout[b] = pos0(bphi[b]);
 }
 
+// limitedLinearV weights of div(phi,U) (limitedLinearLimiter<NVDVTVDV>) from grad(U) g [9][C]
+__device__ __forceinline__ double llv_limiter(double twoByk, const double* vP, const double* vN, const double* g,
+                                              const double* dv) {
+  const double gv[3] = {vN[0] - vP[0], vN[1] - vP[1], vN[2] - vP[2]};
+  const double gradf = gv[0] * gv[0] + gv[1] * gv[1] + gv[2] * gv[2];
+  double dg[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dg[j] = dv[0] * g[j] + dv[1] * g[3 + j] + dv[2] * g[6 + j];
+  const double gradcf = gv[0] * dg[0] + gv[1] * dg[1] + gv[2] * dg[2];
+  double r;
+  if (fabs(gradcf) >= 1000 * fabs(gradf)) r = 2 * 1000 * sgn(gradcf) * sgn(gradf) - 1;
+  else r = 2 * (gradcf / gradf) - 1;
+  return fmax(fmin(twoByk * r, 1.0), 0.0);
+}
+__global__ void k_llv_w_face(MeshView m, double twoByk, const double* __restrict__ phi, const double* __restrict__ U,
+                             const double* __restrict__ g, double* __restrict__ wout) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= m.F) return;
+  const int o = m.own[f];
+  if (o < 0) return;
+  const int n = m.nei[f];
+  const long C = m.C, Fs = m.F;
+  const double ph = phi[f];
+  const double dv[3] = {m.md[f], m.md[Fs + f], m.md[2 * Fs + f]};
+  const double vP[3] = {U[o], U[C + o], U[2 * C + o]}, vN[3] = {U[n], U[C + n], U[2 * C + n]};
+  const int cu = ph > 0 ? o : n;
+  double gu[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) gu[q] = g[q * C + cu];
+  const double lim = llv_limiter(twoByk, vP, vN, gu, dv);
+  wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+}
+__global__ void k_llv_w_slot(MeshView m, const int8_t* __restrict__ ty, double twoByk, const double* __restrict__ bphi,
+                             const double* __restrict__ U, const double* __restrict__ g, double* __restrict__ bwout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  const long C = m.C, B = m.B;
+  const int t = ty[b];
+  const double ph = bphi[b];
+  double lim = 1.0;
+  if (bc_coupled(t) && m.sprim[b]) {   // cyclic (processor patches are rejected at dfmi_set_scheme)
+    const int c = m.bfc[b], pc = m.partner[b];
+    const double dv[3] = {m.bdv[b], m.bdv[B + b], m.bdv[2 * B + b]};
+    const double vP[3] = {U[c], U[C + c], U[2 * C + c]}, vN[3] = {U[pc], U[C + pc], U[2 * C + pc]};
+    const int cu = ph > 0 ? c : pc;
+    double gu[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) gu[q] = g[q * C + cu];
+    lim = llv_limiter(twoByk, vP, vN, gu, dv);
+  }
+  bwout[b] = lim * m.bw[b] + (1 - lim) * pos0(ph);
+}
+
 // cubic::correction of a vector field (3 components), dotted with Sf: the flux cubic adds to the linear
 // face flux (surfaceInterpolationScheme::dotInterpolate + Sf & correction); g = its gradients [9][C]
 __device__ __forceinline__ double cubic_corr(double lam, const double* S, double ms, double dc, const double* vP,
@@ -480,7 +533,8 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
     const double* __restrict__ mu, const double* __restrict__ bmu, const double* __restrict__ p,
     const double* __restrict__ bp, const double* __restrict__ T, const double* __restrict__ bT,
     double* __restrict__ lower, double* __restrict__ upper, double* __restrict__ diag, double* __restrict__ src,
-    double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU, MixBC mxU) {
+    double* __restrict__ srcs, double* __restrict__ ic, double* __restrict__ bc, double* __restrict__ rAU, MixBC mxU,
+    const double* __restrict__ wU, const double* __restrict__ bwU) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
@@ -494,7 +548,7 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
   const double muc = mu[c], pcc = p[c];
   each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double w = m.w[f], ph = phi[f];
-    const double L1 = -w * ph;
+    const double L1 = -(wU ? wU[f] : w) * ph;   // div(phi,U): linear, or limitedLinearV weights
     const double U1 = L1 + ph;
     const double mun = mu[o2];
     const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
@@ -552,9 +606,10 @@ __global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const BCoef q = bcoef_f(t, bU[k * B + b], m.bw[b], m.bdc[b], mxU, b, B, k);
-      icv[k] = bphi[b] * q.vic + (-(pG * q.gic));
+      const BCoef qc = bwU ? bcoef_f(t, bU[k * B + b], bwU[b], m.bdc[b], mxU, b, B, k) : q;   // convection weights
+      icv[k] = bphi[b] * qc.vic + (-(pG * q.gic));
       ic[k * B + b] = icv[k];
-      bc[k * B + b] = -bphi[b] * q.vbc + (-(-pG * q.gbc));
+      bc[k * B + b] = -bphi[b] * qc.vbc + (-(-pG * q.gbc));
     }
     r += (icv[0] + icv[1] + icv[2]) / 3;
   });
@@ -1769,16 +1824,47 @@ void rho_process(Ctx& x, bool write_matrix) {
   halo_fields(x, {"rho"});
 }
 
+// ---- schemes (dfmi_set_scheme): buffers allocated on first use
+static double* scheme_buf(Ctx& x, const char* name, long n, int ncomp, bool face = false) {
+  auto it = x.fields.find(name);
+  if (it == x.fields.end() || it->second.n != n || it->second.ncomp != ncomp) {
+    Field& f = x.fields[name];
+    f.n = n; f.ncomp = ncomp; f.boundary = std::string(name).rfind("boundary_", 0) == 0; f.face = face;
+    f.buf.alloc((size_t)n * ncomp);
+    f.buf.zero(x.stream);
+    return f.buf.p;
+  }
+  return it->second.buf.p;
+}
+static void scheme_checks(Ctx& x, bool limited) {
+  bool proc = false, coupled = false;
+  for (int p = 0; p < x.P; ++p) { proc |= x.pkind[p] == 2; coupled |= x.pkind[p] != 0; }
+  DFMI_CHECK(!proc || !limited, "limited convection schemes on decomposed meshes (processor patches) are not supported");
+  DFMI_CHECK(!limited || !coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
+  DFMI_CHECK(!limited || x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
+}
+
 void u_assemble(Ctx& x) {
   Matrix& A = x.mU;
-  double* gout = x.fields.count("dbg_gradU") ? x.f("dbg_gradU") : nullptr;
+  const bool llv = x.sch.U == SCH_LLV;
+  double* gout = llv ? scheme_buf(x, "gradU", x.C, 9) : x.fields.count("dbg_gradU") ? x.f("dbg_gradU") : nullptr;
   LAUNCH_W(k_u_grad, x.C, x.view(), x.st("U"), x.f("U"), x.f("boundary_U"), x.f("mu"), x.f("boundary_mu"),
          x.f("tauU"), x.f("boundary_tauU"), gout);
   halo_fields(x, {"tauU"});   // fvc_grad_vector_correctBC_processor (dfMatrixOpBase.cu:1366-1389)
+  if (llv) {   // div(phi,U) limitedLinearV weights from this grad(U)
+    scheme_checks(x, true);
+    if (x.fields.count("dbg_gradU"))
+      DFMI_HIP(hipMemcpyAsync(x.f("dbg_gradU"), gout, 9 * sizeof(double) * x.C, hipMemcpyDeviceToDevice, x.stream));
+    double* w = scheme_buf(x, "U_w", x.Fs, 1, true);
+    double* bw = scheme_buf(x, "boundary_U_w", x.B, 1);
+    const double twoByk = 2.0 / std::max(x.sch.k_U, 1e-15);
+    LAUNCH(k_llv_w_face, x.Fs, x.view(), twoByk, x.f("phi"), x.f("U"), gout, w);
+    LAUNCH(k_llv_w_slot, x.B, x.view(), x.st("U"), twoByk, x.f("boundary_phi"), x.f("U"), gout, bw);
+  }
   LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
          x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
          x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
-         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"));
+         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
   k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
   halo_fields(x, {"rAU"});
 }
@@ -1858,26 +1944,6 @@ bool species_generic(int S) {
     case 16: CALL(16); break;                                                                      \
     default: throw Error("dfmi: species count " + std::to_string(S) + " not supported");          \
   }
-
-// ---- schemes (dfmi_set_scheme): buffers allocated on first use
-static double* scheme_buf(Ctx& x, const char* name, long n, int ncomp, bool face = false) {
-  auto it = x.fields.find(name);
-  if (it == x.fields.end() || it->second.n != n || it->second.ncomp != ncomp) {
-    Field& f = x.fields[name];
-    f.n = n; f.ncomp = ncomp; f.boundary = std::string(name).rfind("boundary_", 0) == 0; f.face = face;
-    f.buf.alloc((size_t)n * ncomp);
-    f.buf.zero(x.stream);
-    return f.buf.p;
-  }
-  return it->second.buf.p;
-}
-static void scheme_checks(Ctx& x, bool limited) {
-  bool proc = false, coupled = false;
-  for (int p = 0; p < x.P; ++p) { proc |= x.pkind[p] == 2; coupled |= x.pkind[p] != 0; }
-  DFMI_CHECK(!proc || !limited, "limited convection schemes on decomposed meshes (processor patches) are not supported");
-  DFMI_CHECK(!limited || !coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
-  DFMI_CHECK(!limited || x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
-}
 
 // div(phi,Yi_h) weights from this step's Y, he and phi (YEqn.H:6-14: the multivariate scheme is built at the
 // start of YEqn and EEqn reuses it)

@@ -94,3 +94,76 @@ def run_tgv2d(case_dir: str, golden_dir: str, steps=500, lib_path=None, log=None
                     f"cell max {T.max():.3f}")
     ctx.close()
     return out
+
+
+# ------------------------------------------------------------------ 1D flame speed (test/Tu500K-Phi1)
+# corrtest.cpp:269-270 asserts fs = 6 (token 3 of the fs file, corrtest.cpp:266,276-300): the third
+# "flameSpeed = " line of applications/utilities/flameSpeed/flameSpeed.C:72 over the written times
+# 0, 0.001, 0.002 (system/controlDict writeInterval 1e-3, endTime 2e-3) -> the speed between 1 and 2 ms.
+FLAME_SPEED_EXPECTED = 6.0
+
+
+def flame_position(m, T, bT, types_T):
+    """flameSpeed.C:48-70: x of the cell centre with the largest x-gradient of T (fvc::grad, Gauss
+    linear with T's boundary values; findMax = the first maximum)"""
+    C = m.n_cells
+    own, nei, w = m.owner, m.neighbour, m.weight
+    fv = w * (T[own] - T[nei]) + T[nei]
+    gx = np.zeros(C)
+    np.add.at(gx, own, m.sf[:, 0] * fv)
+    np.add.at(gx, nei, -m.sf[:, 0] * fv)
+    off = 0
+    for p, t in zip(m.patches, types_T):
+        if p.kind != "empty" and p.size:
+            np.add.at(gx, p.face_cells, p.sf[:, 0] * bT[off:off + p.size])
+        off += p.slots
+    gx /= m.volume
+    return float(m.cell_centres[int(np.argmax(gx)), 0])
+
+
+def run_flame1d_speed(golden_dir: str, steps=2000, lib_path=None, log=None, schemes: dict | None = None,
+                      chem_rtol=1e-6, chem_atol=1e-10, solver_tol=1e-8, device: int = 0):
+    """2 ms of the reference's 1D freely-propagating flame (880 cells, Burke2012, its 0/ fields, fvSchemes
+    and waveTransmissive outlet; odeCoeffs relTol 1e-6 / absTol 1e-10) -> flame positions at 0, 1, 2 ms and
+    the flameSpeed utility's value for the last interval"""
+    from .lib import Context
+    from .mech import read_thermo_table, read_yaml_mechanism
+    from .kinetics import parse_mechanism
+    from .schemes import read_fv_schemes
+    from . import case
+    fdir = os.path.join(golden_dir, "flame1d")
+    yml = os.path.join(golden_dir, "Burke2012_s9r23.yaml")
+    ym = read_yaml_mechanism(yml)
+    t = read_thermo_table(os.path.join(golden_dir, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    m = case.flame1d_mesh()
+    if schemes is None:
+        schemes = read_fv_schemes(os.path.join(fdir, "fvSchemes"))
+    ctx = Context(device, lib_path=lib_path)
+    pt = case.flame1d_patch_types(m)
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, pt, schemes=schemes)
+    ctx.chem_set_mechanism(parse_mechanism(yml))
+    ctx.chem_set_options(1, rtol=chem_rtol, atol=chem_atol)
+    for e in ("U", "Y", "E"):
+        ctx.set_solver(e, 200, solver_tol, 1e-300)
+    ctx.set_solver("p", 2000, solver_tol, 1e-300)
+    f, bv = case.flame1d_fields(fdir, ym["species"])
+    case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"], bvals=bv, gammas=case.flame1d_gamma(fdir))
+    U00 = float(f["U"][0, 0])   # flameSpeed.C:60-69 reads U from the 0 directory
+    C, B = m.n_cells, m.n_boundary_slots
+
+    def pos():
+        return flame_position(m, ctx.get_field("T", (C,)), ctx.get_field("boundary_T", (B,)), pt["T"])
+    xs = {0: pos()}
+    for n in range(1, steps + 1):
+        ctx.time_step(2)
+        if n % 1000 == 0:
+            xs[n] = pos()
+            if log:
+                log(f"step {n}: flame at x = {xs[n] * 1e3:.3f} mm")
+    ctx.close()
+    speeds = {}
+    prev = 0.0211   # flameSpeed.C:37 initial flamePosition
+    for n in sorted(xs):
+        speeds[n] = U00 - (xs[n] - prev) / 0.001
+        prev = xs[n]
+    return {"positions": xs, "flameSpeed": speeds, "U_inlet": U00}

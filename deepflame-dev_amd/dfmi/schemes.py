@@ -10,15 +10,15 @@ EEqn.H fvc::div(phi, K) and fvc::div(hDiffCorrFlux)). dfmi_set_scheme (include/d
 """
 from __future__ import annotations
 
-TERMS = ("div(phi,Yi_h)", "div(phi,K)", "div(hDiffCorrFlux)")
-UPWIND, LINEAR, LIMITED_LINEAR, LIMITED_LINEAR01, CUBIC = 0, 1, 2, 3, 4
-DEFAULT = {"div(phi,Yi_h)": "upwind", "div(phi,K)": "linear", "div(hDiffCorrFlux)": "linear"}
+TERMS = ("div(phi,Yi_h)", "div(phi,K)", "div(hDiffCorrFlux)", "div(phi,U)")
+UPWIND, LINEAR, LIMITED_LINEAR, LIMITED_LINEAR01, CUBIC, LIMITED_LINEAR_V = 0, 1, 2, 3, 4, 5
+DEFAULT = {"div(phi,Yi_h)": "upwind", "div(phi,K)": "linear", "div(hDiffCorrFlux)": "linear", "div(phi,U)": "linear"}
 # the reference cases' own divSchemes for these terms
 REFERENCE_CASE = {"div(phi,Yi_h)": "limitedLinear01 1", "div(phi,K)": "limitedLinear 1",
                   "div(hDiffCorrFlux)": "cubic"}
 _ALLOWED = {"div(phi,Yi_h)": (UPWIND, LIMITED_LINEAR, LIMITED_LINEAR01),
             "div(phi,K)": (UPWIND, LINEAR, LIMITED_LINEAR, LIMITED_LINEAR01),
-            "div(hDiffCorrFlux)": (LINEAR, CUBIC)}
+            "div(hDiffCorrFlux)": (LINEAR, CUBIC), "div(phi,U)": (LINEAR, LIMITED_LINEAR_V)}
 
 
 def parse(term: str, scheme: str) -> tuple[int, float]:
@@ -29,12 +29,12 @@ def parse(term: str, scheme: str) -> tuple[int, float]:
     if tok and tok[0] == "Gauss":
         tok = tok[1:]
     names = {"upwind": UPWIND, "linear": LINEAR, "limitedLinear": LIMITED_LINEAR,
-             "limitedLinear01": LIMITED_LINEAR01, "cubic": CUBIC}
+             "limitedLinear01": LIMITED_LINEAR01, "cubic": CUBIC, "limitedLinearV": LIMITED_LINEAR_V}
     if not tok or tok[0] not in names:
         raise ValueError(f"{term}: unsupported scheme {scheme!r}")
     code = names[tok[0]]
     k = 1.0
-    if code in (LIMITED_LINEAR, LIMITED_LINEAR01):
+    if code in (LIMITED_LINEAR, LIMITED_LINEAR01, LIMITED_LINEAR_V):
         if len(tok) != 2:
             raise ValueError(f"{term}: {tok[0]} needs its coefficient k")
         k = float(tok[1])
@@ -48,17 +48,18 @@ def parse(term: str, scheme: str) -> tuple[int, float]:
 
 
 def scheme_codes(schemes: dict) -> tuple[list, list]:
-    """{term: scheme} -> (codes[3], k[2]) in TERMS order, defaults filled in"""
+    """{term: scheme} -> (codes[4], k[3]) in TERMS order (k of Yi_h, K, U), defaults filled in"""
     full = dict(DEFAULT)
     for t, v in schemes.items():
         parse(t, v)
         full[t] = v
-    codes, ks = [], [1.0, 1.0]
+    codes, ks = [], [1.0, 1.0, 1.0]
+    kslot = {0: 0, 1: 1, 3: 2}
     for i, t in enumerate(TERMS):
         c, k = parse(t, full[t])
         codes.append(c)
-        if i < 2:
-            ks[i] = k
+        if i in kslot:
+            ks[kslot[i]] = k
     return codes, ks
 
 

@@ -260,9 +260,11 @@ inline double bface(const M& m, int t, const double* vf, const double* bvf, int 
 // "schemes" (int[3]): div(phi,Yi_h) 0 upwind | 2 limitedLinear | 3 limitedLinear01; div(phi,K) 0 upwind |
 // 1 linear | 2 limitedLinear | 3 limitedLinear01; div(hDiffCorrFlux) 1 linear | 4 cubic. "scheme_k"
 // (double[2]): the limiters' k for Yi_h and K. Absent: the GPU reference's schemes (0, 1, 1).
-enum Scheme { S_UPWIND = 0, S_LINEAR = 1, S_LL = 2, S_LL01 = 3, S_CUBIC = 4 };
+// div(phi,U) (int[3] of "schemes"): 1 linear (the GPU reference's) | 5 limitedLinearV (the 1D flame's,
+// test/Tu500K-Phi1/system/fvSchemes: NVDVTVDV::r on grad(U), scheme_k[2])
+enum Scheme { S_UPWIND = 0, S_LINEAR = 1, S_LL = 2, S_LL01 = 3, S_CUBIC = 4, S_LLV = 5 };
 int scheme(int term) {
-  static const int dflt[3] = {S_UPWIND, S_LINEAR, S_LINEAR};
+  static const int dflt[4] = {S_UPWIND, S_LINEAR, S_LINEAR, S_LINEAR};
   auto it = I.find("schemes");
   return it == I.end() ? dflt[term] : it->second[term];
 }
@@ -330,6 +332,68 @@ void limited_weights(const M& m, const int* type, const std::vector<LimField>& f
 }
 
 void grad_scalar(const M& m, const int* type, const double* vf, const double* bvf, double* g, double* bg);
+
+// limitedLinearV (limitedLinearLimiter<NVDVTVDV>): r from the velocity difference projected on
+// d & grad(U) of the upwind cell; g the upwind cell's gradient tensor (row: direction, column: component)
+double llv_limiter(double twoByk, double faceFlux, const double* vP, const double* vN, const double* g, const double* dv) {
+  const double gv[3] = {vN[0] - vP[0], vN[1] - vP[1], vN[2] - vP[2]};
+  const double gradf = gv[0] * gv[0] + gv[1] * gv[1] + gv[2] * gv[2];
+  double dg[3];
+  for (int j = 0; j < 3; ++j) dg[j] = dv[0] * g[j] + dv[1] * g[3 + j] + dv[2] * g[6 + j];
+  const double gradcf = gv[0] * dg[0] + gv[1] * dg[1] + gv[2] * dg[2];
+  double r;
+  if (std::fabs(gradcf) >= 1000 * std::fabs(gradf)) r = 2 * 1000 * sgn(gradcf) * sgn(gradf) - 1;
+  else r = 2 * (gradcf / gradf) - 1;
+  (void)faceFlux;
+  return std::max(std::min(twoByk * r, 1.0), 0.0);
+}
+
+// fvc::grad of a vector field (Gauss linear) -> g [9][C], g[i*3+j] = d U_j / d x_i
+void grad_vector(const M& m, const int* tU, const double* U, const double* bU, double* g) {
+  const long C = m.C, B = m.B;
+  for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) {
+    auto s = integrate(m, tU,
+        [&](int f) { return m.sf(i, f) * interp_f(m.w[f], U[(long)j * C + m.own[f]], U[(long)j * C + m.nei[f]]); },
+        [&](int b, int t, int c) { return m.bsf(i, b) * bface(m, t, U + (long)j * C, bU + (long)j * B, b, c); });
+    #pragma omp parallel for schedule(static)
+    for (int c = 0; c < C; ++c) g[(long)(i * 3 + j) * C + c] = s[c] / m.V[c];
+  }
+}
+
+// weights of div(phi,U) with limitedLinearV from the cell gradients g [9][C] of U (fvc::grad(U))
+void u_weights(const M& m, const int* tU, const double* U, const double* g, const double* phi, const double* bphi,
+               double* w, double* bw) {
+  const double twoByk = 2.0 / std::max(scheme_k(2), 1e-15);
+  const double* md = d("mesh_distance");
+  const long C = m.C;
+  #pragma omp parallel for schedule(static)
+  for (int f = 0; f < m.F; ++f) {
+    const int o = m.own[f], n = m.nei[f];
+    const double dv[3] = {md[f], md[(long)m.F + f], md[2L * m.F + f]};
+    const double vP[3] = {U[o], U[C + o], U[2 * C + o]}, vN[3] = {U[n], U[C + n], U[2 * C + n]};
+    const int cu = phi[f] > 0 ? o : n;
+    double gu[9];
+    for (int q = 0; q < 9; ++q) gu[q] = g[q * C + cu];
+    const double lim = llv_limiter(twoByk, phi[f], vP, vN, gu, dv);
+    w[f] = lim * m.w[f] + (1 - lim) * pos0(phi[f]);
+  }
+  const double* bd = d("boundary_delta");
+  for (int b = 0; b < m.B; ++b) {
+    const int t = tU[m.slot_patch[b]];
+    double lim = 1.0;
+    if (is_coupled(t) && m.primary[b]) {
+      const int c = m.bfc[b], pc = m.partner_cell[b];
+      if (pc < 0) throw std::runtime_error("oracle: limitedLinearV on processor patches is not supported");
+      const double dv[3] = {bd[b], bd[(long)m.B + b], bd[2L * m.B + b]};
+      const double vP[3] = {U[c], U[C + c], U[2 * C + c]}, vN[3] = {U[pc], U[C + pc], U[2 * C + pc]};
+      const int cu = bphi[b] > 0 ? c : pc;
+      double gu[9];
+      for (int q = 0; q < 9; ++q) gu[q] = g[q * C + cu];
+      lim = llv_limiter(twoByk, bphi[b], vP, vN, gu, dv);
+    }
+    bw[b] = lim * m.bw[b] + (1 - lim) * pos0(bphi[b]);
+  }
+}
 
 // convection weights of div(phi,Yi_h): upwind (pos0(phi)), or the multivariate limited scheme over
 // every Y_i and he (YEqn.H:6-14) -> "conv_w" [F], "boundary_conv_w" [B]; computed once per step at the
@@ -487,10 +551,16 @@ void u_eqn_assemble(const M& m) {
   double *lower = d("out_lower"), *upper = d("out_upper"), *diag = d("out_diag"), *src = d("out_source");
   double *srcs = d("out_source_solve"), *ic = d("out_internal_coeffs"), *bc = d("out_boundary_coeffs");
   double *rAU = d("rAU"), *brAU = d("boundary_rAU");
-  // fvm::div(phi,U), Gauss linear (gaussConvectionScheme::fvmDiv; dfMatrixOpBase.cu:741-781)
+  // fvc::grad(U) (fvc_grad_vector :944-1107): the explicit dev2 term's gradient, and limitedLinearV's
+  std::vector<double> g(9L * C), bg(9L * B, 0.0), T(9L * C), bT(9L * B, 0.0);
+  grad_vector(m, tU, U, bU, g.data());
+  // fvm::div(phi,U) (gaussConvectionScheme::fvmDiv; dfMatrixOpBase.cu:741-781): Gauss linear, or the
+  // limitedLinearV weights
+  std::vector<double> wU(m.w, m.w + F), bwU(m.bw, m.bw + B);
+  if (scheme(3) == S_LLV) u_weights(m, tU, U, g.data(), phi, bphi, wU.data(), bwU.data());
   std::vector<double> L1(F), U1(F), UL(F);
   #pragma omp parallel for schedule(static)
-  for (int f = 0; f < F; ++f) { L1[f] = -m.w[f] * phi[f]; U1[f] = L1[f] + phi[f]; }
+  for (int f = 0; f < F; ++f) { L1[f] = -wU[f] * phi[f]; U1[f] = L1[f] + phi[f]; }
   auto d1 = neg_sum_diag(m, L1.data(), U1.data());
   // fvm::laplacian(mu,U) (gaussLaplacianScheme; :783-810); symmetric
   #pragma omp parallel for schedule(static)
@@ -506,20 +576,13 @@ void u_eqn_assemble(const M& m) {
     double gam = is_coupled(t) ? interp_b(m.bw[b], mu[c], nbr(m, mu, bmu, b)) : bmu[b];
     double pG = gam * m.bmagSf[b];
     for (int k = 0; k < 3; ++k) {
+      BCoef qc = bcoef_f(t, bU[(long)k * B + b], bwU[b], m.bdc[b], mxU, b, B, k);   // convection weights
       BCoef q = bcoef_f(t, bU[(long)k * B + b], m.bw[b], m.bdc[b], mxU, b, B, k);
-      ic[(long)k * B + b] = bphi[b] * q.vic + (-(pG * q.gic));
-      bc[(long)k * B + b] = -bphi[b] * q.vbc + (-(-pG * q.gbc));
+      ic[(long)k * B + b] = bphi[b] * qc.vic + (-(pG * q.gic));
+      bc[(long)k * B + b] = -bphi[b] * qc.vbc + (-(-pG * q.gbc));
     }
   });
-  // -fvc::div(mu*dev2(T(fvc::grad(U)))) (fvc_grad_vector :944-1107, scale_dev2T :623, fvc_div_cell_tensor :1625)
-  std::vector<double> g(9L * C), bg(9L * B, 0.0), T(9L * C), bT(9L * B, 0.0);
-  for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) {
-    auto s = integrate(m, tU,
-        [&](int f) { return m.sf(i, f) * interp_f(m.w[f], U[(long)j * C + m.own[f]], U[(long)j * C + m.nei[f]]); },
-        [&](int b, int t, int c) { return m.bsf(i, b) * bface(m, t, U + (long)j * C, bU + (long)j * B, b, c); });
-    #pragma omp parallel for schedule(static)
-    for (int c = 0; c < C; ++c) g[(long)(i * 3 + j) * C + c] = s[c] / m.V[c];
-  }
+  // -fvc::div(mu*dev2(T(fvc::grad(U)))) (scale_dev2T :623, fvc_div_cell_tensor :1625) on the gradient above
   #pragma omp parallel for schedule(static)
   for (int b = 0; b < B; ++b) {                           // boundary gradient, non-coupled only (:1239-1327)
     int t = tU[m.slot_patch[b]];
@@ -1161,6 +1224,14 @@ int orc_conv_weights() { ORC_CALL(conv_weights(m)) }
 int orc_cubic_flux() { ORC_CALL(cubic_flux(m, ia("ptype_calculated"), d("hDiffCorrFlux"), d("boundary_hDiffCorrFlux"),
                                            d("out_cubic_flux"), d("out_boundary_cubic_flux"))) }
 int orc_k_weights() { ORC_CALL(k_weights(m, d("out_K_w"), d("out_boundary_K_w"))) }
+// inspection: the div(phi,U) limitedLinearV weights -> "out_U_w" [F], "out_boundary_U_w" [B]
+int orc_u_weights() {
+  ORC_CALL({
+    std::vector<double> g(9L * m.C);
+    grad_vector(m, ia("ptype_U"), d("U"), d("boundary_U"), g.data());
+    u_weights(m, ia("ptype_U"), d("U"), g.data(), d("phi"), d("boundary_phi"), d("out_U_w"), d("out_boundary_U_w"));
+  })
+}
 int orc_correct_bc(const char* field, const char* bfield, const char* ptype, int ncomp) {
   const Mix mx = mix_for(field);
   ORC_CALL(correct_bc_vec(m, ia(ptype), d(field), d(bfield), ncomp, &mx))

@@ -1,4 +1,5 @@
 #!/usr/bin/env python3
+# (tests/golden/flame1d_speed_cpu_a.json is written by dfmi.regression.run_flame1d_speed on CPU-A, the same way)
 """Run the reference's 2D reacting-TGV regression (test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver,
 tests/golden/tgv2d) through include/dfmi.h and print / save the values test/corrtest.cpp:51-56 asserts.
 

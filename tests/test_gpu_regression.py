@@ -23,3 +23,16 @@ def test_tgv2d_gpu_matches_reference_regression():
         assert dev < 5e-3, (step, r["value"], r["expected"], dev)
         cpu = ref[str(step)]["value"]
         assert abs(r["value"] - cpu) < 1e-5 * cpu, (step, r["value"], cpu)
+
+
+def test_flame_speed_gpu_matches_reference_regression():
+    """test/Tu500K-Phi1 for 2 ms (2000 steps) on the GPU: the flameSpeed utility's value for 1 -> 2 ms
+    against corrtest.cpp:269-270's 6 m/s within 0.2 m/s (see tests/test_flame_speed_regression.py), and the
+    flame positions equal to CPU-A's (the same cells)."""
+    from dfmi import regression as R
+    out = R.run_flame1d_speed(GOLDEN, log=print)
+    fs = out["flameSpeed"][2000]
+    assert abs(fs - R.FLAME_SPEED_EXPECTED) <= 0.2, out
+    ref = json.load(open(os.path.join(GOLDEN, "flame1d_speed_cpu_a.json")))
+    for k, x in out["positions"].items():
+        assert abs(x - ref["positions"][str(k)]) < 1e-9, (k, x, ref["positions"])

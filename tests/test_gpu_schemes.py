@@ -5,7 +5,8 @@ div(hDiffCorrFlux) cubic -- the schemes of the reference's own dfLowMachFoam cas
 (test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver/system/fvSchemes:32-40), which its GPU path replaces
 by upwind / linear (dfYEqn.cu:543,587-593, dfEEqn.cu:166-174). The "ll" variant selects limitedLinear 1
 for Yi_h (no [0, 1] bounds, so every face's limiter comes from the on-the-fly upwind-cell gradients of all
-S + 1 fields) and limitedLinear01 1 for K. YEqn / EEqn matrices at 0 ulp, the production ELL rows at 0 ulp
+S + 1 fields), limitedLinear01 1 for K and limitedLinearV 1 for U (the 1D flame's div(phi,U),
+test/Tu500K-Phi1/system/fvSchemes). YEqn / EEqn matrices at 0 ulp, the production ELL rows at 0 ulp
 against the LDU fold, one outer iteration vs the oracle's exact solves at the parity suite's tolerances.
 """
 import os
@@ -21,7 +22,7 @@ pytestmark = pytest.mark.gpu
 REF = {"div(phi,Yi_h)": "Gauss limitedLinear01 1", "div(phi,K)": "Gauss limitedLinear 1",
        "div(hDiffCorrFlux)": "Gauss cubic"}
 LL = {"div(phi,Yi_h)": "Gauss limitedLinear 1", "div(phi,K)": "Gauss limitedLinear01 1",
-      "div(hDiffCorrFlux)": "Gauss cubic"}
+      "div(hDiffCorrFlux)": "Gauss cubic", "div(phi,U)": "Gauss limitedLinearV 1"}
 
 
 def _walls(mixed=False):
@@ -73,6 +74,20 @@ def sc(request):
 def _oracle(m, t, st, pt, inert, dt, schemes):
     import oracle as O
     return O.Oracle(m, t, {k: v.copy() for k, v in st.items()}, pt, inert, 1.0 / dt, schemes=schemes)
+
+
+def test_u_eqn_assembly_bitwise(sc):
+    ctx, m, t, st, pt, inert, dt, schemes = sc
+    from dfmi import case
+    case.push_state(ctx, st)
+    o = _oracle(m, t, st, pt, inert, dt, schemes)
+    ref = o.u_assemble()
+    ctx.assemble("U")
+    res = _cmp_matrix(ctx, "U", ref, ["lower", "upper", "diag", "source", "source_solve", "internal_coeffs",
+                                      "boundary_coeffs"], m.n_boundary_slots)
+    bad = {k: v for k, v in res.items() if v[0] != 0}
+    assert not bad, bad
+    assert ulp_diff(ctx.get_field("rAU", (m.n_cells,)), o["rAU"]) == 0
 
 
 def test_y_eqn_assembly_bitwise(sc):

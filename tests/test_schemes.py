@@ -22,16 +22,17 @@ def test_scheme_parser():
     assert parse("div(phi,Yi_h)", "Gauss limitedLinear01 1") == (LIMITED_LINEAR01, 1.0)
     assert parse("div(phi,K)", "limitedLinear 0.5") == (LIMITED_LINEAR, 0.5)
     assert parse("div(hDiffCorrFlux)", "Gauss cubic") == (CUBIC, 1.0)
-    for bad in [("div(phi,U)", "linear"), ("div(phi,Yi_h)", "cubic"), ("div(phi,K)", "limitedLinear"),
+    for bad in [("div(phi,h)", "linear"), ("div(phi,U)", "cubic"), ("div(phi,Yi_h)", "cubic"), ("div(phi,K)", "limitedLinear"),
                 ("div(phi,K)", "limitedLinear 2"), ("div(hDiffCorrFlux)", "upwind")]:
         with pytest.raises(ValueError):
             parse(*bad)
-    assert scheme_codes({}) == ([0, 1, 1], [1.0, 1.0])
+    assert scheme_codes({}) == ([0, 1, 1, 1], [1.0, 1.0, 1.0])
+    assert scheme_codes({"div(phi,U)": "Gauss limitedLinearV 1"}) == ([0, 1, 1, 5], [1.0, 1.0, 1.0])
     import os
     from conftest import GOLDEN
     got = read_fv_schemes(os.path.join(GOLDEN, "tgv2d", "fvSchemes"))
     assert got == {"div(phi,Yi_h)": "Gauss limitedLinear01 1", "div(phi,K)": "Gauss limitedLinear 1",
-                   "div(hDiffCorrFlux)": "Gauss cubic"}
+                   "div(hDiffCorrFlux)": "Gauss cubic", "div(phi,U)": "Gauss linear"}
 
 
 def _box(periodic):
@@ -222,3 +223,35 @@ def test_cubic_interpolation_exact_for_quadratic(es80):
     assert sel.sum() > 20
     assert np.abs(tot[sel] - exact[sel]).max() < 1e-14 * np.abs(exact[sel]).max() * 10
     assert np.abs(lin[sel] - exact[sel]).max() > 1e-4 * np.abs(exact[sel]).max()   # linear alone is not exact
+
+
+@pytest.mark.parametrize("periodic", [True, False])
+def test_limited_linear_v_weights_match_openfoam_formulas(es80, periodic):
+    """div(phi,U) Gauss limitedLinearV 1 (the 1D flame's, test/Tu500K-Phi1/system/fvSchemes): NVDVTVDV::r
+    from (U_N - U_P) . (d & grad(U)_upwind) over |U_N - U_P|^2"""
+    t, _ = es80
+    m = _box(periodic)
+    rng = np.random.default_rng(11)
+    x = m.cell_centres / m.cell_centres.max(axis=0)
+    U = np.stack([np.sin(2 * np.pi * x[:, 0] + a) * np.cos(2 * np.pi * x[:, 1]) for a in (0.3, 1.1, 2.0)])
+    from dfmi.case import boundary_values
+    st = {"U": U, "boundary_U": boundary_values(m, U), "phi": rng.standard_normal(m.n_faces),
+          "boundary_phi": rng.standard_normal(m.n_boundary_slots), "out_U_w": np.zeros(m.n_faces),
+          "out_boundary_U_w": np.zeros(m.n_boundary_slots)}
+    o = _oracle(m, t, st, {"div(phi,U)": "limitedLinearV 1"})
+    o._run("orc_u_weights")
+    # numpy: grad(U) per component, r = 2 (dU . (d & G)) / |dU|^2 - 1
+    G = np.stack([_np_grad(m, U[j], st["boundary_U"][j]) for j in range(3)], axis=1)   # [i dir][j comp][C]
+    own, nei = m.owner, m.neighbour
+    up = np.where(st["phi"] > 0, own, nei)
+    d = m.mesh_distance.T
+    dU = U[:, nei] - U[:, own]
+    gradf = (dU * dU).sum(axis=0)
+    dG = np.einsum("if,ijf->jf", d, G[:, :, up])
+    gradcf = (dU * dG).sum(axis=0)
+    sg = lambda v: np.where(v >= 0, 1.0, -1.0)
+    r = np.where(np.abs(gradcf) >= 1000 * np.abs(gradf), 2 * 1000 * sg(gradcf) * sg(gradf) - 1, 2 * gradcf / gradf - 1)
+    lim = np.clip(2 * r, 0, 1)
+    w = lim * m.weight + (1 - lim) * (st["phi"] >= 0)
+    assert rel_err(o["out_U_w"], w) < 1e-12
+    assert 0 < np.mean(np.abs(o["out_U_w"] - m.weight) > 1e-12) < 1
