@@ -458,9 +458,6 @@ int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
     parse_scheme(t, s, kind, k);
     if (t == "div(phi,Yi_h)") {
       DFMI_CHECK(kind == SCH_UPWIND || kind == SCH_LL || kind == SCH_LL01, t + ": upwind, limitedLinear or limitedLinear01");
-      bool proc = false;
-      for (int p : x.pkind) proc |= p == 2;
-      DFMI_CHECK(kind == SCH_UPWIND || !proc, t + ": limited schemes on decomposed meshes (processor patches) are not supported");
       x.sch.yh = kind; x.sch.k_yh = k;
     } else if (t == "div(phi,K)") {
       DFMI_CHECK(kind != SCH_CUBIC, t + ": upwind, linear, limitedLinear or limitedLinear01");

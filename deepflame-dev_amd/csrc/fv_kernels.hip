@@ -215,10 +215,12 @@ __global__ void k_conv_w_face(MeshView m, int S, const int8_t* __restrict__ tyY,
 
 // the same on the boundary slots: coupled (cyclic) slots with the partner cell as N and the patch delta;
 // every other slot takes limiter 1 (calcLimiter's non-coupled branch), i.e. its CD weight
+// bgx: on decomposed meshes the neighbour-side gradients of every field on the processor slots
+// ([3(S+1)][B], exchanged: patchNeighbourField of fvc::grad), nullptr otherwise
 __global__ void k_conv_w_slot(MeshView m, int S, const int8_t* __restrict__ tyY, const int8_t* __restrict__ tyH,
                               int b01, double twoByk, const double* __restrict__ bphi, const double* __restrict__ Y,
                               const double* __restrict__ bY, const double* __restrict__ he,
-                              const double* __restrict__ bhe, double* __restrict__ bwout) {
+                              const double* __restrict__ bhe, const double* __restrict__ bgx, double* __restrict__ bwout) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= m.B) return;
   const long C = m.C, B = m.B;
@@ -226,27 +228,46 @@ __global__ void k_conv_w_slot(MeshView m, int S, const int8_t* __restrict__ tyY,
   const double ph = bphi[b];
   double lim = 1.0;
   if (bc_coupled(t) && m.sprim[b]) {
-    const int c = m.bfc[b], pc = m.partner[b];   // processor slots are rejected at setup (no pc < 0 here)
+    const int c = m.bfc[b], pc = m.partner[b];   // pc < 0: processor slot, neighbour values in the slot
+    auto vn = [&](const double* v, const double* bv) { return pc >= 0 ? v[pc] : bv[b]; };
     lim = 0.0;
     bool zero = false;
     if (b01) {
-      zero = out01(ph, he[c], he[pc]);
-      for (int s = 0; s < S && !zero; ++s) zero = out01(ph, Y[s * C + c], Y[s * C + pc]);
+      zero = out01(ph, he[c], vn(he, bhe));
+      for (int s = 0; s < S && !zero; ++s) zero = out01(ph, Y[s * C + c], vn(Y + s * C, bY + s * B));
     }
     if (!zero) {
       const double dv[3] = {m.bdv[b], m.bdv[B + b], m.bdv[2 * B + b]};
-      const int cu = ph > 0 ? c : pc;
+      const bool own_up = ph > 0;
       for (int s = 0; s <= S; ++s) {
         const double* v = s < S ? Y + s * C : he;
         const double* bv = s < S ? bY + s * B : bhe;
         double g[3];
-        cell_grad(m, s < S ? tyY : tyH, v, bv, cu, g);
-        const double l = ll_limiter(twoByk, ph, v[c], v[pc], g, dv);
+        if (own_up || pc >= 0) cell_grad(m, s < S ? tyY : tyH, v, bv, own_up ? c : pc, g);
+        else { g[0] = bgx[(3 * s) * B + b]; g[1] = bgx[(3 * s + 1) * B + b]; g[2] = bgx[(3 * s + 2) * B + b]; }
+        const double l = ll_limiter(twoByk, ph, v[c], vn(v, bv), g, dv);
         lim = s == 0 ? l : fmin(lim, l);
       }
     }
   }
   bwout[b] = lim * m.bw[b] + (1 - lim) * pos0(ph);
+}
+
+// gradients of every field of the table at the cells of the processor slots -> g [3(S+1)][C] (only those
+// cells written; the halo then carries them to the neighbour ranks' processor slots)
+__global__ void k_conv_proc_grad(MeshView m, int S, const int8_t* __restrict__ tyY, const int8_t* __restrict__ tyH,
+                                 const double* __restrict__ Y, const double* __restrict__ bY,
+                                 const double* __restrict__ he, const double* __restrict__ bhe, double* __restrict__ g) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  if (!bc_proc(tyY[b]) || !m.sprim[b]) return;
+  const long C = m.C, B = m.B;
+  const int c = m.bfc[b];
+  for (int s = 0; s <= S; ++s) {
+    double gg[3];
+    cell_grad(m, s < S ? tyY : tyH, s < S ? Y + s * C : he, s < S ? bY + s * B : bhe, c, gg);
+    g[(3 * s) * C + c] = gg[0]; g[(3 * s + 1) * C + c] = gg[1]; g[(3 * s + 2) * C + c] = gg[2];
+  }
 }
 
 // Gauss linear gradients of ncomp scalar components (component k at vf + k*C, boundary bvf + k*B)
@@ -1837,9 +1858,8 @@ static double* scheme_buf(Ctx& x, const char* name, long n, int ncomp, bool face
   return it->second.buf.p;
 }
 static void scheme_checks(Ctx& x, bool limited) {
-  bool proc = false, coupled = false;
-  for (int p = 0; p < x.P; ++p) { proc |= x.pkind[p] == 2; coupled |= x.pkind[p] != 0; }
-  DFMI_CHECK(!proc || !limited, "limited convection schemes on decomposed meshes (processor patches) are not supported");
+  bool coupled = false;
+  for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
   DFMI_CHECK(!limited || !coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
   DFMI_CHECK(!limited || x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
 }
@@ -1957,8 +1977,16 @@ void conv_weights(Ctx& x) {
   MeshView m = x.view();
   LAUNCH(k_conv_w_face, x.Fs, m, x.S, x.st("Y"), x.st("he"), b01, twoByk, x.f("phi"), x.f("Y"), x.f("boundary_Y"),
          x.f("he"), x.f("boundary_he"), w);
+  const double* bgx = nullptr;
+  if (halo_active(x)) {   // processor faces: the neighbour cells' gradients (LimitedScheme::calcLimiter's pGradcN)
+    double* g = scheme_buf(x, "conv_grad", x.C, 3 * (x.S + 1));
+    bgx = scheme_buf(x, "boundary_conv_grad", x.B, 3 * (x.S + 1));
+    LAUNCH(k_conv_proc_grad, x.B, m, x.S, x.st("Y"), x.st("he"), x.f("Y"), x.f("boundary_Y"), x.f("he"),
+           x.f("boundary_he"), g);
+    halo_fields(x, {"conv_grad"});
+  }
   LAUNCH(k_conv_w_slot, x.B, m, x.S, x.st("Y"), x.st("he"), b01, twoByk, x.f("boundary_phi"), x.f("Y"),
-         x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), bw);
+         x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), bgx, bw);
 }
 
 // div(phi,K) weights and div(hDiffCorrFlux)'s cubic correction (EEqn.H's fvc::div(phi, K), fvc::div(hDiffCorrFlux))

@@ -176,8 +176,9 @@ def test_full_outer_iteration(sc):
     case.push_state(ctx, st)
 
 
-def test_limited_schemes_rejected_on_processor_patches():
-    """div(phi,Yi_h) limited on a decomposed mesh is an explicit error (not silently upwind)"""
+def test_limited_v_rejected_on_processor_patches():
+    """div(phi,U) limitedLinearV on a decomposed mesh is an explicit error (not silently linear); the
+    other terms run decomposed (test_gpu_multirank.py::test_decomposed_case_schemes_match_single_domain)"""
     from dfmi.lib import Context, DfmiError
     from dfmi.mesh import hex_box
     from dfmi import case
@@ -186,4 +187,4 @@ def test_limited_schemes_rejected_on_processor_patches():
     m = hex_box(8, 4, 4, decomp=(2, 1, 1), rank=0)
     ctx = Context(0)
     with pytest.raises(DfmiError, match="decomposed"):
-        case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, schemes=REF)
+        case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, schemes={"div(phi,U)": "limitedLinearV 1"})
