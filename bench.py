@@ -120,7 +120,39 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2, help="timed outer iterations of the CPU-A baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-flame", action="store_true", help="skip the BASELINE config 2 (1D flame) side line")
+    ap.add_argument("--schemes", default="case", choices=["case", "gpu"],
+                    help="convection schemes of div(phi,Yi_h) / div(phi,K) / div(hDiffCorrFlux): the case's own "
+                         "(examples/dfLowMachFoam/notorch/threeD_reactingTGV/H2/cvodeIntegrator/system/fvSchemes: "
+                         "limitedLinear01 / limitedLinear / cubic, what the reference CPU solver runs) or the "
+                         "reference GPU path's hard-wired upwind / linear / linear; the other set is timed beside")
+    ap.add_argument("--alt-steps", type=int, default=5, help="timed steps with the other scheme set (0: skip)")
     return ap.parse_args()
+
+
+def case_schemes():
+    """divSchemes of the headline case (committed as tests/golden/tgv64/fvSchemes)"""
+    from dfmi.schemes import read_fv_schemes
+    return read_fv_schemes(os.path.join(ROOT, "tests", "golden", "tgv64", "fvSchemes"))
+
+
+def gpu_schemes():
+    from dfmi.schemes import DEFAULT
+    return dict(DEFAULT)
+
+
+def cgroup_cpus():
+    """CPUs the cgroup quota grants this process (cgroup v2 cpu.max, v1 cfs quota), None if unlimited"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
 
 
 def host_cpu():
@@ -153,7 +185,7 @@ def cpu_baseline(args, table, ym, inert):
     L = 2 * 3.141592653589793e-3
     m = hex_box(n, n, n, lengths=(L, L, L))
     ctx = Context(0, lib_path=path)
-    case.setup_context(ctx, m, table, inert, args.dt)
+    case.setup_context(ctx, m, table, inert, args.dt, schemes=case_schemes() if args.schemes == "case" else gpu_schemes())
     if args.chem == "ode":
         ctx.chem_set_mechanism(parse_mechanism(os.path.join(ROOT, "tests", "golden", MECHS[args.mech][0])))
         ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
@@ -177,12 +209,19 @@ def cpu_baseline(args, table, ym, inert):
         configs["config1_zeroD"] = {"chem_integrations_per_s": zd["chem_integrations_per_s"], "steps": 200,
                                     "T_end": zd["T_end"], "T_end_oracle": zd["T_end_oracle"]}
     usable, machine, model = host_cpu()
+    quota = cgroup_cpus()
     chem = "ROS3 chemistry (rtol 1e-6, atol 1e-10)" if args.chem == "ode" else "no chemistry"
-    return {"value": m.n_cells * args.cpu_steps / el, "unit": "cell-updates/s", "cores": threads, "kind": "CPU-A",
-            "sample": f"baseline/cpu_a (OpenMP C++, fp64, same ABI and step) on {n}^3 = {m.n_cells} cells, "
-                      f"{table.S} species, {chem}, {args.cpu_steps} timed outer iterations in {el:.1f} s after "
-                      f"1 untimed; last-step solver iterations {iters}",
-            "host": {"omp_threads": threads, "affinity_cpus": usable, "nproc": machine, "model": model},
+    value = m.n_cells * args.cpu_steps / el
+    return {"value": value, "unit": "cell-updates/s", "cores": threads, "kind": "CPU-A",
+            "value_per_core": value / threads,
+            "sample": f"baseline/cpu_a (OpenMP C++, fp64, same ABI and step, {args.schemes} schemes) on {n}^3 = "
+                      f"{m.n_cells} cells, {table.S} species, {chem}, {args.cpu_steps} timed outer iterations in "
+                      f"{el:.1f} s after 1 untimed; last-step solver iterations {iters}",
+            "host": {"omp_threads": threads, "affinity_cpus": usable, "nproc": machine, "model": model,
+                     "cgroup_cpu_quota": quota, "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+                     "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES"),
+                     "note": "threads = OMP_NUM_THREADS, the box's CPU share (gpurun sets it to 16 on the 1-GPU box "
+                             "and forbids raising it); cgroup_cpu_quota is the kernel's quota for this process"},
             "configs": configs}
 
 
@@ -241,9 +280,13 @@ def flame1d_line(steps=100, warmup=10, lib_path=None):
     golden = os.path.join(ROOT, "tests", "golden")
     ym = read_yaml_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml"))
     t = read_thermo_table(os.path.join(golden, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    from dfmi.schemes import read_fv_schemes
     m = case.flame1d_mesh()
     ctx = Context(int(os.environ.get("LOCAL_RANK", "0")), lib_path=lib_path)
-    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, case.flame1d_patch_types(m))
+    # the case's own fvSchemes (test/Tu500K-Phi1/system/fvSchemes: limitedLinear01 / limitedLinear / cubic /
+    # limitedLinearV for U), as the flame-speed regression runs it (tests/test_gpu_regression.py)
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, case.flame1d_patch_types(m),
+                       schemes=read_fv_schemes(os.path.join(golden, "flame1d", "fvSchemes")))
     ctx.chem_set_mechanism(parse_mechanism(os.path.join(golden, "Burke2012_s9r23.yaml")))
     ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
     f, bv = case.flame1d_fields(os.path.join(golden, "flame1d"), ym["species"])
@@ -258,7 +301,7 @@ def flame1d_line(steps=100, warmup=10, lib_path=None):
     ctx.sync()
     el = time.perf_counter() - t0
     ctx.close()
-    return {"workload": "1D freely-propagating H2/air flame (test/Tu500K-Phi1), 880 cells, Burke2012 9 species, "
+    return {"workload": "1D freely-propagating H2/air flame (test/Tu500K-Phi1, its fvSchemes), 880 cells, Burke2012 9 species, "
                         "waveTransmissive outlet, direct integration, dt=1e-6, nCorr=2 (BASELINE config 2)",
             "ms_per_step": el / steps * 1e3, "cell_updates_per_s": m.n_cells * steps / el, "steps": steps}
 
@@ -366,7 +409,7 @@ def config4_line(m, T, U, p, steps=3, warmup=1):
     sp = gri53_species(os.path.join(golden, "gri30.yaml"))
     t = read_thermo_table(os.path.join(golden, "thermo_gri53_synthetic.txt"), sp)
     ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
-    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6)
+    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6, schemes=case_schemes())
     gri53_dnn(ctx)
     ctx.chem_set_options(2)
     case.init_state(ctx, m, t.S, T, p, U, gri53_smooth_fractions((T - T.min()) / max(np.ptp(T), 1.0)))
@@ -448,7 +491,9 @@ def main():
         uid = [Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = {"uid": uid[0], "nranks": world, "rank": rank}
-    case.setup_context(ctx, m, table, inert, args.dt, comm=comm)
+    schemes = case_schemes() if args.schemes == "case" else gpu_schemes()
+    alt_schemes = gpu_schemes() if args.schemes == "case" else case_schemes()
+    case.setup_context(ctx, m, table, inert, args.dt, comm=comm, schemes=schemes)
     if args.traversal == "bricks" and hasattr(m, "local_index"):
         from dfmi.lib import renumber_cells
         ijk = np.stack(m.local_index, axis=1).astype(np.float64)
@@ -518,6 +563,28 @@ def main():
     ctx.kernel_timer("")
     T = ctx.get_field("T", (m.n_cells,))
     finite = bool(np.isfinite(T).all())
+    # ---- the other scheme set, timed the same way beside the headline (same state, K = alt_steps)
+    alt = None
+    if args.alt_steps > 0:
+        for term, sch in alt_schemes.items():
+            ctx.set_scheme(term, sch)
+        ctx.time_step(args.ncorr)
+        ctx.sync()
+        if world > 1:
+            dist.barrier()
+        ta = time.perf_counter()
+        for _ in range(args.alt_steps):
+            ctx.time_step(args.ncorr)
+        ctx.sync()
+        ea = time.perf_counter() - ta
+        if world > 1:
+            tt = torch.tensor([ea], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ea = float(tt.item())
+        alt = {"schemes": alt_schemes, "steps": args.alt_steps, "ms_per_step": ea / args.alt_steps * 1e3,
+               "value": m.n_cells * world * args.alt_steps / ea}
+        for term, sch in schemes.items():
+            ctx.set_scheme(term, sch)
 
     cells_total = m.n_cells * world
     value = cells_total * args.steps / el
@@ -581,6 +648,9 @@ def main():
                                f"{cells_total} hex cells ({m.n_cells} per GPU), H2/air {table.S} species "
                                f"({args.mech}), nOuter=1 nCorr={args.ncorr}, dt={args.dt}",
                    "cells_per_gpu": m.n_cells, "species": table.S, "cell_order": args.renumber,
+                   "schemes": schemes, "schemes_source": ("the case's system/fvSchemes (tests/golden/tgv64/fvSchemes)"
+                                                          if args.schemes == "case" else
+                                                          "the reference GPU path's hard-wired upwind/linear"),
                    "traversal": args.traversal,
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
@@ -616,6 +686,7 @@ def main():
                  "inferences_per_s_gemm_time": n_react * args.roof_steps / (gemm_ms / 1e3)}
                 if args.chem == "dnn" and gemm_ms > 0 else None),
         "finite": finite,
+        "other_schemes": alt,
     }
     if world == 1:   # the headline kernel against a measured copy peak as well as the datasheet's
         peak_copy = ctx.hbm_copy_peak(4.0, 20)     # dfmi_hbm_copy_peak: 16-B vector streaming copy

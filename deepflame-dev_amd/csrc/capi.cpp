@@ -562,6 +562,7 @@ int dfmi_U_process(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); do
 int dfmi_Y_process(dfmi_ctx* ctx) {
   return guard([&] {
     require_ready(ctx->x);
+    ctx->x.dnn.prepared = false;   // a compaction left by an interrupted time step belongs to an old T
     do_Y(ctx->x);
     if (ctx->x.chem.mode == 1) chem_check(ctx->x);   // the Y solve's polls have passed the chemistry
   });
@@ -580,6 +581,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
   return guard([&] {
     Ctx& x = ctx->x;
     require_ready(x);
+    x.dnn.prepared = false;         // never reuse a compaction of an earlier (failed) step
     copy_old(x);                    // preTimeStep
     if (x.chem.mode == 2) dnn_prepare(x);   // reacting cells of this step's T (read after the UEqn polls)
     rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
@@ -775,6 +777,7 @@ int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting) {
   return guard([&] {
     Ctx& x = ctx->x;
     require_ready(x);
+    x.dnn.prepared = false;         // standalone inference: compact on the current T
     dnn_solve(x, "rho");
     DFMI_HIP(hipStreamSynchronize(x.stream));
     if (n_reacting) *n_reacting = x.dnn.last_reacting;
@@ -810,6 +813,7 @@ int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps) {
     Ctx& x = ctx->x;
     require_ready(x);
     DFMI_CHECK(dt > 0 && n_steps >= 1, "0D step: dt and n_steps must be positive");
+    x.dnn.prepared = false;
     for (int i = 0; i < n_steps; ++i) {
       zero_d_step(x, dt);
       if (x.chem.mode == 1) chem_check(x);

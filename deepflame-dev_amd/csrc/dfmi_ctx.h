@@ -165,6 +165,7 @@ struct Ctx {
   DevBuf<double> md, bdv;        // mesh_distance [3][Fs], boundary delta [3][B] (dfmi_init_boundary_delta)
   bool have_bdelta = false;
   Schemes sch;
+  DevBuf<int> conv_list, conv_nlist;   // faces whose div(phi,Yi_h) limiter needs gradients (k_conv_w_check)
   // per-field patch types (host, per patch) and per-slot device copies
   std::map<std::string, std::vector<int>> ptype;
   std::map<std::string, DevBuf<int8_t>> stype;

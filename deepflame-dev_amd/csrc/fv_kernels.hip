@@ -158,12 +158,13 @@ __device__ __forceinline__ bool out01(double faceFlux, double phiP, double phiN)
 
 // Gauss linear gradient of a scalar at cell c (fvc::grad; the oracle's grad_scalar: faces in
 // increasing index, then the cell's boundary slots, / V)
+template <int WT = 0>
 __device__ __forceinline__ void cell_grad(const MeshView& m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
                                           const double* __restrict__ bvf, int c, double* g) {
   const long F = m.F, B = m.B;
   const double vc = vf[c];
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-  each_face<0>(m, c, [&](int f, int o2, bool own) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
     const double w = m.w[f], vn = vf[o2];
     const double yf = own ? interp_f(w, vc, vn) : interp_f(w, vn, vc);
     const double v0 = m.Sf[f] * yf, v1 = m.Sf[F + f] * yf, v2 = m.Sf[2 * F + f] * yf;
@@ -178,39 +179,86 @@ __device__ __forceinline__ void cell_grad(const MeshView& m, const int8_t* __res
 }
 
 // multivariate limited weights of div(phi,Yi_h) over {Y_0 .. Y_{S-1}, he} on the internal faces (face
-// storage order). Limited01's bounds are checked first for every field (he of a real mixture leaves
-// [0, 1] almost everywhere, which makes the minimum 0 without any gradient); only faces where every
-// field passes evaluate the limiters, each from the upwind cell's Gauss gradient formed on the fly.
-__global__ void k_conv_w_face(MeshView m, int S, const int8_t* __restrict__ tyY, const int8_t* __restrict__ tyH,
-                              int b01, double twoByk, const double* __restrict__ phi, const double* __restrict__ Y,
-                              const double* __restrict__ bY, const double* __restrict__ he,
-                              const double* __restrict__ bhe, double* __restrict__ wout) {
+// storage order), in two passes so that no wave idles behind a few lanes:
+//  k_conv_w_check -- one thread per face: Limited01's bounds for every field (he of a real mixture
+//    leaves [0, 1] almost everywhere, which makes the minimum 0 without any gradient); such faces get
+//    their (upwind) weight here, the others are appended to a list (the order of the list does not
+//    matter: every face's weight is computed on its own);
+//  k_conv_w_list -- a 16-lane group per listed face, one lane per field: the limiter from the upwind
+//    cell's Gauss gradient formed on the fly, the group's minimum (fmin, exact) -> the weight.
+__global__ void k_conv_w_check(MeshView m, int S, int b01, const double* __restrict__ phi,
+                               const double* __restrict__ Y, const double* __restrict__ he,
+                               double* __restrict__ wout, int* __restrict__ list, int* __restrict__ nlist) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= m.F) return;
-  const int o = m.own[f];
-  if (o < 0) return;   // owner-slot padding
-  const int n = m.nei[f];
-  const long C = m.C, Fs = m.F, B = m.B;
-  const double ph = phi[f];
-  double lim = 0.0;
-  bool zero = false;
-  if (b01) {
-    zero = out01(ph, he[o], he[n]);
-    for (int s = 0; s < S && !zero; ++s) zero = out01(ph, Y[s * C + o], Y[s * C + n]);
+  bool need = false;
+  const int o = f < m.F ? m.own[f] : -1;
+  if (o >= 0) {   // not past the end, not owner-slot padding
+    const int n = m.nei[f];
+    const long C = m.C;
+    const double ph = phi[f];
+    bool zero = false;
+    if (b01) {
+      zero = out01(ph, he[o], he[n]);
+      // the species' checks without a loop-carried exit: their loads issue together (a wave runs this
+      // branch when any of its lanes passed the he check)
+      for (int s0 = 0; s0 < S && !zero; s0 += 4) {
+        double yo[4], yn[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int s = s0 + j < S ? s0 + j : S - 1;
+          yo[j] = Y[s * C + o]; yn[j] = Y[s * C + n];
+        }
+        bool z = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z = z || out01(ph, yo[j], yn[j]);
+        zero = z;
+      }
+    }
+    if (zero) {
+      const double lim = 0.0;
+      wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+    }
+    need = !zero;
   }
-  if (!zero) {
+  // one atomic per wavefront: the leader reserves the wave's run of list entries
+  const unsigned long long mask = __ballot(need);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(nlist, (int)__popcll(mask));
+  base = __shfl(base, leader);
+  if (need) list[base + (int)__popcll(mask & ((1ull << lane) - 1ull))] = f;
+}
+constexpr int CWG = 16;   // lanes per listed face (fields beyond 16 loop)
+template <int WT>
+__global__ void __launch_bounds__(256) k_conv_w_list(MeshView m, int S, const int8_t* __restrict__ tyY,
+    const int8_t* __restrict__ tyH, double twoByk, const double* __restrict__ phi, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ he, const double* __restrict__ bhe,
+    const int* __restrict__ list, const int* __restrict__ nlist, double* __restrict__ wout) {
+  const int lane = threadIdx.x % CWG;
+  const int n_items = *nlist;
+  const int groups = gridDim.x * (blockDim.x / CWG);
+  const long C = m.C, Fs = m.F, B = m.B;
+  // a group's lanes share `it`, so each group runs the loop (and its shuffles) in lockstep
+  for (int it = blockIdx.x * (blockDim.x / CWG) + threadIdx.x / CWG; it < n_items; it += groups) {
+    const int f = list[it];
+    const int o = m.own[f], n = m.nei[f];
+    const double ph = phi[f];
     const double dv[3] = {m.md[f], m.md[Fs + f], m.md[2 * Fs + f]};
     const int cu = ph > 0 ? o : n;   // NVDTVD::r reads the upwind cell's gradient
-    for (int s = 0; s <= S; ++s) {
+    double lim = 2.0;                // above every limiter: the neutral element of the min
+    for (int s = lane; s <= S; s += CWG) {
       const double* v = s < S ? Y + s * C : he;
       const double* bv = s < S ? bY + s * B : bhe;
       double g[3];
-      cell_grad(m, s < S ? tyY : tyH, v, bv, cu, g);
-      const double l = ll_limiter(twoByk, ph, v[o], v[n], g, dv);
-      lim = s == 0 ? l : fmin(lim, l);
+      cell_grad<WT>(m, s < S ? tyY : tyH, v, bv, cu, g);
+      lim = fmin(lim, ll_limiter(twoByk, ph, v[o], v[n], g, dv));
     }
+#pragma unroll
+    for (int off = CWG / 2; off > 0; off >>= 1) lim = fmin(lim, __shfl_xor(lim, off, CWG));
+    if (lane == 0) wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
   }
-  wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
 }
 
 // the same on the boundary slots: coupled (cyclic) slots with the partner cell as N and the patch delta;
@@ -270,18 +318,41 @@ __global__ void k_conv_proc_grad(MeshView m, int S, const int8_t* __restrict__ t
   }
 }
 
-// Gauss linear gradients of ncomp scalar components (component k at vf + k*C, boundary bvf + k*B)
-// -> g [(3k + dir)][C] (fvc::grad of each vf.component(k))
-__global__ void k_grad_cells(MeshView m, const int8_t* __restrict__ ty, int ncomp, const double* __restrict__ vf,
-                             const double* __restrict__ bvf, double* __restrict__ g) {
+// Gauss linear gradients of NC scalar components (component k at vf + k*C, boundary bvf + k*B)
+// -> g [(3k + dir)][C] (fvc::grad of each vf.component(k)); one face walk for all components, each
+// component summed in cell_grad's order
+template <int NC, int WT>
+__global__ void __launch_bounds__(TPB) k_grad_cells(MeshView m, const int8_t* __restrict__ ty,
+                                                    const double* __restrict__ vf, const double* __restrict__ bvf,
+                                                    double* __restrict__ g) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
-  const long C = m.C, B = m.B;
-  for (int k = 0; k < ncomp; ++k) {
-    double gg[3];
-    cell_grad(m, ty, vf + k * C, bvf + k * B, c, gg);
-    g[(3 * k + 0) * C + c] = gg[0]; g[(3 * k + 1) * C + c] = gg[1]; g[(3 * k + 2) * C + c] = gg[2];
-  }
+  const long C = m.C, F = m.F, B = m.B;
+  double s[NC][3], vc[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) { s[k][0] = 0.0; s[k][1] = 0.0; s[k][2] = 0.0; vc[k] = vf[k * C + c]; }
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
+    const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const double vn = vf[k * C + o2];
+      const double yf = own ? interp_f(w, vc[k], vn) : interp_f(w, vn, vc[k]);
+      const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+      if (own) { s[k][0] += v0; s[k][1] += v1; s[k][2] += v2; } else { s[k][0] -= v0; s[k][1] -= v1; s[k][2] -= v2; }
+    }
+  });
+  each_slot(m, ty, c, [&](int b, int t) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const double yf = bface(m, t, vf + k * C, bvf + k * B, b, c);
+      s[k][0] += m.bSf[b] * yf; s[k][1] += m.bSf[B + b] * yf; s[k][2] += m.bSf[2 * B + b] * yf;
+    }
+  });
+  const double vol = m.V[c];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g[(3 * k + d) * C + c] = s[k][d] / vol;
 }
 
 // single-field limited weights (LimitedScheme: div(phi,K)) from a precomputed gradient g [3][C]
@@ -1975,8 +2046,23 @@ void conv_weights(Ctx& x) {
   const int b01 = x.sch.yh == SCH_LL01;
   const double twoByk = 2.0 / std::max(x.sch.k_yh, 1e-15);
   MeshView m = x.view();
-  LAUNCH(k_conv_w_face, x.Fs, m, x.S, x.st("Y"), x.st("he"), b01, twoByk, x.f("phi"), x.f("Y"), x.f("boundary_Y"),
-         x.f("he"), x.f("boundary_he"), w);
+  if (x.conv_list.n < (size_t)std::max(x.Fs, 1)) x.conv_list.alloc(std::max(x.Fs, 1));
+  if (!x.conv_nlist.n) x.conv_nlist.alloc(1);
+  DFMI_HIP(hipMemsetAsync(x.conv_nlist.p, 0, sizeof(int), x.stream));
+  LAUNCH(k_conv_w_check, x.Fs, m, x.S, b01, x.f("phi"), x.f("Y"), x.f("he"), w, x.conv_list.p, x.conv_nlist.p);
+  {
+    KScope _ks(x, "k_conv_w_list");   // a fixed grid of 16-lane groups strides over the listed faces
+    const int blocks = std::min(4096, std::max(1, blocks_for(x.Fs, 256 / CWG)));
+    if (face_rows(x))
+      hipLaunchKernelGGL(k_conv_w_list<6>, dim3(blocks), dim3(256), 0, x.stream, m, x.S, x.st("Y"), x.st("he"), twoByk,
+                         x.f("phi"), x.f("Y"), x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), x.conv_list.p,
+                         x.conv_nlist.p, w);
+    else
+      hipLaunchKernelGGL(k_conv_w_list<0>, dim3(blocks), dim3(256), 0, x.stream, m, x.S, x.st("Y"), x.st("he"), twoByk,
+                         x.f("phi"), x.f("Y"), x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), x.conv_list.p,
+                         x.conv_nlist.p, w);
+    DFMI_HIP(hipGetLastError());
+  }
   const double* bgx = nullptr;
   if (halo_active(x)) {   // processor faces: the neighbour cells' gradients (LimitedScheme::calcLimiter's pGradcN)
     double* g = scheme_buf(x, "conv_grad", x.C, 3 * (x.S + 1));
@@ -2004,7 +2090,8 @@ static void e_scheme_terms(Ctx& x) {
       bool coupled = false;
       for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
       DFMI_CHECK(!coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
-      LAUNCH(k_grad_cells, x.C, m, x.st("K"), 1, x.f("K"), x.f("boundary_K"), g);
+      if (face_rows(x)) LAUNCH((k_grad_cells<1, 6>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
+      else LAUNCH((k_grad_cells<1, 0>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
       halo_fields(x, {"gradK"});   // the neighbour cell's gradient on processor faces (patchNeighbourField)
     }
     // upwind: limiter 0 everywhere (Limited01 with bounds that reject every face)
@@ -2023,7 +2110,8 @@ static void e_scheme_terms(Ctx& x) {
     double* bcf = scheme_buf(x, "boundary_cubic_flux", x.B, 1);
     double* g = scheme_buf(x, "gradHD", x.C, 9);
     scheme_buf(x, "boundary_gradHD", x.B, 9);
-    LAUNCH(k_grad_cells, x.C, m, x.st("calculated"), 3, x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
+    if (face_rows(x)) LAUNCH((k_grad_cells<3, 6>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
+    else LAUNCH((k_grad_cells<3, 0>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
     halo_fields(x, {"gradHD"});
     LAUNCH(k_cubic_face, x.Fs, m, x.f("hDiffCorrFlux"), g, cf);
     LAUNCH(k_cubic_slot, x.B, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g,

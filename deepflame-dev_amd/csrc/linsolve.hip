@@ -1033,7 +1033,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   }
   const long N = nsys * Ce;
   double* base = WS.buf.p;
-  // U's three components share one operator: built and read once (k_ell_build vshared)
+  // U's three components share one operator: built and read once (k_ell_build vshared). Valid because every
+  // coupled patch this library accepts is translational (cyclic / processor / processorCyclic: the generic
+  // "coupled" code and rotational transforms are rejected at dfmi_set_patch_types), so the coupled-slot
+  // coefficients -boundaryCoeffs do not depend on the vector component
   const int vshared = (!prebuilt && nsys > 1 && lstride == 0 && ustride == 0 && std::string(eqn) == "U") ? 1 : 0;
   BV b{base, base + N, base + 2 * N, base + 3 * N, base + 4 * N, base + 5 * N, base + 6 * N, base + 7 * N,
        base + 8 * N, vshared};
@@ -1211,7 +1214,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       AmgLevel& l0 = x.amg.lv[0];
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
-        KScope _ks(x, "k_cg_x");
+        KScope _ks(x, "k_cg_x_smooth");   // its own timer name: tests assert the fused path ran
         hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.col.p, red, WS.scal.p, xsol, v,
                            pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
                            l0.fx.p, l0.fr.p);

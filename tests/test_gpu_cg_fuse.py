@@ -28,10 +28,13 @@ def _run(fuse):
         f = case.tgv_fields(m, ym["species"], kernel_radius=1.2e-3)
         case.init_state(ctx, m, t.S, f["T"], f["p"], f["U"], f["Y"])
         ctx.call("pre_time_step")
+        ctx.kernel_timer("k_cg_x_smooth")     # the fused launch has its own timer name
         ctx.time_step(2)
+        fused_launches = ctx.kernel_time("k_cg_x_smooth")[1]
         out = {k: ctx.get_field(k, (m.n_cells,)) for k in ("p", "T", "rho")}
         out["U"] = ctx.get_field("U", (3, m.n_cells))
         out["p_iters"] = ctx.solver_stats("p")[0]
+        out["fused_launches"] = fused_launches
         ctx.close()
         return out
     finally:
@@ -41,5 +44,7 @@ def _run(fuse):
 def test_fused_pcg_update_is_bitwise_the_separate_launches():
     a, b = _run(1), _run(0)
     assert a["p_iters"] == b["p_iters"] and a["p_iters"] > 3, (a["p_iters"], b["p_iters"])
+    # the comparison means something only if the fused kernel ran in one run and not in the other
+    assert a["fused_launches"] > 0 and b["fused_launches"] == 0, (a["fused_launches"], b["fused_launches"])
     for k in ("p", "T", "rho", "U"):
         assert np.array_equal(a[k], b[k]), k

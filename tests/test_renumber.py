@@ -111,3 +111,38 @@ def test_oracle_step_invariant_under_renumbering():
     for k in ("T", "p", "rho", "he", "U", "Y"):
         assert rel_err(r.cell_field_back(b[k]), a[k]) < 1e-12, k
     assert rel_err(b["phi"], r.face_flux(a["phi"])) < 1e-12
+
+
+def test_renumber_decomposed_unequal_blocks():
+    """a decomposition with unequal rank sizes (RCB into 3) renumbered rank by rank: every
+    procCol still names the same physical cell (its centre) after both sides' permutations; renumber_mesh
+    alone refuses such a mesh instead of mis-mapping it"""
+    import numpy as np
+    import pytest
+    from dfmi.mesh import hex_box
+    from dfmi.partition import partition_cells, decompose
+    from dfmi.renumber import renumber_mesh, renumber_decomposed
+    mg = hex_box(7, 5, 4, periodic=(True, False, True))
+    part = partition_cells(mg, 3, "rcb")
+    meshes = decompose(mg, part)
+    sizes = [mm.n_cells for mm in meshes]
+    assert len(set(sizes)) > 1
+    bad = [mm for mm in meshes if mm.global_offset % mm.n_cells or mm.n_total_cells % mm.n_cells]
+    assert bad
+    with pytest.raises(ValueError, match="unequal"):
+        renumber_mesh(bad[0], "morton")
+    new, rens = renumber_decomposed(meshes, "morton")
+    offs = np.array([mm.global_offset for mm in meshes] + [mg.n_cells])
+    for r, (mo, mn) in enumerate(zip(meshes, new)):
+        assert np.allclose(mn.cell_centres, mo.cell_centres[rens[r].cells])
+        for po, pn in zip(mo.patches, mn.patches):
+            if po.nbr_cells_global is None:
+                continue
+            go = np.asarray(po.nbr_cells_global); gn = np.asarray(pn.nbr_cells_global)
+            for a, b in zip(go, gn):
+                qa = np.searchsorted(offs, a, side="right") - 1
+                qb = np.searchsorted(offs, b, side="right") - 1
+                assert qa == qb
+                assert np.allclose(meshes[qa].cell_centres[a - offs[qa]], new[qb].cell_centres[b - offs[qb]])
+            # this side's face cells follow its own permutation
+            assert np.allclose(mn.cell_centres[pn.face_cells], mo.cell_centres[po.face_cells])
