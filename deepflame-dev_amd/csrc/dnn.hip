@@ -52,6 +52,10 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 v) {
   return __builtin_elementwise_fma(hv, se, hv);
 }
 
+// fp16 rounding kept in fp32 registers: torch's fp16 Linear writes its output (x W^T + b, fp32
+// accumulation) as fp16 before the GELU reads it, and the GELU's own output is rounded again
+__device__ __forceinline__ f32x2 round16(f32x2 v) { return {(float)(_Float16)v.x, (float)(_Float16)v.y}; }
+
 // 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_wave + 16 l
 __device__ __forceinline__ void glds16(const _Float16* g, _Float16* lds_wave) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -185,7 +189,7 @@ __global__ void __launch_bounds__(256, 2)
         f32x2 sacc = {0.0f, 0.0f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          f32x2 v = f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j];
+          f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j]);   // the Linear's fp16 output
           if (GELU) v = gelu_fast2(v);
           const f32x2 hq = {(float)(_Float16)v.x, (float)(_Float16)v.y};   // the fp16 activation
           sacc = __builtin_elementwise_fma(hq, f32x2(wv[j]), sacc);
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
         const int rl = wm + 16 * i + 4 * (lane >> 4) + e;
-        f32x2 v = f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv;
+        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
         if (GELU) v = gelu_fast2(v);
         cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
         cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
@@ -281,11 +285,11 @@ __global__ void k_dnn_input(int n, int C, int S, int Kp, const int* __restrict__
   if (i >= n) return;
   const int c = idx[i];
   _Float16* row = X + (long)i * Kp;
-  row[0] = (_Float16)((T[c] - Xmu[0]) / Xstd[0]);
-  row[1] = (_Float16)((101325.0 - Xmu[1]) / Xstd[1]);
+  row[0] = (_Float16)(float)((T[c] - Xmu[0]) / Xstd[0]);   // torch's double -> half goes through float
+  row[1] = (_Float16)(float)((101325.0 - Xmu[1]) / Xstd[1]);
   for (int s = 0; s < S; ++s) {
     const double b = (pow(Y[(long)s * C + c], 0.1) - 1.0) * 10.0;
-    row[2 + s] = (_Float16)((b - Xmu[2 + s]) / Xstd[2 + s]);
+    row[2 + s] = (_Float16)(float)((b - Xmu[2 + s]) / Xstd[2 + s]);
   }
   for (int k = S + 2; k < Kp; ++k) row[k] = (_Float16)0.0f;
 }
@@ -340,7 +344,7 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
     d.Kp[l] = (dims[l] + KPAD - 1) / KPAD * KPAD;
     if (l == nlayers - 1) DFMI_CHECK(dims[l] % 8 == 0, "DNN: last hidden width must be a multiple of 8");
   }
-  // repack weights: per layer [module][out][Kp] fp16 (K zero-padded), biases fp32 [module][out]
+  // repack weights: per layer [module][out][Kp] fp16 (K zero-padded), biases fp16-rounded, kept as fp32 [module][out]
   d.W.clear(); d.b.clear();
   d.W.resize(nlayers); d.b.resize(nlayers);
   std::vector<std::vector<_Float16>> hw(nlayers);
@@ -356,7 +360,7 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
       for (int o = 0; o < out; ++o)
         for (int i = 0; i < in; ++i) hw[l][((size_t)m * out + o) * d.Kp[l] + i] = (_Float16)p[(size_t)o * in + i];
       p += (size_t)out * in;
-      for (int o = 0; o < out; ++o) hb[l][(size_t)m * out + o] = p[o];
+      for (int o = 0; o < out; ++o) hb[l][(size_t)m * out + o] = (float)(_Float16)p[o];   // module.to(kHalf)
       p += out;
     }
   for (int l = 0; l < nlayers; ++l) {

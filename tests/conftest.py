@@ -15,6 +15,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libdfmi.so)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """Some GPU tests compare against torch running on the device (the DNN's fp16 restatement). torch
+    ships its own HIP runtime; it must initialise before libdfmi.so's, or torch finds no GPU (smoke() and
+    bench.py initialise torch first as well)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def es80():
     from dfmi.mech import read_thermo_table, read_yaml_mechanism

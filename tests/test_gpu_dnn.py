@@ -99,6 +99,53 @@ def test_dnn_matches_torch_fp32():
     assert np.all(np.isfinite(RR))
     assert np.median(err) < 2e-3, np.median(err)
     assert err.max() < 2e-2, err.max()
+    _check_half_semantics(RR, mods, T, p, rho, Y, XMU, XSTD, YMU, YSTD)
+
+
+def _half_reference(mods, T, p, rho, Y, xmu, xstd, ymu, ystd, dt=1e-6, Tr=610.0):
+    """fp16-everywhere restatement on the GPU, as the reference runs it: modules_[i].to(device, kHalf)
+    (dfChemistrySolver.cu:125), the normalised double input .to(kHalf) (:175), each net's output
+    .to(kDouble) (:180) -- torch's own fp16 Linear (fp32 accumulation, fp16 output) and GELU"""
+    import torch
+    torch.backends.cuda.matmul.allow_fp16_reduced_precision_reduction = False
+    S, C = Y.shape
+    react = T >= Tr
+    Yr = Y[:, react]
+    bct = (Yr ** 0.1 - 1) * 10
+    x = np.concatenate([T[react][None, :], np.full((1, react.sum()), 101325.0), bct], axis=0).T
+    x = (x - np.asarray(xmu)) / np.asarray(xstd)
+    xt = torch.tensor(x, dtype=torch.float64, device="cuda").to(torch.float16)
+    yn = np.zeros((S - 1, react.sum()))
+    with torch.no_grad():
+        for m, layers in enumerate(mods):
+            h = xt
+            for l, (W, b) in enumerate(layers):
+                Wt = torch.tensor(W, device="cuda").to(torch.float16)
+                bt = torch.tensor(b, device="cuda").to(torch.float16)
+                h = torch.nn.functional.linear(h, Wt, bt)
+                if l < len(layers) - 1:
+                    h = torch.nn.functional.gelu(h)
+            out = h[:, 0].to(torch.float64).cpu().numpy()
+            yn[m] = ((out * ystd[m] + ymu[m] + bct[m]) * 0.1 + 1) ** 10
+    yn = yn / (yn.sum(axis=0) + Yr[S - 1])
+    RR = np.zeros((S, C))
+    RR[:S - 1, react] = (yn - Yr[:S - 1]) * rho[react] * (p[react] / 101325.0) / dt
+    return RR
+
+
+def _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd):
+    """per species, RR against the fp16-everywhere restatement: the kernel rounds where torch rounds
+    (input, Linear output, GELU output, net output), so what remains is fp32 summation order and the
+    erf approximation flipping the last fp16 bit of some activations"""
+    S = Y.shape[0]
+    ref = _half_reference(mods, T, p, rho, Y, xmu, xstd, ymu, ystd)
+    scale = np.abs(ref).max(axis=1, keepdims=True)[:S - 1]
+    err = np.abs(RR[:S - 1] - ref[:S - 1]) / scale
+    per_species = err.max(axis=1)
+    print("fp16-everywhere: median", np.median(err), "per-species max", per_species.max(),
+          "exact fraction", float(np.mean(RR[:S - 1] == ref[:S - 1])))
+    assert np.median(err) < 1e-4, np.median(err)
+    assert per_species.max() < 4e-3, per_species
 
 
 def test_dnn_53_species_matches_torch_fp32():
@@ -163,3 +210,4 @@ def test_dnn_53_species_matches_torch_fp32():
     err = np.abs(RR[:S - 1] - ref[:S - 1]) / scale
     assert np.median(err) < 2e-3, np.median(err)
     assert err.max() < 2e-2, err.max()
+    _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd)
