@@ -186,49 +186,71 @@ __device__ __forceinline__ void cell_grad(const MeshView& m, const int8_t* __res
 //    matter: every face's weight is computed on its own);
 //  k_conv_w_list -- a 16-lane group per listed face, one lane per field: the limiter from the upwind
 //    cell's Gauss gradient formed on the fly, the group's minimum (fmin, exact) -> the weight.
-__global__ void k_conv_w_check(MeshView m, int S, int b01, const double* __restrict__ phi,
-                               const double* __restrict__ Y, const double* __restrict__ he,
-                               double* __restrict__ wout, int* __restrict__ list, int* __restrict__ nlist) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  bool need = false;
-  const int o = f < m.F ? m.own[f] : -1;
-  if (o >= 0) {   // not past the end, not owner-slot padding
-    const int n = m.nei[f];
-    const long C = m.C;
-    const double ph = phi[f];
-    bool zero = false;
-    if (b01) {
-      zero = out01(ph, he[o], he[n]);
-      // the species' checks without a loop-carried exit: their loads issue together (a wave runs this
-      // branch when any of its lanes passed the he check)
-      for (int s0 = 0; s0 < S && !zero; s0 += 4) {
-        double yo[4], yn[4];
+// The list is reserved with ONE atomic per workgroup (1024 threads x 4 faces): a per-wavefront atomic on
+// the single counter serialised ~10^5 times per launch (most waves hold a listed face) and cost 450 us.
+constexpr int CK_TPB = 1024, CK_FPT = 4, CK_NW = CK_TPB / 64;
+__global__ void __launch_bounds__(CK_TPB) k_conv_w_check(MeshView m, int S, int b01, const double* __restrict__ phi,
+                                                         const double* __restrict__ Y, const double* __restrict__ he,
+                                                         double* __restrict__ wout, int* __restrict__ list,
+                                                         int* __restrict__ nlist) {
+  __shared__ int wcnt[CK_FPT * CK_NW];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long C = m.C;
+  unsigned long long mask[CK_FPT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int s = s0 + j < S ? s0 + j : S - 1;
-          yo[j] = Y[s * C + o]; yn[j] = Y[s * C + n];
+  for (int j = 0; j < CK_FPT; ++j) {
+    const int f = (blockIdx.x * CK_FPT + j) * CK_TPB + threadIdx.x;
+    bool need = false;
+    const int o = f < m.F ? m.own[f] : -1;
+    if (o >= 0) {   // not past the end, not owner-slot padding
+      const int n = m.nei[f];
+      const double ph = phi[f];
+      bool zero = false;
+      if (b01) {
+        zero = out01(ph, he[o], he[n]);
+        // the species' checks without a loop-carried exit: their loads issue together (a wave runs this
+        // branch when any of its lanes passed the he check)
+        for (int s0 = 0; s0 < S && !zero; s0 += 4) {
+          double yo[4], yn[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int sp = s0 + q < S ? s0 + q : S - 1;
+            yo[q] = Y[sp * C + o]; yn[q] = Y[sp * C + n];
+          }
+          bool z = false;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z = z || out01(ph, yo[q], yn[q]);
+          zero = z;
         }
-        bool z = false;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) z = z || out01(ph, yo[j], yn[j]);
-        zero = z;
       }
+      if (zero) {
+        const double lim = 0.0;
+        wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+      }
+      need = !zero;
     }
-    if (zero) {
-      const double lim = 0.0;
-      wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
-    }
-    need = !zero;
+    mask[j] = __ballot(need);
+    if (lane == 0) wcnt[j * CK_NW + wid] = (int)__popcll(mask[j]);
   }
-  // one atomic per wavefront: the leader reserves the wave's run of list entries
-  const unsigned long long mask = __ballot(need);
-  if (mask == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(nlist, (int)__popcll(mask));
-  base = __shfl(base, leader);
-  if (need) list[base + (int)__popcll(mask & ((1ull << lane) - 1ull))] = f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int k = 0; k < CK_FPT * CK_NW; ++k) tot += wcnt[k];
+    base = tot ? atomicAdd(nlist, tot) : 0;
+  }
+  __syncthreads();
+  int off = base;   // entries of the (j, wave) runs before this wave's run of pass j
+  for (int k = 0; k < wid; ++k) off += wcnt[k];
+#pragma unroll
+  for (int j = 0; j < CK_FPT; ++j) {
+    if ((mask[j] >> lane) & 1ull)
+      list[off + (int)__popcll(mask[j] & ((1ull << lane) - 1ull))] = (blockIdx.x * CK_FPT + j) * CK_TPB + threadIdx.x;
+    // next pass: skip the remaining waves of pass j and the first waves of pass j + 1
+    for (int k = wid; k < CK_NW; ++k) off += wcnt[j * CK_NW + k];
+    if (j + 1 < CK_FPT)
+      for (int k = 0; k < wid; ++k) off += wcnt[(j + 1) * CK_NW + k];
+  }
 }
 constexpr int CWG = 16;   // lanes per listed face (fields beyond 16 loop)
 template <int WT>
@@ -2049,7 +2071,14 @@ void conv_weights(Ctx& x) {
   if (x.conv_list.n < (size_t)std::max(x.Fs, 1)) x.conv_list.alloc(std::max(x.Fs, 1));
   if (!x.conv_nlist.n) x.conv_nlist.alloc(1);
   DFMI_HIP(hipMemsetAsync(x.conv_nlist.p, 0, sizeof(int), x.stream));
-  LAUNCH(k_conv_w_check, x.Fs, m, x.S, b01, x.f("phi"), x.f("Y"), x.f("he"), w, x.conv_list.p, x.conv_nlist.p);
+  {
+    KScope _ks(x, "k_conv_w_check");
+    const int blocks = (int)((x.Fs + (long)CK_TPB * CK_FPT - 1) / ((long)CK_TPB * CK_FPT));
+    if (blocks > 0)
+      hipLaunchKernelGGL(k_conv_w_check, dim3(blocks), dim3(CK_TPB), 0, x.stream, m, x.S, b01, x.f("phi"), x.f("Y"),
+                         x.f("he"), w, x.conv_list.p, x.conv_nlist.p);
+    DFMI_HIP(hipGetLastError());
+  }
   {
     KScope _ks(x, "k_conv_w_list");   // a fixed grid of 16-lane groups strides over the listed faces
     const int blocks = std::min(4096, std::max(1, blocks_for(x.Fs, 256 / CWG)));
