@@ -1047,6 +1047,10 @@ int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int*
     for (int l = 0; l < (int)x.amg.size() && l < max_levels; ++l) { cells[l] = x.amg[l].n; width[l] = x.amg[l].W; }
   });
 }
+int dfmi_row_classes(dfmi_ctx*, int* n) {   // explicit CSR rows on the CPU
+  if (n) *n = 0;
+  return 0;
+}
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel) {
   return guard([&] {
     auto it = ctx->x.stats.find(eqn);

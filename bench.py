@@ -35,17 +35,22 @@ MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species 
 }
 
 
-def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None, W: int = 6) -> float:
+def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None, W: int = 6,
+                      classes: bool = False) -> float:
     """Bytes one unit of a kernel's work must move at minimum: every input element read once and every
     output element written once (fp64 values, int32 indices, int8 slot types), shared face/cell arrays
     counted ONCE per launch however many species use them. Units: one launch for the assembly/thermo
     kernels (all species of that launch); k_cg_spmv one active PCG iteration; k_bcg_spmv one SpMV of
     one active system. Bc = coupled boundary slots (cyclic / processor), W = solver row width.
     Gather topology of the cell-centric kernels: 12 B per cell (nbrStart, ownStart, cbStart) + 12 B per
-    face (nbrFace, own, nei) + 9 B per coupled slot (cbSlot, partner, type). DESIGN.md 5 lists them."""
+    face (nbrFace, own, nei) + 9 B per coupled slot (cbSlot, partner, type). DESIGN.md 5 lists them.
+    classes: the gather rows are decoded from row classes (dfmi_row_classes > 0: 1 B per cell, cbStart for
+    the boundary slots), so the per-face index bytes are not read -- topology 5 B per cell + 9 B per coupled
+    slot, and the solver matrices' 8 B of owner/neighbour ids per face become 1 B per cell."""
     Sa = S - 1                                     # solved species (inert excluded)
     Bc = B if Bc is None else Bc
-    topo = 12.0 * C + 12.0 * F + 9.0 * Bc
+    topo = (5.0 * C + 9.0 * Bc) if classes else (12.0 * C + 12.0 * F + 9.0 * Bc)
+    mat = (C * 1.0 + F * 16.0) if classes else F * 24.0   # solver matrix per SpMV (values + indices)
     if kernel == "k_y_prep":
         # Y, hai, rhoD (S each), alpha, V in; sumYDiffError, hDiffCorrFlux (3 each), diffAlphaD out;
         # faces w, Sf, magSf, dc; coupled slots bw, bSf, bmagSf, bdc
@@ -76,11 +81,11 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
         # fused PCG step p = z + beta p_old; q = A p: cells z, p_old, dS in, p, q out (40 B);
         # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
         # ELL gather stores the same 2 x 12 B per face from the two cells' sides); coupled slots 12 B
-        return C * 40.0 + F * 24.0 + Bc * 12.0
+        return C * 40.0 + mat + Bc * 12.0
     if kernel == "k_bcg_spmv":
         # mean of the two SpMVs of an iteration: v = A p reads dS, p, r0, writes v (32 B / cell);
         # t = A s with s = r - alpha v formed on the fly reads dS, r, v, r0, writes t (40 B); matrix as above
-        return C * 36.0 + F * 24.0 + Bc * 12.0
+        return C * 36.0 + mat + Bc * 12.0
     if kernel == "k_thermo_cells":
         # T, he, p, Y (S) in; T, he, psi, rho, mu, alpha, rhoD (S), hai (S) out
         return C * 8.0 * (3 + S) + C * 8.0 * (6 + 2 * S)
@@ -586,6 +591,7 @@ def main():
         for term, sch in schemes.items():
             ctx.set_scheme(term, sch)
 
+    ncls = ctx.row_classes()
     cells_total = m.n_cells * world
     value = cells_total * args.steps / el
     # HBM bytes per launch from the PMC passes committed under profiles/ (scripts/pmc_traffic.sh +
@@ -615,10 +621,11 @@ def main():
         ms, nl = ktime[k]
         if not nl or ms <= 0:
             continue
-        per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc)
+        per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc, classes=ncls > 0)
         total_bytes = per_unit * units[k]
         if k == "k_bcg_spmv":   # U's three components share one operator: its bytes count once per three systems
-            total_bytes -= 2.0 * work["U"] * (2.0 / 3.0) * (24.0 * m.n_faces + 12.0 * Bc)
+            total_bytes -= 2.0 * work["U"] * (2.0 / 3.0) * ((1.0 * m.n_cells + 16.0 * m.n_faces if ncls > 0 else
+                                                              24.0 * m.n_faces) + 12.0 * Bc)
         achieved = total_bytes / (ms / 1e3) / 1e9
         tr = pmc.get(k)
         roofs[k] = {"kernel": k, "bound": "hbm" if k != "k_thermo_cells" else "fp64-valu",
@@ -669,11 +676,13 @@ def main():
                                     "rocprofv3 --stats summary of the same command, frac = bytes_per_unit x units / "
                                     "summed kernel time (scripts/roof_from_profile.py)",
                             "bytes_per_unit": {k: algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots,
-                                                                    table.S, m.n_coupled_slots)
+                                                                    table.S, m.n_coupled_slots, classes=ncls > 0)
                                                for k in ("k_bcg_spmv", "k_cg_spmv")},
                             # U's shared operator: each U SpMV's matrix bytes count one third
-                            "u_matrix_bytes": 24.0 * m.n_faces + 12.0 * m.n_coupled_slots},
+                            "u_matrix_bytes": (1.0 * m.n_cells + 16.0 * m.n_faces if ncls > 0 else 24.0 * m.n_faces)
+                                              + 12.0 * m.n_coupled_slots},
         "amg_levels": ctx.amg_info(),
+        "row_classes": ncls,
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
                        "k_chem_ms_per_step": chem_ms / max(chem_n, 1),

@@ -75,7 +75,7 @@ void amg_setup(Ctx& x);
 void amg_galerkin(Ctx& x, const double* val0, const double* D0);
 // z = M^-1 r with block partials of r.z written to partial[0 .. nblk) (grid of `nblk` blocks); every
 // kernel returns at once when *active == 0 (a converged solve; nullptr: always run)
-void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
+void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
                double* partial, int nblk, const double* active = nullptr, bool l0_done = false);
 // the level-0 first sweep (x0, residual) can be written by the PCG update kernel instead (linsolve.hip:
 // k_cg_x_smooth): fp32 V-cycle, launch-per-level path, one pre-sweep, at least two levels

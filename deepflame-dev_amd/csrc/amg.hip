@@ -66,7 +66,7 @@ __global__ void k_round_f32(long n, const double* __restrict__ a, float* __restr
 
 // x = omega b / D (first sweep from zero); r = b - A x   (columns >= n: other ranks, dropped)
 template <int WT, class T, class TB>
-__global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, ColView col,
                                                     const T* __restrict__ val, const T* __restrict__ D,
                                                     const TB* __restrict__ b, T omega,
                                                     T* __restrict__ x, T* __restrict__ r, const double* act) {
@@ -76,9 +76,10 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, const int* __
   const T bc = (T)b[c];
   const T xc = omega * bc / D[c];
   T y = D[c] * xc;
+const int* ct = col.row(c);
 #pragma unroll
   for (int k = 0; k < W; ++k) {
-    const int j = col[(long)k * n + c];
+    const int j = col.get(ct, n, k, c);
     if (j < n) y += val[(long)k * n + c] * (omega * (T)b[j] / D[j]);
   }
   x[c] = xc;
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(TPB) k_smooth_restrict(int nc, const int* __re
 
 // a further level-0 pre-sweep on (x, r = b - A x): x += omega r / D, r' = r - A (omega r / D)
 template <int WT, class T>
-__global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, ColView col,
                                                      const T* __restrict__ val, const T* __restrict__ D,
                                                      const T* __restrict__ r, T omega, T* __restrict__ x,
                                                      T* __restrict__ rn, const double* act) {
@@ -125,9 +126,10 @@ __global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, const int* _
   const T rc = r[c];
   const T dc = omega * rc / D[c];
   T y = D[c] * dc;
+const int* ct = col.row(c);
 #pragma unroll
   for (int k = 0; k < W; ++k) {
-    const int j = col[(long)k * n + c];
+    const int j = col.get(ct, n, k, c);
     if (j < n) y += val[(long)k * n + c] * (omega * r[j] / D[j]);
   }
   x[c] += dc;
@@ -136,7 +138,7 @@ __global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, const int* _
 
 // a further level-0 post-sweep: out = in + omega (b - A in) / D; optional block partials of b.out
 template <int WT, class T, class TB, class TO>
-__global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, ColView col,
                                                       const T* __restrict__ val, const T* __restrict__ D,
                                                       const TB* __restrict__ b, const TO* __restrict__ in, T omega,
                                                       TO* __restrict__ out, double* partial, const double* act) {
@@ -147,9 +149,10 @@ __global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, const int* 
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = (T)in[c];
     T ay = D[c] * yc;
+const int* ct = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col[(long)k * n + c];
+      const int j = col.get(ct, n, k, c);
       if (j < n) ay += val[(long)k * n + c] * (T)in[j];
     }
     const TB bc = b[c];
@@ -208,7 +211,7 @@ __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __
 // y = x + s P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z,
 // formed in double from the values actually stored)
 template <int WT, class T, class TB, class TO>
-__global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, ColView col,
                                                         const T* __restrict__ val, const T* __restrict__ D,
                                                         const TB* __restrict__ b, const T* __restrict__ x,
                                                         const int* __restrict__ agg, const T* __restrict__ xc,
@@ -221,9 +224,10 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, const int
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = x[c] + sc * xc[agg[c]];
     T ay = D[c] * yc;
+const int* ct = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col[(long)k * n + c];
+      const int j = col.get(ct, n, k, c);
       if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
     }
     const TB bc = b[c];
@@ -604,7 +608,7 @@ void launch_w(int W, dim3 g, hipStream_t st, K0 k0, K6 k6, A... a) {
 
 // z = M^-1 r in precision T; block partials of r.z (one per block of the level-0 grid) into `partial`
 template <class T>
-void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
+void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
              double* partial, int nblk, const double* act, bool l0_done) {
   constexpr bool F = std::is_same<T, float>::value;
   Amg& a = x.amg;
@@ -616,7 +620,9 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
   auto DD = [&](int l) -> const T* {
     if constexpr (F) return a.lv[l].fD.p; else return l == 0 ? D0 : (const double*)a.lv[l].D.p;
   };
-  auto COL = [&](int l) { return l == 0 ? col0 : (const int*)a.lv[l].col.p; };
+  // level 0: the solver rows (row classes where built); coarse levels: explicit columns
+  auto COL = [&](int l) { return l == 0 ? col0 : ColView{a.lv[l].col.p, nullptr, nullptr, a.lv[l].W}; };
+  auto RAW = [&](int l) { return l == 0 ? col0.col : (const int*)a.lv[l].col.p; };
   auto BV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fb.p; else return a.lv[l].b.p; };
   auto XV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fx.p; else return a.lv[l].x.p; };
   auto RV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fr.p; else return a.lv[l].r.p; };
@@ -638,7 +644,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
     ca.L = L;
     for (int l = 1; l < L; ++l) {
       AmgLevel& v = a.lv[l];
-      ca.n[l] = v.n; ca.W[l] = v.W; ca.col[l] = COL(l); ca.val[l] = VAL(l); ca.D[l] = DD(l);
+      ca.n[l] = v.n; ca.W[l] = v.W; ca.col[l] = RAW(l); ca.val[l] = VAL(l); ca.D[l] = DD(l);
       ca.b[l] = BV(l); ca.x[l] = XV(l); ca.r[l] = RV(l); ca.xo[l] = XO(l);
       ca.agg[l] = v.agg.p; ca.mstart[l] = v.mstart.p; ca.members[l] = v.members.p;
     }
@@ -667,15 +673,15 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
       const dim3 gc(blocks_for(a.lv[l + 1].n, TPB));
       if (l == 0)
         hipLaunchKernelGGL((k_smooth_restrict<T, double>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
-                           f.members.p, f.n, f.W, COL(0), VAL(0), DD(0), r, om, XV(0), BV(1), act);
+                           f.members.p, f.n, f.W, RAW(0), VAL(0), DD(0), r, om, XV(0), BV(1), act);
       else
         hipLaunchKernelGGL((k_smooth_restrict<T, T>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
-                           f.members.p, f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
+                           f.members.p, f.n, f.W, RAW(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
       continue;
     }
     if (l > 0 && a.padded) {   // aggregates in aligned groups of 8: smoothing and restriction in one launch
       KScope _ks(x, "k_smooth_res");
-      launch_w(f.W, g, x.stream, k_smooth_res_r8<0, T>, k_smooth_res_r8<6, T>, f.n, f.W, COL(l), VAL(l), DD(l),
+      launch_w(f.W, g, x.stream, k_smooth_res_r8<0, T>, k_smooth_res_r8<6, T>, f.n, f.W, RAW(l), VAL(l), DD(l),
                (const T*)BV(l), om, XV(l), BV(l + 1), act);
       continue;
     }
@@ -710,10 +716,10 @@ void apply_t(Ctx& x, const double* val0, const double* D0, const int* col0, cons
     AmgLevel& c = a.lv[L - 1];
     KScope _ks(x, "k_coarsest");
     if (L > 1)
-      hipLaunchKernelGGL((k_coarsest<T, T, T>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, COL(L - 1), VAL(L - 1),
+      hipLaunchKernelGGL((k_coarsest<T, T, T>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, RAW(L - 1), VAL(L - 1),
                          DD(L - 1), (const T*)BV(L - 1), om, a.coarse_sweeps, XV(L - 1), act);
     else if constexpr (!F)   // single level (double only): solve straight into z
-      hipLaunchKernelGGL((k_coarsest<double, double, double>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, col0, val0,
+      hipLaunchKernelGGL((k_coarsest<double, double, double>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, col0.col, val0,
                          D0, r, om, a.coarse_sweeps, z, act);
   }
   if (L == 1) {
@@ -786,7 +792,7 @@ bool amg_l0_fusable(const Ctx& x) {
          !(a.coop_blocks > 0 && a.lv.size() >= 3);
 }
 
-void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, const double* r, double* z,
+void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
                double* partial, int nblk, const double* active, bool l0_done) {
   Amg& a = x.amg;
   DFMI_CHECK(!l0_done || amg_l0_fusable(x), "AMG: level-0 sweep fused on an unsupported configuration");
@@ -795,7 +801,7 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, const int* col0, co
     else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
   };
   if (!a.use_graph || !x.ktimer.targets.empty()) { direct(); return; }
-  const std::array<uintptr_t, 8> key{(uintptr_t)val0, (uintptr_t)D0, (uintptr_t)col0, (uintptr_t)r, (uintptr_t)z,
+  const std::array<uintptr_t, 8> key{(uintptr_t)val0, (uintptr_t)D0, (uintptr_t)col0.col, (uintptr_t)r, (uintptr_t)z,
                                      (uintptr_t)partial, (uintptr_t)nblk * 2 + (l0_done ? 1 : 0), (uintptr_t)active};
   auto it = a.graphs.find(key);
   if (it == a.graphs.end()) {

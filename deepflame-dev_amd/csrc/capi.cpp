@@ -837,6 +837,10 @@ int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int*
   });
 }
 
+int dfmi_row_classes(dfmi_ctx* ctx, int* n) {
+  return guard([&] { *n = ctx->x.ell.ready ? ctx->x.ell.ncls : 0; });
+}
+
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
   return guard([&] {
     std::string e(eqn), n(name);

@@ -93,4 +93,25 @@ template <class T> struct PinnedBuf {
 
 inline int blocks_for(long n, int tpb) { return (int)((n + tpb - 1) / tpb); }
 
+// Columns of the per-cell gather rows [W][C] (the solver ELL, linsolve.hip build_ell). Row classes: on
+// meshes where few distinct rows occur relative to the cell (a hex box in blockMesh order: 27 -- interior,
+// faces, edges, corners), cell c stores one byte, its class, and the class table holds the W column
+// offsets j - c; an entry the table cannot express (a processor halo column) is read from the explicit
+// array. A gather then reads 1 B per cell instead of 4 W B (24 B on hex meshes). cls == nullptr: explicit.
+constexpr int CEXPL = -2147483647 - 1;   // class-table entry: read the explicit array
+struct ColView {
+  const int* col = nullptr;         // explicit [W][C]
+  const uint8_t* cls = nullptr;     // [C] row class, or nullptr
+  const int* tab = nullptr;         // [ncls][W] column offsets
+  int W = 0;
+  __device__ __forceinline__ const int* row(int c) const { return cls ? tab + (int)cls[c] * W : nullptr; }
+  __device__ __forceinline__ int get(const int* t, long C, int k, int c) const {
+    if (t) {
+      const int o = t[k];
+      if (o != CEXPL) return c + o;
+    }
+    return col[k * C + c];
+  }
+};
+
 }  // namespace dfmi

@@ -26,6 +26,8 @@
 
 namespace dfmi {
 
+constexpr int SCODE_PAD = -1;   // row-class source code of a padding entry (esrc PAD)
+
 struct MeshView {
   int C, F, B, S;
   const int *own, *nei, *ownStart, *nbrStart, *nbrFace, *cbStart, *cbSlot, *bfc, *partner;
@@ -34,10 +36,31 @@ struct MeshView {
   const double *Sf, *magSf, *w, *dc, *V, *bSf, *bmagSf, *bw, *bdc;
   const int *ecol, *esrc;   // solver gather rows [W][C] (linsolve.hip build_ell): the face loops read them
   int W;
+  // row classes (ColView): column offsets and source codes per class [ncls][W]; a source code is
+  // 2 kslot + own (face storage kslot * C + owner cell), SCODE_PAD for padding, CEXPL: read esrc
+  const uint8_t* ecls;
+  const int *ectab, *estab;
   double rdt;
   const int* trav;          // optional traversal order of the per-cell gather kernels (thread t -> cell)
   const double *md, *bdv;   // C[nei] - C[own] [3][F] (face storage) and patch delta vectors [3][B] (limited schemes)
 };
+
+// entry k of cell c's gather row: column j and coefficient source e (2 f + own for the face at storage f,
+// -(b + 1) for boundary slot b, INT_MIN padding), from the row class cl (ecls_of) or the explicit arrays
+__device__ __forceinline__ int ecls_of(const MeshView& m, int c) { return m.ecls ? (int)m.ecls[c] : -1; }
+__device__ __forceinline__ void erow(const MeshView& m, int cl, int k, int c, int& j, int& e) {
+  const long C = m.C;
+  if (cl >= 0) {
+    const int o = m.ectab[cl * m.W + k], sc = m.estab[cl * m.W + k];
+    j = o != CEXPL ? c + o : m.ecol[k * C + c];
+    if (sc == SCODE_PAD) e = CEXPL;   // == INT_MIN, the ELL padding code
+    else if (sc != CEXPL) e = 2 * ((sc >> 1) * (int)C + ((sc & 1) ? c : j)) + (sc & 1);
+    else e = m.esrc[k * C + c];
+    return;
+  }
+  j = m.ecol[k * C + c];
+  e = m.esrc[k * C + c];
+}
 
 // interpolation / convection schemes of the terms the reference GPU path hard-wires (dfmi_set_scheme;
 // dfmi/schemes.py): div(phi,Yi_h), div(phi,K), div(hDiffCorrFlux)
@@ -192,6 +215,17 @@ struct Ctx {
     DevBuf<int8_t> bflag;        // [C] 1: the row has a processor (halo) column
     DevBuf<int> brow;            // those rows, ascending
     int nb = 0;
+    // row classes (ColView; built when the mesh has <= 255 distinct rows and owner-slot face storage;
+    // DFMI_ROW_CLASSES=0: explicit columns everywhere)
+    DevBuf<uint8_t> cls;
+    DevBuf<int> ctab, stab;
+    int ncls = 0;
+    ColView cols() const {
+      ColView v;
+      v.col = col.p; v.W = W;
+      if (ncls > 0) { v.cls = cls.p; v.tab = ctab.p; }
+      return v;
+    }
   } ell;
   bool halo_overlap = false;     // DFMI_HALO_OVERLAP=1: solver halo exchanges overlap the interior rows
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
@@ -220,6 +254,8 @@ struct Ctx {
     m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
     m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
+    m.ecls = ell.ready && ell.ncls > 0 ? ell.cls.p : nullptr;
+    m.ectab = ell.ctab.p; m.estab = ell.stab.p;
     m.rdt = rdt;
     m.trav = trav.n ? trav.p : nullptr;
     m.md = md.p; m.bdv = bdv.p;

@@ -80,10 +80,10 @@ __device__ __forceinline__ double bface(const MeshView& m, int t, const double* 
 // WT = 0: the CSR walk (nbrStart/nbrFace, ownStart), same order, any mesh.
 template <int WT, class FN> __device__ __forceinline__ void each_face(const MeshView& m, int c, FN&& fn) {
   if constexpr (WT > 0) {
-    const long C = m.C;
     int es[WT], cs[WT];
+    const int cl = ecls_of(m, c);
 #pragma unroll
-    for (int k = 0; k < WT; ++k) { es[k] = m.esrc[k * C + c]; cs[k] = m.ecol[k * C + c]; }
+    for (int k = 0; k < WT; ++k) erow(m, cl, k, c, cs[k], es[k]);
 #pragma unroll
     for (int k = 0; k < WT; ++k)
       if (es[k] >= 0) fn(es[k] >> 1, cs[k], (es[k] & 1) != 0);   // slots (< 0) and padding skipped
@@ -1133,8 +1133,9 @@ __global__ void __launch_bounds__(TPB) k_y_prep_rows(MeshView m, const int8_t* _
   if (c >= m.C) return;
   const long C = m.C, F = m.F, B = m.B;
   int es[WT], cs[WT];
+  const int cl = ecls_of(m, c);
 #pragma unroll
-  for (int k = 0; k < WT; ++k) { es[k] = m.esrc[k * C + c]; cs[k] = m.ecol[k * C + c]; }
+  for (int k = 0; k < WT; ++k) erow(m, cl, k, c, cs[k], es[k]);
   double fw[WT], f0[WT], f1[WT], f2[WT], fms[WT], fdc[WT], fan[WT];
 #pragma unroll
   for (int k = 0; k < WT; ++k) {

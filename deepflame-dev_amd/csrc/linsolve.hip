@@ -20,6 +20,7 @@
 #include "dfmi_ctx.h"
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 
 namespace dfmi {
 namespace {
@@ -114,13 +115,14 @@ template <int NV> __global__ void k_red_local(const double* partial, int nblk, d
 __device__ __forceinline__ bool leader() { return blockIdx.x == 0 && threadIdx.x == 0; }
 
 // y = dS x + sum_k val[k] x[col[k]]  (lduMatrix::Amul + updateMatrixInterfaces, same order)
-template <int WT> __device__ __forceinline__ double ell_mv(int W_, long C, const int* __restrict__ col,
+template <int WT> __device__ __forceinline__ double ell_mv(int W_, long C, const ColView& col,
                                                             const double* __restrict__ val, double d,
                                                             const double* __restrict__ xv, int c) {
   const int W = WT > 0 ? WT : W_;
+  const int* t = col.row(c);
   double y = d * xv[c];
 #pragma unroll
-  for (int k = 0; k < W; ++k) y += val[k * C + c] * xv[col[k * C + c]];
+  for (int k = 0; k < W; ++k) y += val[k * C + c] * xv[col.get(t, C, k, c)];
   return y;
 }
 
@@ -147,8 +149,10 @@ __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, co
   double* vs = val + (long)s * W * C;
   const bool wv = !(vshared && s > 0);
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
+    const int cl = ecls_of(m, c);
     for (int k = 0; wv && k < W; ++k) {
-      const int e = esrc[k * C + c];
+      int j, e;
+      erow(m, cl, k, c, j, e);
       double v;
       if (e == PAD) v = 0.0;
       else if (e >= 0) v = (e & 1) ? U[e >> 1] : L[e >> 1];
@@ -197,19 +201,20 @@ struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; int vshared; };
 constexpr int BCG_VECS = 9;
 
 // y = (A in)_c / D_c = in_c + (sum_k val in_j) / D_c
-template <int WT> __device__ __forceinline__ double scaled_mv(int W_, long C, const int* __restrict__ col,
+template <int WT> __device__ __forceinline__ double scaled_mv(int W_, long C, const ColView& col,
                                                               const double* __restrict__ val, double d,
                                                               const double* __restrict__ xv, int c) {
   const int W = WT > 0 ? WT : W_;
+  const int* t = col.row(c);
   double o = 0.0;
 #pragma unroll
-  for (int k = 0; k < W; ++k) o += val[k * C + c] * xv[col[k * C + c]];
+  for (int k = 0; k < W; ++k) o += val[k * C + c] * xv[col.get(t, C, k, c)];
   return xv[c] + o / d;
 }
 
 // r = D^-1 (b - A x); r0 = p = r; partials (||D r||^2, r0.r)
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, ColView col,
                                                   const double* __restrict__ val, BV b, double* partial) {
   const int s = blockIdx.y;
   const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
@@ -228,7 +233,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, const 
 
 // prologue: res = ||D r||, rho; convergence; v = D^-1 A p; partial r0.v
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, ColView col,
                                                    const double* __restrict__ val, int it, int max_iter, double tol,
                                                    double abs_tol, Red red, double* scal, BV b, double* partial,
                                                    RowSet rs) {
@@ -278,7 +283,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_s(long C, long Ce, Red red, double*
 // s and nothing re-reads it; halo entries (processor neighbours, j >= C) read the exchanged copy sv.
 // t = D^-1 A s; partials (t.s, t.t, r0.t, r0.s)
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, ColView col,
                                                    const double* __restrict__ val, Red red, double* scal, BV b,
                                                    double* partial, RowSet rows) {
   const int s = blockIdx.y;
@@ -297,10 +302,11 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, cons
   for_rows(C, rows, [&](int c) {
     const long i = s * Ce + c;
     const double sc = rs[c] - alpha * ws[c];
+    const int* ct = col.row(c);
     double o = 0.0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col[k * C + c];
+      const int j = col.get(ct, C, k, c);
       const double sj = j < C ? rs[j] - alpha * ws[j] : hs[j];
       o += vs[k * C + c] * sj;
     }
@@ -351,7 +357,7 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys 
 struct CV { double *dS, *rhs, *r, *z, *pa, *pb, *q, *xw; };
 
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, ColView col,
                                                  const double* __restrict__ val, CV v, double* partial) {
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
@@ -367,7 +373,7 @@ __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, const int* __res
 // prologue: rz, res, convergence, beta; p_new = z + beta p_old (own and, on the fly, neighbours);
 // q = A p_new; partial p_new.q
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __restrict__ col,
+__global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, ColView col,
                                                  const double* __restrict__ val, int it, int max_iter, double tol,
                                                  double abs_tol, Red red_rz, Red red_rr, double* scal, CV v,
                                                  const double* __restrict__ pold, double* __restrict__ pnew,
@@ -394,10 +400,11 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, const int* __res
   for_rows(C, rs, [&](int c) {
     const double pc = z[c] + beta * pold[c];
     pnew[c] = pc;
+    const int* ct = col.row(c);
     double y = v.dS[c] * pc;
 #pragma unroll
     for (int k = 0; k < Wr; ++k) {
-      const int j = col[k * C + c];
+      const int j = col.get(ct, C, k, c);
       y += val[k * C + c] * (z[j] + beta * pold[j]);
     }
     v.q[c] = y;
@@ -438,7 +445,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
 // precision T; a neighbour's r_j is re-formed as r_j - alpha q_j (the expression the update stores), so
 // x0 and res are bitwise those of k_smooth_res on the stored r. Partials (0, r.r) as k_cg_x<false>.
 template <int WT, class T>
-__global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, const int* __restrict__ col, Red red,
+__global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col, Red red,
                                                      double* scal, double* __restrict__ x, CV v,
                                                      const double* __restrict__ pnew, double* __restrict__ rnew,
                                                      double* partial, const T* __restrict__ val0,
@@ -460,9 +467,10 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, const int* 
     const T bc = (T)rr;
     const T xc = omega * bc / D0[c];
     T y = D0[c] * xc;
+    const int* ct = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col[(long)k * C + c];
+      const int j = col.get(ct, C, k, c);
       if (j < C) y += val0[(long)k * C + c] * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
     }
     x0[c] = xc;
@@ -512,7 +520,7 @@ __global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, con
   double a2[2] = {0.0, 0.0};
   for (int c = threadIdx.x; c < C; c += STPB) {
     const double d = dS[c];
-    const double res = b.rhs[s * Ce + c] - ell_mv<WT>(W, C, col, vs, d, b.xw + s * Ce, c);
+    const double res = b.rhs[s * Ce + c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, vs, d, b.xw + s * Ce, c);
     const double rr = res / d;
     r[c] = rr; r0[c] = rr; p[c] = rr;
     a2[0] += res * res;
@@ -530,7 +538,7 @@ __global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, con
     // v = D^-1 A p; r0.v
     double a1[1] = {0.0};
     for (int c = threadIdx.x; c < C; c += STPB) {
-      const double y = scaled_mv<WT>(W, C, col, vs, dS[c], p, c);
+      const double y = scaled_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, vs, dS[c], p, c);
       v[c] = y;
       a1[0] += r0[c] * y;
     }
@@ -701,7 +709,7 @@ __global__ void __launch_bounds__(STPB) k_pcg_small(long C, int W_, const int* _
   double* p = v.pa;
   double a2[2] = {0.0, 0.0};
   for (int c = threadIdx.x; c < C; c += STPB) {
-    const double rr = v.rhs[c] - ell_mv<WT>(W, C, col, val, v.dS[c], v.xw, c);
+    const double rr = v.rhs[c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, val, v.dS[c], v.xw, c);
     v.r[c] = rr;
     p[c] = 0.0;
     if (!AMG) { const double zz = rr / v.dS[c]; v.z[c] = zz; a2[0] += rr * zz; }
@@ -928,6 +936,47 @@ void build_ell(Ctx& x) {
   if (brow.empty()) brow.push_back(0);
   x.ell.bflag.upload(bflag, x.stream);
   x.ell.brow.upload(brow, x.stream);
+  // row classes: per cell the W (column offset, source code) pairs; coupled slots keep explicit sources
+  // (slot ids are not relative to the cell) and processor columns explicit columns
+  x.ell.ncls = 0;
+  const char* rc = std::getenv("DFMI_ROW_CLASSES");
+  if (x.fslot && !(rc && std::atoi(rc) == 0)) {
+    std::map<std::vector<int>, int> ids;
+    std::vector<uint8_t> cls(C);
+    std::vector<int> key(2 * W);
+    bool ok = true;
+    for (int c = 0; c < C && ok; ++c) {
+      for (int k = 0; k < W; ++k) {
+        const int j = col[(size_t)k * C + c], s = src[(size_t)k * C + c];
+        int co, sc;
+        if (s == PAD) { co = j - c; sc = SCODE_PAD; }
+        else if (s < 0) { co = j < C ? j - c : CEXPL; sc = CEXPL; }
+        else {
+          const int fs = s >> 1, own = s & 1, owner = own ? c : j;
+          const int ks = (fs - owner) / C;
+          ok = ok && (long)ks * C + owner == fs;
+          co = j - c; sc = 2 * ks + own;
+        }
+        key[k] = co; key[W + k] = sc;
+      }
+      auto it = ids.find(key);
+      if (it == ids.end()) {
+        if (ids.size() >= 255) { ok = false; break; }
+        it = ids.emplace(key, (int)ids.size()).first;
+      }
+      cls[c] = (uint8_t)it->second;
+    }
+    if (ok && C > 0) {
+      const int n = (int)ids.size();
+      std::vector<int> ctab((size_t)n * W), stab((size_t)n * W);
+      for (auto& kv : ids)
+        for (int k = 0; k < W; ++k) { ctab[(size_t)kv.second * W + k] = kv.first[k]; stab[(size_t)kv.second * W + k] = kv.first[W + k]; }
+      x.ell.cls.upload(cls, x.stream);
+      x.ell.ctab.upload(ctab, x.stream);
+      x.ell.stab.upload(stab, x.stream);
+      x.ell.ncls = n;
+    }
+  }
   DFMI_HIP(hipStreamSynchronize(x.stream));
   x.ell.ready = true;
 }
@@ -1070,7 +1119,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   }
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
-    { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, b, pR); }
+    { KScope _ks(x, "k_bcg_init"); hipLaunchKernelGGL(k_bcg_init<WT>, g, bl, 0, x.stream, C, Ce, W, x.ell.cols(), val, b, pR); }
   });
   DFMI_HIP(hipGetLastError());
   Red red = L.after(pR, 2);
@@ -1081,7 +1130,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_spmv");
-        hipLaunchKernelGGL((k_bcg_spmv1<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, it, cfg.max_iter,
+        hipLaunchKernelGGL((k_bcg_spmv1<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.cols(), val, it, cfg.max_iter,
                            cfg.tol, cfg.abs_tol, red, WS.scal.p, b, pV, rs);
       });
     });
@@ -1093,7 +1142,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_spmv");
-        hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.col.p, val, red, WS.scal.p, b, pT, rs);
+        hipLaunchKernelGGL((k_bcg_spmv2<WT>), g, bl, 0, x.stream, C, Ce, W, x.ell.cols(), val, red, WS.scal.p, b, pT, rs);
       });
     });
     const Red red_t = L.after(pT, 4, 0, np2);
@@ -1162,7 +1211,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
     KScope _ks(x, "k_cg_init");
-    hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, v, q2);
+    hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, v, q2);
   });
   DFMI_HIP(hipGetLastError());
   // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
@@ -1175,7 +1224,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       if (x.ws.red_all.n < (size_t)8 * x.nranks) x.ws.red_all.alloc((size_t)8 * x.nranks);
       double* loc = x.ws.red_local.p;
       hipLaunchKernelGGL(k_red_local<2>, dim3(1), dim3(TPB), 0, x.stream, q2, nblk, loc);
-      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, act);
+      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, act);
       hipLaunchKernelGGL(k_red_local<1>, dim3(1), dim3(TPB), 0, x.stream, q3, nblk, loc + 2);
       DFMI_HIP(hipGetLastError());
       halo_allgather(x, loc, x.ws.red_all.p, 3);
@@ -1186,7 +1235,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     Red r2 = L.after(q2, 2, 0);
     rr = r2; rr.p += 1;
     if (amg) {
-      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, act);
+      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, act);
       rz = L.after(q3, 1, 1);
     } else rz = r2;
   };
@@ -1204,7 +1253,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_cg_spmv");
-        hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.col.p, val, it, cfg.max_iter, cfg.tol,
+        hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, it, cfg.max_iter, cfg.tol,
                            cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1, rs);
       });
     });
@@ -1215,7 +1264,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_cg_x_smooth");   // its own timer name: tests assert the fused path ran
-        hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.col.p, red, WS.scal.p, xsol, v,
+        hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p, xsol, v,
                            pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
                            l0.fx.p, l0.fr.p);
       });
@@ -1223,7 +1272,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       std::swap(v.r, v.z);   // z was dead (k_cg_spmv has read it); the V-cycle writes the new z over the old r
       Red r2 = L.after(q2, 2, 0);
       red_rr = r2; red_rr.p += 1;
-      amg_apply(x, val, v.dS, x.ell.col.p, v.r, v.z, q3, nblk, WS.scal.p + 6, true);
+      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, WS.scal.p + 6, true);
       red_rz = L.after(q3, 1, 1);
       std::swap(pold, pnew);
       if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;

@@ -68,6 +68,7 @@ SIGNATURES = {
     "dfmi_solver_work": [_P, C.c_char_p, _DP, C.c_int],
     "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
     "dfmi_amg_info": [_P, C.c_int, _IP, _IP, _IP],
+    "dfmi_row_classes": [_P, _IP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
@@ -343,6 +344,12 @@ class Context:
         n = C.c_int(); cells = np.zeros(32, np.int32); w = np.zeros(32, np.int32)
         self._call("dfmi_amg_info", self.h, 32, C.byref(n), _ip(cells), _ip(w))
         return [(int(cells[i]), int(w[i])) for i in range(n.value)]
+
+    def row_classes(self):
+        """distinct gather-row classes decoded per cell (0: explicit ELL columns)"""
+        n = C.c_int()
+        self._call("dfmi_row_classes", self.h, C.byref(n))
+        return n.value
 
     def solver_stats(self, eqn):
         it = C.c_int(); r0 = C.c_double(); rel = C.c_double()

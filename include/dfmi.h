@@ -184,6 +184,11 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
 /* AMG hierarchy after the first p solve: level count, cells and ELL width per level */
 int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width);
+/* gather-row classes in use (0: explicit columns): after the first solve, the number of distinct
+ * (column offset, coefficient source) rows the solver / assembly gathers decode from one byte per cell
+ * instead of reading 2 W ints (hex boxes in blockMesh order: 27). Measurement aid (no reference
+ * counterpart; the reference's ldu_to_csr keeps explicit CSR columns, dfMatrixDataBase.cu:166-177). */
+int dfmi_row_classes(dfmi_ctx* ctx, int* n_classes);
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
 /* work done by the solves of `eqn` since the last reset: the sum over solves and systems of the
