@@ -31,11 +31,27 @@ struct Amg {
   double omega = 0.85;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
-  int l0_sweeps = 1;
-  bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)       // weighted-Jacobi sweeps before and after the coarse correction on level 0
+  int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
+  bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;
+  // Agglomerated coarsest level (several ranks; DFMI_AMG_GLOBAL=1, off by default: measured no fewer
+  // p-iterations). The rank-local hierarchies stop at
+  // coarsest / nranks cells; every rank's coarsest cells are gathered into ONE global level of ng = nranks x
+  // nmax cells (rank r's cell I at r nmax + I, padding rows with a unit diagonal) whose operator includes the
+  // couplings across processor faces (level-0 halo coefficients summed per pair of coarsest aggregates).
+  // Per solve the ranks all-gather their packed rows; per V-cycle their coarsest right-hand sides, and every
+  // rank smooths the identical global level redundantly (k_coarsest) -- the role of AmgX's consolidated
+  // coarse levels (src_gpu/AmgXSolver.cu:184-266) in place of block-Jacobi across ranks.
+  bool global = false;
+  int nmax = 0, ng = 0, wc = 0, we = 0, wg = 0, nloc = 0;
+  DevBuf<int> g_col;                      // [wg][ng] global columns
+  DevBuf<int> e_start, e_src;             // external sums: (row I, slot e) -> level-0 ELL sources k C + c
+  DevBuf<double> g_send, g_recv;          // packed rows: own nmax (wg + 1), all ng (wg + 1)
+  DevBuf<double> g_bs, g_bg;              // coarsest right-hand side: own nmax, all ng
+  DevBuf<double> g_val, g_D, g_x;         // global operator / solution in the V-cycle precision (f64 ...)
+  DevBuf<float> g_fval, g_fD, g_fx;       // (... or f32)
   // the V-cycle's launches captured once per (operands, precision) and replayed as one graph launch
   // (DFMI_AMG_GRAPH=0: direct launches); not used while kernel timers are armed
   bool use_graph = false;

@@ -70,16 +70,18 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, ColView col,
                                                     const T* __restrict__ val, const T* __restrict__ D,
                                                     const TB* __restrict__ b, T omega,
                                                     T* __restrict__ x, T* __restrict__ r, const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= n || (act && *act == 0.0)) return;
   const T bc = (T)b[c];
   const T xc = omega * bc / D[c];
   T y = D[c] * xc;
-const int* ct = col.row(c);
+  const int rb = col.row(c);
 #pragma unroll
   for (int k = 0; k < W; ++k) {
-    const int j = col.get(ct, n, k, c);
+    const int j = col.get(s_ct, rb, n, k, c);
     if (j < n) y += val[(long)k * n + c] * (omega * (T)b[j] / D[j]);
   }
   x[c] = xc;
@@ -120,16 +122,18 @@ __global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, ColView col,
                                                      const T* __restrict__ val, const T* __restrict__ D,
                                                      const T* __restrict__ r, T omega, T* __restrict__ x,
                                                      T* __restrict__ rn, const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= n || (act && *act == 0.0)) return;
   const T rc = r[c];
   const T dc = omega * rc / D[c];
   T y = D[c] * dc;
-const int* ct = col.row(c);
+  const int rb = col.row(c);
 #pragma unroll
   for (int k = 0; k < W; ++k) {
-    const int j = col.get(ct, n, k, c);
+    const int j = col.get(s_ct, rb, n, k, c);
     if (j < n) y += val[(long)k * n + c] * (omega * r[j] / D[j]);
   }
   x[c] += dc;
@@ -142,6 +146,8 @@ __global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, ColView col
                                                       const T* __restrict__ val, const T* __restrict__ D,
                                                       const TB* __restrict__ b, const TO* __restrict__ in, T omega,
                                                       TO* __restrict__ out, double* partial, const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   if (act && *act == 0.0) return;
   __shared__ double sh[TPB / 64];
@@ -149,10 +155,10 @@ __global__ void __launch_bounds__(TPB) k_jacobi_sweep(int n, int W_, ColView col
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = (T)in[c];
     T ay = D[c] * yc;
-const int* ct = col.row(c);
+  const int rb = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col.get(ct, n, k, c);
+      const int j = col.get(s_ct, rb, n, k, c);
       if (j < n) ay += val[(long)k * n + c] * (T)in[j];
     }
     const TB bc = b[c];
@@ -217,6 +223,8 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, ColView c
                                                         const int* __restrict__ agg, const T* __restrict__ xc,
                                                         T omega, T sc, TO* __restrict__ out, double* partial,
                                                         const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   if (act && *act == 0.0) return;   // uniform: no barrier below is reached by part of the block
   __shared__ double sh[TPB / 64];
@@ -224,10 +232,10 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, ColView c
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = x[c] + sc * xc[agg[c]];
     T ay = D[c] * yc;
-const int* ct = col.row(c);
+  const int rb = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col.get(ct, n, k, c);
+      const int j = col.get(s_ct, rb, n, k, c);
       if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
     }
     const TB bc = b[c];
@@ -291,6 +299,42 @@ __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __re
     T* t = cur; cur = nxt; nxt = t;
   }
   for (int c = threadIdx.x; c < n; c += CTPB) x[c] = (TO)cur[c];
+}
+
+// ---------------------------------------------------------------- agglomerated coarsest level (Amg::global)
+// rank's packed rows (nmax rows of wg values + the diagonal): local coarsest couplings (slots < wloc of the
+// level's own ELL; up to wc), the external couplings summed in double from the level-0 halo coefficients
+// in their listed order (slots wc .. wc + we), the diagonal; padding rows (I >= nloc) are a unit diagonal
+template <class T>
+__global__ void k_gc_pack(int nmax, int nloc, int wloc, int wc, int we, const T* __restrict__ valc,
+                          const T* __restrict__ Dc, const double* __restrict__ val0, const int* __restrict__ estart,
+                          const int* __restrict__ esrc, double* __restrict__ send) {
+  const int I = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I >= nmax) return;
+  const int wg = wc + we;
+  double* o = send + (long)I * (wg + 1);
+  for (int k = 0; k < wc; ++k) o[k] = (I < nloc && k < wloc) ? (double)valc[(long)k * nloc + I] : 0.0;
+  for (int e = 0; e < we; ++e) {
+    double s = 0.0;
+    for (int q = estart[I * we + e]; q < estart[I * we + e + 1]; ++q) s += val0[esrc[q]];
+    o[wc + e] = s;
+  }
+  o[wg] = I < nloc ? (double)Dc[I] : 1.0;
+}
+// every rank unpacks the gathered rows identically: global row G = r nmax + I
+template <class T>
+__global__ void k_gc_unpack(int ng, int nmax, int wg, const double* __restrict__ recv, T* __restrict__ val,
+                            T* __restrict__ D) {
+  const int G = blockIdx.x * blockDim.x + threadIdx.x;
+  if (G >= ng) return;
+  const double* s = recv + (long)(G / nmax) * nmax * (wg + 1) + (long)(G % nmax) * (wg + 1);
+  for (int k = 0; k < wg; ++k) val[(long)k * ng + G] = (T)s[k];
+  D[G] = (T)s[wg];
+}
+template <class T>
+__global__ void k_gc_bpack(int nmax, int nloc, const T* __restrict__ b, double* __restrict__ out) {
+  const int I = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I < nmax) out[I] = I < nloc ? (double)b[I] : 0.0;
 }
 
 // ---------------------------------------------------------------- coarse levels in one launch
@@ -421,7 +465,10 @@ double env_d(const char* k, double d) { const char* v = std::getenv(k); return v
 // level is then a sum over 8 adjacent lanes inside the smoothing kernel (k_smooth_res_r8), so levels
 // 1 .. L-2 need one launch on the way down instead of two. Level 0 keeps the mesh order. Member order
 // inside an aggregate is unchanged, so every restriction sums the same values in the same order.
-void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vector<int>>& aggs) {
+// On return fin_aggs / last_col hold the final fine -> coarse maps and the coarsest level's columns (they
+// are left untouched when the levels stay plain).
+void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vector<int>>& aggs,
+                std::vector<std::vector<int>>& fin_aggs, std::vector<int>& last_col) {
   Amg& a = x.amg;
   const int L = (int)a.lv.size();
   if (L < 3) return;
@@ -462,11 +509,119 @@ void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vec
     c.W = r.Wc;
     c.col.upload(r.ccol, x.stream);
     fcol.swap(r.ccol);
+    fin_aggs[l] = r.agg;
     Wf = c.W;
     nf = c.n;
   }
+  last_col = fcol;
   DFMI_HIP(hipStreamSynchronize(x.stream));
   a.padded = true;
+}
+
+// Amg::global (amg.h): the agglomerated coarsest level. Collective: every rank calls it in its first
+// pressure solve. col0: level-0 ELL columns [W][C] (>= C: halo entries); aggs: fine -> coarse maps of the
+// final levels; lcol: the local coarsest level's columns.
+void global_setup(Ctx& x, const std::vector<int>& col0, const std::vector<std::vector<int>>& aggs,
+                  const std::vector<int>& lcol) {
+  Amg& a = x.amg;
+  a.global = false;
+  const int L = (int)a.lv.size();
+  const int C = x.C, W0 = x.ell.W, H = x.H, R = x.nranks;
+  const int nloc = a.lv[L - 1].n, wloc = a.lv[L - 1].W;
+  // collective size agreement: (levels, coarsest cells, coarsest width) of every rank
+  auto gather = [&](const std::vector<double>& mine) {
+    const long n = (long)mine.size();
+    DevBuf<double> sb, rb;
+    sb.upload(mine, x.stream);
+    rb.alloc((size_t)n * R);
+    halo_allgather(x, sb.p, rb.p, n);
+    std::vector<double> all((size_t)n * R);
+    DFMI_HIP(hipMemcpyAsync(all.data(), rb.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    return all;
+  };
+  int nmax = 0, wc = 0, we = 0;
+  {
+    const std::vector<double> all = gather({(double)L, (double)nloc, (double)wloc});
+    for (int r = 0; r < R; ++r) {
+      if (all[3 * r] < 2) return;   // a rank without coarse levels: block-Jacobi everywhere
+      nmax = std::max(nmax, (int)all[3 * r + 1]); wc = std::max(wc, (int)all[3 * r + 2]);
+    }
+  }
+  // coarsest-level aggregate of every fine cell, and of the cell across every processor face
+  std::vector<int> cid(C);
+  for (int c = 0; c < C; ++c) {
+    int v = c;
+    for (int l = 0; l + 1 < L; ++l) v = aggs[l][v];
+    cid[c] = v;
+  }
+  std::vector<double> ids((size_t)C + H, -1.0);
+  for (int c = 0; c < C; ++c) ids[c] = cid[c];
+  DevBuf<double> dids;
+  dids.upload(ids, x.stream);
+  HaloItem it{dids.p, dids.p, 1, (long)C + H, (long)C + H, false};
+  halo_update(x, &it, 1);
+  DFMI_HIP(hipMemcpyAsync(ids.data(), dids.p, ids.size() * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  std::vector<int> hpeer(H, -1);
+  for (int p = 0; p < x.P; ++p) {
+    if (x.pkind[p] != 2) continue;
+    for (int i = 0; i < x.psize[p]; ++i) {
+      const int h = x.h_hidx[x.poff[p] + i];
+      if (h >= 0) hpeer[h] = x.peer[p];
+    }
+  }
+  // external couplings of each local coarsest row: (peer, peer's coarsest id) -> level-0 ELL sources k C + c
+  std::vector<std::map<std::pair<int, int>, std::vector<int>>> ext(nloc);
+  for (int c = 0; c < C; ++c)
+    for (int k = 0; k < W0; ++k) {
+      const int j = col0[(size_t)k * C + c];
+      if (j < C) continue;
+      const int h = j - C;
+      DFMI_CHECK(hpeer[h] >= 0 && ids[j] >= 0, "AMG: processor face without a peer aggregate");
+      ext[cid[c]][{hpeer[h], (int)ids[j]}].push_back(k * C + c);
+    }
+  int wext = 0;
+  for (auto& e : ext) wext = std::max(wext, (int)e.size());
+  {
+    const std::vector<double> all = gather({(double)wext});
+    for (int r = 0; r < R; ++r) we = std::max(we, (int)all[r]);
+  }
+  const int ng = R * nmax, wg = wc + we;
+  if (ng > COARSEST || (size_t)ng * wg > LDS_ENT) return;   // the same decision on every rank
+  // external sum lists per (row, slot), ordered by global column
+  std::vector<int> es(1, 0), esrc;
+  std::vector<double> pc((size_t)nmax * wg);
+  const int G0 = x.rank * nmax;
+  for (int I = 0; I < nmax; ++I) {
+    for (int k = 0; k < wc; ++k) pc[(size_t)I * wg + k] = G0 + ((I < nloc && k < wloc) ? lcol[(size_t)k * nloc + I] : I);
+    int e = 0;
+    if (I < nloc)
+      for (auto& kv : ext[I]) {   // (peer, id) ascending = global column ascending
+        pc[(size_t)I * wg + wc + e] = kv.first.first * nmax + kv.first.second;
+        for (int q : kv.second) esrc.push_back(q);
+        es.push_back((int)esrc.size());
+        ++e;
+      }
+    for (; e < we; ++e) { pc[(size_t)I * wg + wc + e] = G0 + I; es.push_back((int)esrc.size()); }
+  }
+  if (esrc.empty()) esrc.push_back(0);
+  const std::vector<double> allc = gather(pc);
+  std::vector<int> gcol((size_t)wg * ng);
+  for (int G = 0; G < ng; ++G)
+    for (int k = 0; k < wg; ++k) gcol[(size_t)k * ng + G] = (int)allc[(size_t)G * wg + k];
+  a.g_col.upload(gcol, x.stream);
+  a.e_start.upload(es, x.stream);
+  a.e_src.upload(esrc, x.stream);
+  a.g_send.alloc((size_t)nmax * (wg + 1));
+  a.g_recv.alloc((size_t)ng * (wg + 1));
+  a.g_bs.alloc(nmax);
+  a.g_bg.alloc(ng);
+  if (a.fp32) { a.g_fval.alloc((size_t)wg * ng); a.g_fD.alloc(ng); a.g_fx.alloc(ng); }
+  else { a.g_val.alloc((size_t)wg * ng); a.g_D.alloc(ng); a.g_x.alloc(ng); }
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  a.nmax = nmax; a.ng = ng; a.wc = wc; a.we = we; a.wg = wg; a.nloc = nloc;
+  a.global = true;
 }
 
 }  // namespace
@@ -533,7 +688,11 @@ void amg_setup(Ctx& x) {
   a.lv[0].W = x.ell.W;
   std::vector<int> fcol = col;
   std::vector<std::vector<int>> aggs;   // host copies of each level's fine -> coarse map
-  auto too_big = [&](const AmgLevel& l) { return l.n > a.coarsest || (size_t)l.n * l.W > 6144; };
+  // several ranks: the rank-local levels stop at coarsest / nranks cells, below them the agglomerated level
+  const bool want_global = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_GLOBAL", 0) != 0 && !a.use_graph &&
+                           a.coop_blocks == 0;
+  const int cap = want_global ? std::max(8, a.coarsest / x.nranks) : a.coarsest;
+  auto too_big = [&](const AmgLevel& l) { return l.n > cap || (size_t)l.n * l.W > 6144; };
   while (too_big(a.lv.back())) {
     AmgLevel c;
     std::vector<int> ccol;
@@ -550,7 +709,10 @@ void amg_setup(Ctx& x) {
   }
   DFMI_CHECK(!too_big(a.lv.back()) || a.lv.back().n <= 8, "AMG coarsening stalled above the coarsest-level capacity");
   a.padded = false;
-  if (env_d("DFMI_AMG_PADDED", 1) != 0) pad_levels(x, col, aggs);
+  a.global = false;
+  std::vector<std::vector<int>> fin_aggs = aggs;
+  std::vector<int> last_col = fcol;
+  if (env_d("DFMI_AMG_PADDED", 1) != 0) pad_levels(x, col, aggs, fin_aggs, last_col);
   if (a.lv.size() == 1) a.fp32 = false;   // a single level writes z directly: keep it in double
   for (size_t l = 0; l < a.lv.size(); ++l) {
     AmgLevel& v = a.lv[l];
@@ -567,6 +729,7 @@ void amg_setup(Ctx& x) {
     }
     if (l == 0 && a.l0_sweeps > 1) v.zt.alloc(nv);
   }
+  if (want_global) global_setup(x, col, fin_aggs, last_col);
   a.ready = true;
 }
 
@@ -594,6 +757,26 @@ void amg_galerkin(Ctx& x, const double* val0, const double* D0) {
     else
       hipLaunchKernelGGL((k_galerkin<float, float>), g, dim3(TPB), 0, x.stream, c.n, c.W + 1, f.gstart.p, f.gsrc.p,
                          (const float*)f.fval.p, (const float*)f.fD.p, c.fval.p, c.fD.p);
+    DFMI_HIP(hipGetLastError());
+  }
+  if (a.global) {   // the agglomerated level: pack this rank's rows, all-gather, unpack (identical on every rank)
+    AmgLevel& c = a.lv.back();
+    KScope _ks(x, "k_gc_pack");
+    const dim3 gp(blocks_for(a.nmax, TPB)), gu(blocks_for(a.ng, TPB));
+    if (a.fp32)
+      hipLaunchKernelGGL(k_gc_pack<float>, gp, dim3(TPB), 0, x.stream, a.nmax, a.nloc, c.W, a.wc, a.we,
+                         (const float*)c.fval.p, (const float*)c.fD.p, val0, a.e_start.p, a.e_src.p, a.g_send.p);
+    else
+      hipLaunchKernelGGL(k_gc_pack<double>, gp, dim3(TPB), 0, x.stream, a.nmax, a.nloc, c.W, a.wc, a.we,
+                         (const double*)c.val.p, (const double*)c.D.p, val0, a.e_start.p, a.e_src.p, a.g_send.p);
+    DFMI_HIP(hipGetLastError());
+    halo_allgather(x, a.g_send.p, a.g_recv.p, (long)a.nmax * (a.wg + 1));
+    if (a.fp32)
+      hipLaunchKernelGGL(k_gc_unpack<float>, gu, dim3(TPB), 0, x.stream, a.ng, a.nmax, a.wg, (const double*)a.g_recv.p,
+                         a.g_fval.p, a.g_fD.p);
+    else
+      hipLaunchKernelGGL(k_gc_unpack<double>, gu, dim3(TPB), 0, x.stream, a.ng, a.nmax, a.wg, (const double*)a.g_recv.p,
+                         a.g_val.p, a.g_D.p);
     DFMI_HIP(hipGetLastError());
   }
 }
@@ -711,8 +894,22 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
                          f.mstart.p, f.members.p, (const T*)rcur, BV(l + 1), act);
     }
   }
-  // coarsest
-  {
+  // coarsest: the agglomerated level (every rank's coarsest right-hand sides gathered, the global level
+  // smoothed redundantly), or this rank's own coarsest level
+  T* gx = nullptr;
+  if constexpr (F) gx = a.g_fx.p; else gx = a.g_x.p;
+  if (a.global && L > 1) {
+    KScope _ks(x, "k_coarsest");
+    hipLaunchKernelGGL(k_gc_bpack<T>, dim3(blocks_for(a.nmax, TPB)), dim3(TPB), 0, x.stream, a.nmax, a.nloc,
+                       (const T*)BV(L - 1), a.g_bs.p);
+    DFMI_HIP(hipGetLastError());
+    halo_allgather(x, a.g_bs.p, a.g_bg.p, a.nmax);
+    const T* gv;
+    const T* gd;
+    if constexpr (F) { gv = a.g_fval.p; gd = a.g_fD.p; } else { gv = a.g_val.p; gd = a.g_D.p; }
+    hipLaunchKernelGGL((k_coarsest<T, double, T>), dim3(1), dim3(CTPB), 0, x.stream, a.ng, a.wg, (const int*)a.g_col.p,
+                       gv, gd, (const double*)a.g_bg.p, om, a.coarse_sweeps, gx, act);
+  } else {
     AmgLevel& c = a.lv[L - 1];
     KScope _ks(x, "k_coarsest");
     if (L > 1)
@@ -722,6 +919,8 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
       hipLaunchKernelGGL((k_coarsest<double, double, double>), dim3(1), dim3(CTPB), 0, x.stream, c.n, c.W, col0.col, val0,
                          D0, r, om, a.coarse_sweeps, z, act);
   }
+  // the coarse correction the level above the coarsest prolongates: this rank's rows of the global solution
+  auto XC = [&](int l) -> const T* { return (a.global && l + 1 == L - 1) ? gx + (long)x.rank * a.nmax : XV(l + 1); };
   if (L == 1) {
     KScope _ks(x, "k_dot_partial");
     hipLaunchKernelGGL(k_dot_partial, dim3(nblk), dim3(TPB), 0, x.stream, x.C, r, (const double*)z, partial);
@@ -735,7 +934,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
       const int ns = a.l0_sweeps;
       auto outk = [&](int k) { return ((ns - k) % 2 == 0) ? z : f.zt.p; };   // k = 1 .. ns
       launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
-               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, (const T*)XV(1), om, sc,
+               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, XC(0), om, sc,
                outk(1), ns == 1 ? partial : (double*)nullptr, act);
       for (int k = 2; k <= ns; ++k) {
         KScope _ks2(x, "k_jacobi_sweep");
@@ -746,7 +945,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     } else {
       launch_w(f.W, dim3(blocks_for(f.n, TPB)), x.stream, k_prolong_smooth<0, T, T, T>, k_prolong_smooth<6, T, T, T>,
                f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), (const T*)XV(l), (const int*)f.agg.p,
-               (const T*)XV(l + 1), om, sc, XO(l), (double*)nullptr, act);
+               XC(l), om, sc, XO(l), (double*)nullptr, act);
       // the corrected x of this level feeds the next finer prolongation
       if constexpr (F) std::swap(f.fx, f.fxo); else std::swap(f.x, f.xo);
     }

@@ -834,6 +834,10 @@ int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int*
     const Amg& a = ctx->x.amg;
     *n_levels = (int)a.lv.size();
     for (int l = 0; l < (int)a.lv.size() && l < max_levels; ++l) { cells[l] = a.lv[l].n; width[l] = a.lv[l].W; }
+    if (a.global && (int)a.lv.size() < max_levels) {   // the agglomerated level, listed last
+      cells[a.lv.size()] = a.ng; width[a.lv.size()] = a.wg;
+      *n_levels += 1;
+    }
   });
 }
 

@@ -99,15 +99,25 @@ inline int blocks_for(long n, int tpb) { return (int)((n + tpb - 1) / tpb); }
 // offsets j - c; an entry the table cannot express (a processor halo column) is read from the explicit
 // array. A gather then reads 1 B per cell instead of 4 W B (24 B on hex meshes). cls == nullptr: explicit.
 constexpr int CEXPL = -2147483647 - 1;   // class-table entry: read the explicit array
+constexpr int CT_MAX = 1536;              // class-table entries (ncls x W) a kernel stages in LDS
 struct ColView {
   const int* col = nullptr;         // explicit [W][C]
   const uint8_t* cls = nullptr;     // [C] row class, or nullptr
   const int* tab = nullptr;         // [ncls][W] column offsets
   int W = 0;
-  __device__ __forceinline__ const int* row(int c) const { return cls ? tab + (int)cls[c] * W : nullptr; }
-  __device__ __forceinline__ int get(const int* t, long C, int k, int c) const {
-    if (t) {
-      const int o = t[k];
+  int ntab = 0;                     // ncls * W <= CT_MAX
+  // every thread of the block, before any divergent exit: the class table into LDS (sh: CT_MAX ints)
+  __device__ __forceinline__ void stage(int* sh) const {
+    if (cls) {
+      for (int i = threadIdx.x; i < ntab; i += blockDim.x) sh[i] = tab[i];
+      __syncthreads();
+    }
+  }
+  // the row's offset into the staged table (-1: explicit columns)
+  __device__ __forceinline__ int row(int c) const { return cls ? (int)cls[c] * W : -1; }
+  __device__ __forceinline__ int get(const int* sh, int rb, long C, int k, int c) const {
+    if (rb >= 0) {
+      const int o = sh[rb + k];
       if (o != CEXPL) return c + o;
     }
     return col[k * C + c];

@@ -220,10 +220,11 @@ struct Ctx {
     DevBuf<uint8_t> cls;
     DevBuf<int> ctab, stab;
     int ncls = 0;
+    bool fv_classes = false;
     ColView cols() const {
       ColView v;
       v.col = col.p; v.W = W;
-      if (ncls > 0) { v.cls = cls.p; v.tab = ctab.p; }
+      if (ncls > 0) { v.cls = cls.p; v.tab = ctab.p; v.ntab = ncls * W; }
       return v;
     }
   } ell;
@@ -254,7 +255,9 @@ struct Ctx {
     m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
     m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
-    m.ecls = ell.ready && ell.ncls > 0 ? ell.cls.p : nullptr;
+    // the assembly face loops and the ELL fold read explicit rows unless DFMI_ROW_CLASSES_FV=1 (their class
+    // lookups go through the global table: measured slower for these latency-bound gathers)
+    m.ecls = ell.ready && ell.ncls > 0 && ell.fv_classes ? ell.cls.p : nullptr;
     m.ectab = ell.ctab.p; m.estab = ell.stab.p;
     m.rdt = rdt;
     m.trav = trav.n ? trav.p : nullptr;

@@ -115,14 +115,14 @@ template <int NV> __global__ void k_red_local(const double* partial, int nblk, d
 __device__ __forceinline__ bool leader() { return blockIdx.x == 0 && threadIdx.x == 0; }
 
 // y = dS x + sum_k val[k] x[col[k]]  (lduMatrix::Amul + updateMatrixInterfaces, same order)
-template <int WT> __device__ __forceinline__ double ell_mv(int W_, long C, const ColView& col,
+template <int WT> __device__ __forceinline__ double ell_mv(int W_, long C, const ColView& col, const int* sh,
                                                             const double* __restrict__ val, double d,
                                                             const double* __restrict__ xv, int c) {
   const int W = WT > 0 ? WT : W_;
-  const int* t = col.row(c);
+  const int rb = col.row(c);
   double y = d * xv[c];
 #pragma unroll
-  for (int k = 0; k < W; ++k) y += val[k * C + c] * xv[col.get(t, C, k, c)];
+  for (int k = 0; k < W; ++k) y += val[k * C + c] * xv[col.get(sh, rb, C, k, c)];
   return y;
 }
 
@@ -201,14 +201,14 @@ struct BV { double *dS, *rhs, *r, *r0, *p, *v, *sv, *t, *xw; int vshared; };
 constexpr int BCG_VECS = 9;
 
 // y = (A in)_c / D_c = in_c + (sum_k val in_j) / D_c
-template <int WT> __device__ __forceinline__ double scaled_mv(int W_, long C, const ColView& col,
+template <int WT> __device__ __forceinline__ double scaled_mv(int W_, long C, const ColView& col, const int* sh,
                                                               const double* __restrict__ val, double d,
                                                               const double* __restrict__ xv, int c) {
   const int W = WT > 0 ? WT : W_;
-  const int* t = col.row(c);
+  const int rb = col.row(c);
   double o = 0.0;
 #pragma unroll
-  for (int k = 0; k < W; ++k) o += val[k * C + c] * xv[col.get(t, C, k, c)];
+  for (int k = 0; k < W; ++k) o += val[k * C + c] * xv[col.get(sh, rb, C, k, c)];
   return xv[c] + o / d;
 }
 
@@ -218,11 +218,13 @@ __global__ void __launch_bounds__(TPB) k_bcg_init(long C, long Ce, int W, ColVie
                                                   const double* __restrict__ val, BV b, double* partial) {
   const int s = blockIdx.y;
   const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     const long i = s * Ce + c;
     const double d = b.dS[i];
-    const double res = b.rhs[i] - ell_mv<WT>(W, C, col, vs, d, b.xw + s * Ce, c);
+    const double res = b.rhs[i] - ell_mv<WT>(W, C, col, s_ct, vs, d, b.xw + s * Ce, c);
     const double rr = res / d;
     b.r[i] = rr; b.r0[i] = rr; b.p[i] = rr;
     acc[0] += res * res;
@@ -254,10 +256,12 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv1(long C, long Ce, int W, ColVi
   }
   if (stop) return;
   const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[1] = {0.0};
   for_rows(C, rs, [&](int c) {
     const long i = s * Ce + c;
-    const double y = scaled_mv<WT>(W, C, col, vs, b.dS[i], b.p + s * Ce, c);
+    const double y = scaled_mv<WT>(W, C, col, s_ct, vs, b.dS[i], b.p + s * Ce, c);
     b.v[i] = y;
     acc[0] += b.r0[i] * y;
   });
@@ -298,15 +302,17 @@ __global__ void __launch_bounds__(TPB) k_bcg_spmv2(long C, long Ce, int W_, ColV
   const double* rs = b.r + s * Ce;
   const double* ws = b.v + s * Ce;
   const double* hs = b.sv + s * Ce;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for_rows(C, rows, [&](int c) {
     const long i = s * Ce + c;
     const double sc = rs[c] - alpha * ws[c];
-    const int* ct = col.row(c);
+    const int rb = col.row(c);
     double o = 0.0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col.get(ct, C, k, c);
+      const int j = col.get(s_ct, rb, C, k, c);
       const double sj = j < C ? rs[j] - alpha * ws[j] : hs[j];
       o += vs[k * C + c] * sj;
     }
@@ -359,9 +365,11 @@ struct CV { double *dS, *rhs, *r, *z, *pa, *pb, *q, *xw; };
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, ColView col,
                                                  const double* __restrict__ val, CV v, double* partial) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const double ax = ell_mv<WT>(W, C, col, val, v.dS[c], v.xw, c);
+    const double ax = ell_mv<WT>(W, C, col, s_ct, val, v.dS[c], v.xw, c);
     const double rr = v.rhs[c] - ax;
     const double zz = rr / v.dS[c];
     v.r[c] = rr; v.z[c] = zz; v.pa[c] = 0.0; v.pb[c] = 0.0;
@@ -396,15 +404,17 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, ColView col,
   const double beta = it == 0 ? 0.0 : rz / rzp;
   const double* z = v.z;
   const int Wr = WT > 0 ? WT : W;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[1] = {0.0};
   for_rows(C, rs, [&](int c) {
     const double pc = z[c] + beta * pold[c];
     pnew[c] = pc;
-    const int* ct = col.row(c);
+    const int rb = col.row(c);
     double y = v.dS[c] * pc;
 #pragma unroll
     for (int k = 0; k < Wr; ++k) {
-      const int j = col.get(ct, C, k, c);
+      const int j = col.get(s_ct, rb, C, k, c);
       y += val[k * C + c] * (z[j] + beta * pold[j]);
     }
     v.q[c] = y;
@@ -458,6 +468,8 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
   const double alpha = pv[0] != 0.0 ? rz / pv[0] : 0.0;
   if (leader()) { scal[2] = alpha; scal[1] = rz; }
   const int W = WT > 0 ? WT : W_;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
@@ -467,10 +479,10 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
     const T bc = (T)rr;
     const T xc = omega * bc / D0[c];
     T y = D0[c] * xc;
-    const int* ct = col.row(c);
+    const int rb = col.row(c);
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const int j = col.get(ct, C, k, c);
+      const int j = col.get(s_ct, rb, C, k, c);
       if (j < C) y += val0[(long)k * C + c] * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
     }
     x0[c] = xc;
@@ -520,7 +532,7 @@ __global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, con
   double a2[2] = {0.0, 0.0};
   for (int c = threadIdx.x; c < C; c += STPB) {
     const double d = dS[c];
-    const double res = b.rhs[s * Ce + c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, vs, d, b.xw + s * Ce, c);
+    const double res = b.rhs[s * Ce + c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, nullptr, vs, d, b.xw + s * Ce, c);
     const double rr = res / d;
     r[c] = rr; r0[c] = rr; p[c] = rr;
     a2[0] += res * res;
@@ -538,7 +550,7 @@ __global__ void __launch_bounds__(STPB) k_bcg_small(long C, long Ce, int W_, con
     // v = D^-1 A p; r0.v
     double a1[1] = {0.0};
     for (int c = threadIdx.x; c < C; c += STPB) {
-      const double y = scaled_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, vs, dS[c], p, c);
+      const double y = scaled_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, nullptr, vs, dS[c], p, c);
       v[c] = y;
       a1[0] += r0[c] * y;
     }
@@ -709,7 +721,7 @@ __global__ void __launch_bounds__(STPB) k_pcg_small(long C, int W_, const int* _
   double* p = v.pa;
   double a2[2] = {0.0, 0.0};
   for (int c = threadIdx.x; c < C; c += STPB) {
-    const double rr = v.rhs[c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, val, v.dS[c], v.xw, c);
+    const double rr = v.rhs[c] - ell_mv<WT>(W, C, ColView{col, nullptr, nullptr, W}, nullptr, val, v.dS[c], v.xw, c);
     v.r[c] = rr;
     p[c] = 0.0;
     if (!AMG) { const double zz = rr / v.dS[c]; v.z[c] = zz; a2[0] += rr * zz; }
@@ -939,6 +951,10 @@ void build_ell(Ctx& x) {
   // row classes: per cell the W (column offset, source code) pairs; coupled slots keep explicit sources
   // (slot ids are not relative to the cell) and processor columns explicit columns
   x.ell.ncls = 0;
+  {
+    const char* fv = std::getenv("DFMI_ROW_CLASSES_FV");
+    x.ell.fv_classes = fv && std::atoi(fv) != 0;
+  }
   const char* rc = std::getenv("DFMI_ROW_CLASSES");
   if (x.fslot && !(rc && std::atoi(rc) == 0)) {
     std::map<std::vector<int>, int> ids;
@@ -966,7 +982,7 @@ void build_ell(Ctx& x) {
       }
       cls[c] = (uint8_t)it->second;
     }
-    if (ok && C > 0) {
+    if (ok && C > 0 && (long)ids.size() * W <= CT_MAX) {
       const int n = (int)ids.size();
       std::vector<int> ctab((size_t)n * W), stab((size_t)n * W);
       for (auto& kv : ids)

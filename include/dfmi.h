@@ -182,7 +182,8 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
 /* preconditioner: "jacobi" (all) or "amg" (p; aggregation AMG V-cycle, the amgxpOptions
  * AGGREGATION solver's role) -- p defaults to "amg", U/Y/E to "jacobi" */
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
-/* AMG hierarchy after the first p solve: level count, cells and ELL width per level */
+/* AMG hierarchy after the first p solve: level count, cells and ELL width per level (with several ranks
+ * and DFMI_AMG_GLOBAL=1 the agglomerated coarsest level of all ranks is listed last) */
 int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width);
 /* gather-row classes in use (0: explicit columns): after the first solve, the number of distinct
  * (column offset, coefficient source) rows the solver / assembly gathers decode from one byte per cell
