@@ -1051,6 +1051,12 @@ int dfmi_row_classes(dfmi_ctx*, int* n) {   // explicit CSR rows on the CPU
   if (n) *n = 0;
   return 0;
 }
+int dfmi_hex_dims(dfmi_ctx*, int* nx, int* ny, int* nz) {
+  if (nx) *nx = 0;
+  if (ny) *ny = 0;
+  if (nz) *nz = 0;
+  return 0;
+}
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel) {
   return guard([&] {
     auto it = ctx->x.stats.find(eqn);

@@ -36,7 +36,7 @@ MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species 
 
 
 def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None, W: int = 6,
-                      classes: bool = False) -> float:
+                      classes: bool = False, hex_walk: bool = False) -> float:
     """Bytes one unit of a kernel's work must move at minimum: every input element read once and every
     output element written once (fp64 values, int32 indices, int8 slot types), shared face/cell arrays
     counted ONCE per launch however many species use them. Units: one launch for the assembly/thermo
@@ -44,12 +44,13 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
     one active system. Bc = coupled boundary slots (cyclic / processor), W = solver row width.
     Gather topology of the cell-centric kernels: 12 B per cell (nbrStart, ownStart, cbStart) + 12 B per
     face (nbrFace, own, nei) + 9 B per coupled slot (cbSlot, partner, type). DESIGN.md 5 lists them.
-    classes: the gather rows are decoded from row classes (dfmi_row_classes > 0: 1 B per cell, cbStart for
-    the boundary slots), so the per-face index bytes are not read -- topology 5 B per cell + 9 B per coupled
-    slot, and the solver matrices' 8 B of owner/neighbour ids per face become 1 B per cell."""
+    classes: the solver rows are decoded from row classes (dfmi_row_classes > 0), so the solver matrices'
+    8 B of owner/neighbour ids per face become 1 B per cell. hex_walk: the assembly kernels compute their
+    face and neighbour indices (dfmi_hex_dims), so only cbStart (4 B per cell) and the coupled slots'
+    9 B remain of the topology."""
     Sa = S - 1                                     # solved species (inert excluded)
     Bc = B if Bc is None else Bc
-    topo = (5.0 * C + 9.0 * Bc) if classes else (12.0 * C + 12.0 * F + 9.0 * Bc)
+    topo = (4.0 * C + 9.0 * Bc) if hex_walk else (12.0 * C + 12.0 * F + 9.0 * Bc)
     mat = (C * 1.0 + F * 16.0) if classes else F * 24.0   # solver matrix per SpMV (values + indices)
     if kernel == "k_y_prep":
         # Y, hai, rhoD (S each), alpha, V in; sumYDiffError, hDiffCorrFlux (3 each), diffAlphaD out;
@@ -592,6 +593,8 @@ def main():
             ctx.set_scheme(term, sch)
 
     ncls = ctx.row_classes()
+    hexd = ctx.hex_dims()
+    hexw = hexd[0] > 0 and os.environ.get("DFMI_FACE_HEX", "1") != "0"
     cells_total = m.n_cells * world
     value = cells_total * args.steps / el
     # HBM bytes per launch from the PMC passes committed under profiles/ (scripts/pmc_traffic.sh +
@@ -621,7 +624,8 @@ def main():
         ms, nl = ktime[k]
         if not nl or ms <= 0:
             continue
-        per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc, classes=ncls > 0)
+        per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc, classes=ncls > 0,
+                                     hex_walk=hexw)
         total_bytes = per_unit * units[k]
         if k == "k_bcg_spmv":   # U's three components share one operator: its bytes count once per three systems
             total_bytes -= 2.0 * work["U"] * (2.0 / 3.0) * ((1.0 * m.n_cells + 16.0 * m.n_faces if ncls > 0 else
@@ -683,6 +687,7 @@ def main():
                                               + 12.0 * m.n_coupled_slots},
         "amg_levels": ctx.amg_info(),
         "row_classes": ncls,
+        "hex_face_walk": list(hexd) if hexw else None,
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
                        "k_chem_ms_per_step": chem_ms / max(chem_n, 1),

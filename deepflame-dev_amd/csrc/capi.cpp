@@ -845,6 +845,13 @@ int dfmi_row_classes(dfmi_ctx* ctx, int* n) {
   return guard([&] { *n = ctx->x.ell.ready ? ctx->x.ell.ncls : 0; });
 }
 
+int dfmi_hex_dims(dfmi_ctx* ctx, int* nx, int* ny, int* nz) {
+  return guard([&] {
+    const bool on = ctx->x.ell.ready;
+    *nx = on ? ctx->x.hex[0] : 0; *ny = on ? ctx->x.hex[1] : 0; *nz = on ? ctx->x.hex[2] : 0;
+  });
+}
+
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
   return guard([&] {
     std::string e(eqn), n(name);

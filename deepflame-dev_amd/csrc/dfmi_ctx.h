@@ -41,6 +41,10 @@ struct MeshView {
   const uint8_t* ecls;
   const int *ectab, *estab;
   double rdt;
+  // hex box in blockMesh order (cell c = i + nx (j + ny k), internal faces towards +x/+y/+z in owner-slot
+  // storage, build_ell checked every row against it): the face walk computes face and neighbour indices
+  // instead of loading them (each_face<-1>); hx = 0: not such a mesh
+  int hx, hy, hz;
   const int* trav;          // optional traversal order of the per-cell gather kernels (thread t -> cell)
   const double *md, *bdv;   // C[nei] - C[own] [3][F] (face storage) and patch delta vectors [3][B] (limited schemes)
 };
@@ -245,6 +249,7 @@ struct Ctx {
   DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
   DevBuf<int> trav;   // dfmi_set_traversal: the order threads visit cells in the gather kernels (empty: natural)
+  int hex[3] = {0, 0, 0};   // MeshView::hx/hy/hz (build_ell)
   ~Ctx();
   int n_corr = 2;
 
@@ -261,6 +266,7 @@ struct Ctx {
     m.ectab = ell.ctab.p; m.estab = ell.stab.p;
     m.rdt = rdt;
     m.trav = trav.n ? trav.p : nullptr;
+    m.hx = hex[0]; m.hy = hex[1]; m.hz = hex[2];
     m.md = md.p; m.bdv = bdv.p;
     return m;
   }

@@ -78,8 +78,22 @@ __device__ __forceinline__ double bface(const MeshView& m, int t, const double* 
 // -- coalesced index loads, one indirection, all WT entries loaded up front and the loop unrolled, so
 // every face's gathers are in flight together instead of one face's latency after another's.
 // WT = 0: the CSR walk (nbrStart/nbrFace, ownStart), same order, any mesh.
+// WT = -1: hex box in blockMesh order (MeshView::hx): the same faces in the same order from the cell's
+// (i, j, k) -- neighbour faces from the z-, y-, x- cells, then the owned +x, +y, +z faces; a face of
+// owner o sits at storage kslot C + o, kslot = the owner's owned faces before it -- no index loads.
 template <int WT, class FN> __device__ __forceinline__ void each_face(const MeshView& m, int c, FN&& fn) {
-  if constexpr (WT > 0) {
+  if constexpr (WT < 0) {
+    const int nx = m.hx, ny = m.hy, nxy = m.hx * m.hy;
+    const int t = c / nx, i = c - t * nx, k = t / ny, j = t - k * ny;
+    const int hxp = i < nx - 1, hyp = j < ny - 1;
+    const int C = m.C;
+    if (k > 0) { const int o = c - nxy; fn((hxp + hyp) * C + o, o, false); }
+    if (j > 0) { const int o = c - nx; fn(hxp * C + o, o, false); }
+    if (i > 0) fn(c - 1, c - 1, false);
+    if (hxp) fn(c, c + 1, true);
+    if (hyp) fn(hxp * C + c, c + nx, true);
+    if (k < m.hz - 1) fn((hxp + hyp) * C + c, c + nxy, true);
+  } else if constexpr (WT > 0) {
     int es[WT], cs[WT];
     const int cl = ecls_of(m, c);
 #pragma unroll
@@ -1887,8 +1901,14 @@ bool face_rows(const Ctx& x) {
   const char* e = std::getenv("DFMI_FACE_CSR");
   return x.ell.W == 6 && !(e && std::atoi(e) != 0);
 }
+// hex boxes in blockMesh order: the computed face walk (each_face<-1>) everywhere (DFMI_FACE_HEX=0: off)
+bool face_hex(const Ctx& x) {
+  const char* e = std::getenv("DFMI_FACE_HEX");
+  return x.hex[0] > 0 && !(e && std::atoi(e) == 0);
+}
 #define LAUNCH_W(kern, n, ...) \
-  do { if (face_rows(x)) LAUNCH(kern<6>, n, __VA_ARGS__); else LAUNCH(kern<0>, n, __VA_ARGS__); } while (0)
+  do { if (face_hex(x)) LAUNCH(kern<-1>, n, __VA_ARGS__); else if (face_rows(x)) LAUNCH(kern<6>, n, __VA_ARGS__); \
+       else LAUNCH(kern<0>, n, __VA_ARGS__); } while (0)
 // species-chunked kernels for large mechanisms: the CSR face walk measured faster than the face rows
 // (2M cells x 53 species: y_prep 9.5 vs 17.5 ms, y_assemble_ell 4.5 vs 6.1 ms); DFMI_GEN_ROWS=1 for the rows
 bool gen_rows(const Ctx& x) {
@@ -1896,9 +1916,11 @@ bool gen_rows(const Ctx& x) {
   return face_rows(x) && e && std::atoi(e) != 0;
 }
 #define LAUNCH_SWG(kern, NS, n, ...) \
-  do { if (gen_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
+  do { if (face_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (gen_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
+       else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
 #define LAUNCH_SW(kern, NS, n, ...) \
-  do { if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
+  do { if (face_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
+       else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
 
 // the mixed-condition data of a field (MixBC): p's waveTransmissive state, every field's inletValue
 MixBC mixbc(Ctx& x, const std::string& field) {
@@ -2083,7 +2105,11 @@ void conv_weights(Ctx& x) {
   {
     KScope _ks(x, "k_conv_w_list");   // a fixed grid of 16-lane groups strides over the listed faces
     const int blocks = std::min(4096, std::max(1, blocks_for(x.Fs, 256 / CWG)));
-    if (face_rows(x))
+    if (face_hex(x))
+      hipLaunchKernelGGL(k_conv_w_list<-1>, dim3(blocks), dim3(256), 0, x.stream, m, x.S, x.st("Y"), x.st("he"), twoByk,
+                         x.f("phi"), x.f("Y"), x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), x.conv_list.p,
+                         x.conv_nlist.p, w);
+    else if (face_rows(x))
       hipLaunchKernelGGL(k_conv_w_list<6>, dim3(blocks), dim3(256), 0, x.stream, m, x.S, x.st("Y"), x.st("he"), twoByk,
                          x.f("phi"), x.f("Y"), x.f("boundary_Y"), x.f("he"), x.f("boundary_he"), x.conv_list.p,
                          x.conv_nlist.p, w);
@@ -2120,7 +2146,8 @@ static void e_scheme_terms(Ctx& x) {
       bool coupled = false;
       for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
       DFMI_CHECK(!coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
-      if (face_rows(x)) LAUNCH((k_grad_cells<1, 6>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
+      if (face_hex(x)) LAUNCH((k_grad_cells<1, -1>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
+      else if (face_rows(x)) LAUNCH((k_grad_cells<1, 6>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
       else LAUNCH((k_grad_cells<1, 0>), x.C, m, x.st("K"), x.f("K"), x.f("boundary_K"), g);
       halo_fields(x, {"gradK"});   // the neighbour cell's gradient on processor faces (patchNeighbourField)
     }
@@ -2140,7 +2167,8 @@ static void e_scheme_terms(Ctx& x) {
     double* bcf = scheme_buf(x, "boundary_cubic_flux", x.B, 1);
     double* g = scheme_buf(x, "gradHD", x.C, 9);
     scheme_buf(x, "boundary_gradHD", x.B, 9);
-    if (face_rows(x)) LAUNCH((k_grad_cells<3, 6>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
+    if (face_hex(x)) LAUNCH((k_grad_cells<3, -1>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
+    else if (face_rows(x)) LAUNCH((k_grad_cells<3, 6>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
     else LAUNCH((k_grad_cells<3, 0>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
     halo_fields(x, {"gradHD"});
     LAUNCH(k_cubic_face, x.Fs, m, x.f("hDiffCorrFlux"), g, cf);
@@ -2162,6 +2190,11 @@ void y_prep(Ctx& x) {
   do {                                                                                                               \
     if (prep_rows)                                                                                                   \
       LAUNCH_AS("k_y_prep", (k_y_prep_rows<NS>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
+             x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
+             x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
+             gout);                                                                                                  \
+    else if (face_hex(x))                                                                                            \
+      LAUNCH((k_y_prep<NS, -1>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"),  \
              x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
              x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
              gout);                                                                                                  \

@@ -948,6 +948,43 @@ void build_ell(Ctx& x) {
   if (brow.empty()) brow.push_back(0);
   x.ell.bflag.upload(bflag, x.stream);
   x.ell.brow.upload(brow, x.stream);
+  // hex box in blockMesh order (MeshView::hx, each_face<-1>): nx and nx ny from the face offsets, then every
+  // cell's face entries checked against the computed walk (same faces, storage indices, order)
+  x.hex[0] = x.hex[1] = x.hex[2] = 0;
+  if (x.fslot && x.F > 0) {
+    int nx = 0, nxy = 0;
+    bool ok = true;
+    for (int f = 0; f < x.F && ok; ++f) {
+      const int d = x.h_nei[f] - x.h_own[f];
+      if (d > 1 && (nx == 0 || d < nx)) nx = d;
+      nxy = std::max(nxy, d);
+      ok = d > 0;
+    }
+    if (ok && nx > 1 && nxy > nx && nxy % nx == 0 && C % nxy == 0) {
+      const int ny = nxy / nx, nz = C / nxy;
+      for (int c = 0; c < C && ok; ++c) {
+        const int t = c / nx, i = c - t * nx, k = t / ny, j = t - k * ny;
+        const int hxp = i < nx - 1, hyp = j < ny - 1;
+        int sf[6], so[6], sw[6], n = 0;
+        auto add = [&](int f, int o, int w) { sf[n] = f; so[n] = o; sw[n] = w; ++n; };
+        if (k > 0) add((hxp + hyp) * C + c - nxy, c - nxy, 0);
+        if (j > 0) add(hxp * C + c - nx, c - nx, 0);
+        if (i > 0) add(c - 1, c - 1, 0);
+        if (hxp) add(c, c + 1, 1);
+        if (hyp) add(hxp * C + c, c + nx, 1);
+        if (k < nz - 1) add((hxp + hyp) * C + c, c + nxy, 1);
+        int q = 0;
+        for (int kk = 0; kk < W && ok; ++kk) {
+          const int s = src[(size_t)kk * C + c];
+          if (s < 0) continue;   // slot or padding: not part of the face walk
+          ok = q < n && (s >> 1) == sf[q] && (s & 1) == sw[q] && col[(size_t)kk * C + c] == so[q];
+          ++q;
+        }
+        ok = ok && q == n;
+      }
+      if (ok) { x.hex[0] = nx; x.hex[1] = ny; x.hex[2] = nz; }
+    }
+  }
   // row classes: per cell the W (column offset, source code) pairs; coupled slots keep explicit sources
   // (slot ids are not relative to the cell) and processor columns explicit columns
   x.ell.ncls = 0;

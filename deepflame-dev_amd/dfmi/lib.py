@@ -69,6 +69,7 @@ SIGNATURES = {
     "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
     "dfmi_amg_info": [_P, C.c_int, _IP, _IP, _IP],
     "dfmi_row_classes": [_P, _IP],
+    "dfmi_hex_dims": [_P, _IP, _IP, _IP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
     "dfmi_kernel_time": [_P, _DP, _IP],
@@ -350,6 +351,12 @@ class Context:
         n = C.c_int()
         self._call("dfmi_row_classes", self.h, C.byref(n))
         return n.value
+
+    def hex_dims(self):
+        """(nx, ny, nz) of a detected hex box in blockMesh order (computed face walk), or (0, 0, 0)"""
+        v = [C.c_int(), C.c_int(), C.c_int()]
+        self._call("dfmi_hex_dims", self.h, *[C.byref(a) for a in v])
+        return tuple(a.value for a in v)
 
     def solver_stats(self, eqn):
         it = C.c_int(); r0 = C.c_double(); rel = C.c_double()

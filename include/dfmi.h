@@ -190,6 +190,10 @@ int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int*
  * instead of reading 2 W ints (hex boxes in blockMesh order: 27). Measurement aid (no reference
  * counterpart; the reference's ldu_to_csr keeps explicit CSR columns, dfMatrixDataBase.cu:166-177). */
 int dfmi_row_classes(dfmi_ctx* ctx, int* n_classes);
+/* hex box in blockMesh order detected at the first solve (every cell's face rows checked against the
+ * computed i + nx (j + ny k) walk the assembly kernels then use instead of loading indices): nx, ny, nz,
+ * or zeros. Measurement aid (no reference counterpart). */
+int dfmi_hex_dims(dfmi_ctx* ctx, int* nx, int* ny, int* nz);
 /* last solve: iterations and final relative residual */
 int dfmi_solver_stats(dfmi_ctx* ctx, const char* eqn, int* iters, double* res0, double* rel_res);
 /* work done by the solves of `eqn` since the last reset: the sum over solves and systems of the

@@ -14,12 +14,14 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _run(classes, periodic):
+def _run(classes, periodic, env=None):
     from dfmi.lib import Context
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
     os.environ["DFMI_ROW_CLASSES"] = str(classes)
+    for k, v in (env or {}).items():
+        os.environ[k] = v
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
         t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
@@ -35,10 +37,13 @@ def _run(classes, periodic):
         out["Y"] = ctx.get_field("Y", (t.S, m.n_cells))
         out["iters"] = {e: ctx.solver_stats(e)[0] for e in ("U", "Y", "E", "p")}
         out["ncls"] = ctx.row_classes()
+        out["hex"] = ctx.hex_dims()
         ctx.close()
         return out
     finally:
         os.environ.pop("DFMI_ROW_CLASSES", None)
+        for k in (env or {}):
+            os.environ.pop(k, None)
 
 
 @pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "walls"])
@@ -48,3 +53,15 @@ def test_row_classes_bitwise_explicit_rows(periodic):
     assert a["iters"] == b["iters"], (a["iters"], b["iters"])
     for k in ("p", "T", "rho", "he", "U", "Y"):
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "walls"])
+def test_hex_face_walk_bitwise_explicit_rows(periodic):
+    """the computed hex face walk (each_face<-1>) against the ELL-row and CSR walks: bitwise"""
+    a = _run(1, periodic)
+    b = _run(1, periodic, {"DFMI_FACE_HEX": "0"})
+    c = _run(1, periodic, {"DFMI_FACE_HEX": "0", "DFMI_FACE_CSR": "1"})
+    assert a["hex"] == (20, 18, 14), a["hex"]
+    assert a["iters"] == b["iters"] == c["iters"], (a["iters"], b["iters"], c["iters"])
+    for k in ("p", "T", "rho", "he", "U", "Y"):
+        assert np.array_equal(a[k], b[k]) and np.array_equal(a[k], c[k]), k
