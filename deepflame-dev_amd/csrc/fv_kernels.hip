@@ -1007,62 +1007,15 @@ __global__ void k_kinetic_slots(int B, const double* __restrict__ bU, double* __
 // ------------------------------------------------------------------ YEqn preparation (YEqn.H:24-118)
 // per cell: grad(Y_s), sumYDiffError, hDiffCorrFlux, diffAlphaD; per non-coupled slot of the cell:
 // corrected boundary gradients -> boundary sumYDiffError / hDiffCorrFlux.
-template <int S, int WT>
-__global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+// the rest of k_y_prep for cell c once its face and slot sums are in: gradients / V, sumYDiffError,
+// hDiffCorrFlux, diffAlphaD, and the non-coupled slots' boundary fields (shared with the brick kernel)
+template <int S>
+__device__ __forceinline__ void y_prep_tail(const MeshView& m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
     const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
-    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
-    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
-    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
-  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
-  if (c >= m.C) return;
-  const long C = m.C, F = m.F, B = m.B;
-  // One pass over the cell's faces computes every species' Gauss gradient AND its diffAlphaD
-  // laplacian term (the two per-species face loops of the sequential code fused; each accumulator
-  // still sums in face order, so the result is bitwise the sequential one). Own-cell values live
-  // in registers; each face loads the neighbour's Y_s and hai_s once.
-  double g[S][3], lap[S], yc[S], ahc[S];
-  const double ac = alpha[c];
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0;
-    yc[s] = Y[s * C + c];
-    ahc[s] = ac * hai[s * C + c];
-  }
-  each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
-    const double ms = m.magSf[f], dcf = m.dc[f];
-    const double an = alpha[o2];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const double yn = Y[s * C + o2];
-      const double ahn = an * hai[s * C + o2];
-      const double yf = own ? interp_f(w, yc[s], yn) : interp_f(w, yn, yc[s]);
-      const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
-      const double gam = own ? interp_f(w, ahc[s], ahn) : interp_f(w, ahn, ahc[s]);
-      const double dy = own ? yn - yc[s] : yc[s] - yn;
-      const double v = gam * ms * (dcf * dy);
-      if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
-      else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
-    }
-  });
-  each_slot(m, tyY, c, [&](int b, int t) {
-    const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
-      g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
-      double v;
-      if (bc_coupled(t)) {
-        const int pc = m.partner[b];
-        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
-        v = interp_b(m.bw[b], ahc[s], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[s]));
-      } else {
-        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
-        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
-      }
-      lap[s] += v;
-    }
-  });
+    const double* __restrict__ hai, const double* __restrict__ bhai, double* __restrict__ sumE,
+    double* __restrict__ bsumE, double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD,
+    double* __restrict__ gout, int c, double (&g)[S][3], const double (&lap)[S], const double (&yc)[S]) {
+  const long C = m.C, B = m.B;
   const double vol = m.V[c];
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -1129,6 +1082,159 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
     }
   });
 }
+
+template <int S, int WT>
+__global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
+    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
+    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
+    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
+  if (c >= m.C) return;
+  const long C = m.C, F = m.F, B = m.B;
+  // One pass over the cell's faces computes every species' Gauss gradient AND its diffAlphaD
+  // laplacian term (the two per-species face loops of the sequential code fused; each accumulator
+  // still sums in face order, so the result is bitwise the sequential one). Own-cell values live
+  // in registers; each face loads the neighbour's Y_s and hai_s once.
+  double g[S][3], lap[S], yc[S], ahc[S];
+  const double ac = alpha[c];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0;
+    yc[s] = Y[s * C + c];
+    ahc[s] = ac * hai[s * C + c];
+  }
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
+    const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+    const double ms = m.magSf[f], dcf = m.dc[f];
+    const double an = alpha[o2];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double yn = Y[s * C + o2];
+      const double ahn = an * hai[s * C + o2];
+      const double yf = own ? interp_f(w, yc[s], yn) : interp_f(w, yn, yc[s]);
+      const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+      const double gam = own ? interp_f(w, ahc[s], ahn) : interp_f(w, ahn, ahc[s]);
+      const double dy = own ? yn - yc[s] : yc[s] - yn;
+      const double v = gam * ms * (dcf * dy);
+      if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
+      else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
+    }
+  });
+  each_slot(m, tyY, c, [&](int b, int t) {
+    const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
+      g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
+      double v;
+      if (bc_coupled(t)) {
+        const int pc = m.partner[b];
+        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+        v = interp_b(m.bw[b], ahc[s], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[s]));
+      } else {
+        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
+        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+      }
+      lap[s] += v;
+    }
+  });
+  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hai, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
+}
+
+// k_y_prep on a hex box in blockMesh order (MeshView::hx), one YBX x YBY x YBZ brick of cells per
+// workgroup: Y_s and alpha hai_s of the brick and of its face-adjacent halo are staged in LDS with
+// coalesced loads (SC species at a time), and every face term reads its neighbour from LDS instead of
+// two dependent global gathers per species -- the north star's "face contributions staged in LDS". The
+// faces, their order and every product are those of k_y_prep<S, -1> (alpha hai formed at staging is the
+// same product), so the results are bitwise the face walk's.
+constexpr int YBX = 16, YBY = 4, YBZ = 4;
+constexpr int YPY = YBX + 2, YPZ = (YBX + 2) * (YBY + 2), YNB = YPZ * (YBZ + 2);
+static_assert(YBX * YBY * YBZ == TPB, "one thread per brick cell");
+template <int S, int SC>
+__global__ void __launch_bounds__(TPB) k_y_prep_brick(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
+    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
+    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
+    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
+  constexpr int NCH = (S + SC - 1) / SC;
+  __shared__ double sY[SC][YNB], sA[SC][YNB];
+  const int nx = m.hx, ny = m.hy, nz = m.hz;
+  const int nbx = nx / YBX, nby = ny / YBY;
+  const int bid = xcd_block();
+  const int bx = bid % nbx, bt = bid / nbx, by = bt % nby, bz = bt / nby;
+  const int i0 = bx * YBX, j0 = by * YBY, k0 = bz * YBZ;
+  const int t = threadIdx.x;
+  const int li = t % YBX, lj = (t / YBX) % YBY, lk = t / (YBX * YBY);
+  const int c = (i0 + li) + nx * ((j0 + lj) + ny * (k0 + lk));
+  const int me = (li + 1) + YPY * (lj + 1) + YPZ * (lk + 1);
+  const long C = m.C, F = m.F, B = m.B;
+  double g[S][3], lap[S], yc[S], ahc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) { g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0; }
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int s0 = ch * SC;
+    if (ch > 0) __syncthreads();   // every thread done with the previous chunk's values
+    for (int p = t; p < YNB; p += TPB) {   // the brick and its face halo (edges and corners have no face)
+      const int a = p % YPY, b = (p / YPY) % (YBY + 2), d = p / YPZ;
+      const int oa = (a == 0 || a == YBX + 1), ob = (b == 0 || b == YBY + 1), od = (d == 0 || d == YBZ + 1);
+      if (oa + ob + od > 1) continue;
+      const int gi = i0 + a - 1, gj = j0 + b - 1, gk = k0 + d - 1;
+      if (gi < 0 || gi >= nx || gj < 0 || gj >= ny || gk < 0 || gk >= nz) continue;
+      const long gc = gi + (long)nx * (gj + (long)ny * gk);
+      const double al = alpha[gc];
+#pragma unroll
+      for (int q = 0; q < SC; ++q)
+        if (s0 + q < S) { sY[q][p] = Y[(s0 + q) * C + gc]; sA[q][p] = al * hai[(s0 + q) * C + gc]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < SC; ++q)
+      if (s0 + q < S) { yc[s0 + q] = sY[q][me]; ahc[s0 + q] = sA[q][me]; }
+    each_face<-1>(m, c, [&](int f, int o2, bool own) {
+      const int dd = o2 - c;
+      const int lo = me + (dd == 1 ? 1 : dd == -1 ? -1 : dd == nx ? YPY : dd == -nx ? -YPY : dd > 0 ? YPZ : -YPZ);
+      const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+      const double ms = m.magSf[f], dcf = m.dc[f];
+#pragma unroll
+      for (int q = 0; q < SC; ++q) {
+        if (s0 + q >= S) continue;
+        const int s = s0 + q;
+        const double yn = sY[q][lo];
+        const double ahn = sA[q][lo];
+        const double yf = own ? interp_f(w, yc[s], yn) : interp_f(w, yn, yc[s]);
+        const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+        const double gam = own ? interp_f(w, ahc[s], ahn) : interp_f(w, ahn, ahc[s]);
+        const double dy = own ? yn - yc[s] : yc[s] - yn;
+        const double v = gam * ms * (dcf * dy);
+        if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
+        else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
+      }
+    });
+  }
+  each_slot(m, tyY, c, [&](int b, int tt) {
+    const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double yf = bface(m, tt, Y + s * C, bY + s * B, b, c);
+      g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
+      double v;
+      if (bc_coupled(tt)) {
+        const int pc = m.partner[b];
+        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+        v = interp_b(m.bw[b], ahc[s], an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc[s]));
+      } else {
+        const double sng = (tt == FIXED_VALUE || tt == CALCULATED || tt == FIXED_ENERGY || bc_mixed(tt)) ? m.bdc[b] * (bY[s * B + b] - yc[s]) : 0.0;
+        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+      }
+      lap[s] += v;
+    }
+  });
+  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hai, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
+}
+// species per staged chunk: all (S <= 5) or about half (LDS 2 SC YNB doubles: 9 species -> 5 = 52 KiB)
+constexpr int ybrick_sc(int S) { return S <= 5 ? S : (S + 1) / 2; }
 
 // k_y_prep, species-outer over the solver's gather rows (hex meshes, W = 6): the cell's six faces'
 // indices, geometry and neighbour alpha are loaded once up front, then each species loads its twelve
@@ -2186,6 +2292,12 @@ void y_prep(Ctx& x) {
 // (DFMI_YPREP_ROWS=1: the species-outer row kernel k_y_prep_rows on hex meshes)
   const char* erows = std::getenv("DFMI_YPREP_ROWS");
   const bool prep_rows = face_rows(x) && erows && std::atoi(erows) != 0;
+  // LDS-staged brick kernel on hex boxes whose dimensions the brick divides (DFMI_YPREP_BRICK=0: off,
+  // 2: all species staged at once)
+  const char* eb = std::getenv("DFMI_YPREP_BRICK");
+  const int bmode = eb ? std::atoi(eb) : 1;
+  const int brick = (face_hex(x) && !x.trav.n && x.hex[0] % YBX == 0 && x.hex[1] % YBY == 0 && x.hex[2] % YBZ == 0 &&
+                     bmode > 0) ? (bmode == 2 ? 2 : 1) : 0;
 #define CALL(NS)                                                                                                     \
   do {                                                                                                               \
     if (prep_rows)                                                                                                   \
@@ -2193,6 +2305,16 @@ void y_prep(Ctx& x) {
              x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
              x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
              gout);                                                                                                  \
+    else if (brick == 1)                                                                                             \
+      LAUNCH_AS("k_y_prep", (k_y_prep_brick<NS, ybrick_sc(NS)>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"),    \
+             x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
+             x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                              \
+             x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                               \
+    else if (brick == 2)                                                                                             \
+      LAUNCH_AS("k_y_prep", (k_y_prep_brick<NS, (NS < 10 ? NS : ybrick_sc(NS))>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"),               \
+             x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
+             x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                              \
+             x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                               \
     else if (face_hex(x))                                                                                            \
       LAUNCH((k_y_prep<NS, -1>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"),  \
              x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
