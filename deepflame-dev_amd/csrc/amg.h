@@ -44,6 +44,12 @@ struct Amg {
   // Per solve the ranks all-gather their packed rows; per V-cycle their coarsest right-hand sides, and every
   // rank smooths the identical global level redundantly (k_coarsest) -- the role of AmgX's consolidated
   // coarse levels (src_gpu/AmgXSolver.cu:184-266) in place of block-Jacobi across ranks.
+  // level 0 with its processor couplings (several ranks; DFMI_AMG_HALO_L0=0: off): the first sweep's residual and
+  // the post-sweep include the halo columns (the PCG residual and diagonal exchanged, the prolongated
+  // correction exchanged before the post-sweep) instead of dropping them (block-Jacobi)
+  bool halo_l0 = false;
+  const double* dS_full = nullptr;        // this solve's level-0 diagonal incl. the exchanged halo entries [C + H]
+  DevBuf<double> hy;                      // prolongated level-0 iterate incl. halo [C + H]
   bool global = false;
   int nmax = 0, ng = 0, wc = 0, we = 0, wg = 0, nloc = 0;
   DevBuf<int> g_col;                      // [wg][ng] global columns

@@ -204,6 +204,78 @@ __global__ void __launch_bounds__(TPB) k_smooth_res_r8(int n, int W_, const int*
   if ((threadIdx.x & 7) == 0) bnext[c >> 3] = s;
 }
 
+// level 0 with its processor couplings (Amg::halo_l0): the first sweep from zero + residual as k_smooth_res,
+// the halo columns included -- x0 at a halo cell is omega r_j / D_j from the exchanged residual and diagonal
+// (the peer's own x0_j: D_j rounded to T as its level-0 copy is)
+template <int WT, class T>
+__global__ void __launch_bounds__(TPB) k_smooth_res_h(int n, int W_, ColView col, const T* __restrict__ val,
+                                                      const T* __restrict__ D, const double* __restrict__ b,
+                                                      const double* __restrict__ dh, T omega, T* __restrict__ x,
+                                                      T* __restrict__ r, const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
+  const int W = WT > 0 ? WT : W_;
+  const int c = xcd_block() * blockDim.x + threadIdx.x;
+  if (c >= n || (act && *act == 0.0)) return;
+  const T bc = (T)b[c];
+  const T xc = omega * bc / D[c];
+  T y = D[c] * xc;
+  const int rb = col.row(c);
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const int j = col.get(s_ct, rb, n, k, c);
+    const T dj = j < n ? D[j] : (T)dh[j];
+    y += val[(long)k * n + c] * (omega * (T)b[j] / dj);
+  }
+  x[c] = xc;
+  r[c] = bc - y;
+}
+// y = x0 + sc P xc on level 0 (the iterate the post-sweep smooths), in double for the halo exchange
+template <class T>
+__global__ void k_prolong_y(int n, const T* __restrict__ x, const int* __restrict__ agg, const T* __restrict__ xc, T sc,
+                            double* __restrict__ y, const double* act) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n || (act && *act == 0.0)) return;
+  y[c] = (double)(x[c] + sc * xc[agg[c]]);
+}
+// the post-sweep with the processor columns: out = y + omega (b - A y) / D, y incl. the exchanged halo;
+// block partials of b.out
+template <int WT, class T>
+__global__ void __launch_bounds__(TPB) k_post_smooth_h(int n, int W_, ColView col, const T* __restrict__ val,
+                                                       const T* __restrict__ D, const double* __restrict__ b,
+                                                       const double* __restrict__ y, T omega, double* __restrict__ out,
+                                                       double* partial, const double* act) {
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
+  const int W = WT > 0 ? WT : W_;
+  if (act && *act == 0.0) return;
+  __shared__ double sh[TPB / 64];
+  double acc = 0.0;
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const T yc = (T)y[c];
+    T ay = D[c] * yc;
+    const int rb = col.row(c);
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int j = col.get(s_ct, rb, n, k, c);
+      ay += val[(long)k * n + c] * (T)y[j];
+    }
+    const double bc = b[c];
+    const double o = (double)(yc + omega * ((T)bc - ay) / D[c]);
+    out[c] = o;
+    acc += bc * o;
+  }
+  if (!partial) return;
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0;
+    for (int w = 0; w < TPB / 64; ++w) a += sh[w];
+    partial[blockIdx.x] = a;
+  }
+}
+
 template <class T>
 __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
                            const T* __restrict__ r, T* __restrict__ bc, const double* act) {
@@ -730,6 +802,11 @@ void amg_setup(Ctx& x) {
     if (l == 0 && a.l0_sweeps > 1) v.zt.alloc(nv);
   }
   if (want_global) global_setup(x, col, fin_aggs, last_col);
+  // measured (in-process ranks of 64^3): p-iterations per solve 14 / 17 / 19 -> 12 / 14 / 14-15 for 2 / 4 / 8
+  // ranks (one rank: 12) for two more halo exchanges per PCG iteration; DFMI_AMG_HALO_L0=0: block-Jacobi
+  a.halo_l0 = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_HALO_L0", 1) != 0 && a.lv.size() >= 2 &&
+              a.l0_sweeps == 1 && a.fused_coarse == 0 && a.coop_blocks == 0 && !a.use_graph;
+  if (a.halo_l0) a.hy.alloc((size_t)C + x.H);
   a.ready = true;
 }
 
@@ -871,7 +948,10 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     T* rcur = RV(l);
     if (!(l == 0 && l0_done)) {
       KScope _ks(x, "k_smooth_res");
-      if (l == 0)
+      if (l == 0 && a.halo_l0)   // r and the diagonal carry the exchanged halo entries (solve_pcg)
+        launch_w(f.W, g, x.stream, k_smooth_res_h<0, T>, k_smooth_res_h<6, T>, f.n, f.W, COL(0), VAL(0), DD(0), r,
+                 a.dS_full, om, XV(0), RV(0), act);
+      else if (l == 0)
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
                  DD(0), r, om, XV(0), RV(0), act);
       else
@@ -929,7 +1009,15 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   for (int l = L - 2; l >= 0; --l) {
     AmgLevel& f = a.lv[l];
     KScope _ks(x, "k_prolong_smooth");
-    if (l == 0) {
+    if (l == 0 && a.halo_l0) {   // prolongate, exchange the iterate, post-sweep with the processor columns
+      hipLaunchKernelGGL(k_prolong_y<T>, dim3(blocks_for(f.n, TPB)), dim3(TPB), 0, x.stream, f.n, (const T*)XV(0),
+                         (const int*)f.agg.p, XC(0), sc, a.hy.p, act);
+      DFMI_HIP(hipGetLastError());
+      HaloItem it{a.hy.p, a.hy.p, 1, (long)f.n + x.H, (long)f.n + x.H, false};
+      halo_update(x, &it, 1);
+      launch_w(f.W, dim3(nblk), x.stream, k_post_smooth_h<0, T>, k_post_smooth_h<6, T>, f.n, f.W, COL(0), VAL(0), DD(0),
+               r, (const double*)a.hy.p, om, z, partial, act);
+    } else if (l == 0) {
       // with ns post-sweeps the outputs alternate zt / z so that the last one lands in z
       const int ns = a.l0_sweeps;
       auto outk = [&](int k) { return ((ns - k) % 2 == 0) ? z : f.zt.p; };   // k = 1 .. ns

@@ -1239,6 +1239,10 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   if (amg) {
     if (!x.amg.ready) amg_setup(x);
     amg_galerkin(x, val, v.dS);
+    if (x.amg.halo_l0) {   // the level-0 diagonal across processor faces, once per solve
+      halo_vecs(x, {v.dS}, 1, Ce);
+      x.amg.dS_full = v.dS;
+    }
   }
   halo_vecs(x, {v.xw}, 1, Ce);
   if (small_solve(x)) {
@@ -1277,6 +1281,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       if (x.ws.red_all.n < (size_t)8 * x.nranks) x.ws.red_all.alloc((size_t)8 * x.nranks);
       double* loc = x.ws.red_local.p;
       hipLaunchKernelGGL(k_red_local<2>, dim3(1), dim3(TPB), 0, x.stream, q2, nblk, loc);
+      if (x.amg.halo_l0) halo_vecs(x, {v.r}, 1, Ce);   // the V-cycle's level 0 reads the residual across ranks
       amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, act);
       hipLaunchKernelGGL(k_red_local<1>, dim3(1), dim3(TPB), 0, x.stream, q3, nblk, loc + 2);
       DFMI_HIP(hipGetLastError());

@@ -35,7 +35,7 @@ def _setup(m, t, ym, dt, comm=None, schemes=None):
 
 
 def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True, renumber=None, overlap=False,
-         schemes=None, perturb=False):
+         schemes=None, perturb=False, env=None):
     from dfmi.mesh import hex_box, global_cell_ids
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
@@ -98,14 +98,19 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
         except Exception as e:   # surfaced below
             err[r] = e
 
-    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work)
+    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work), `env` (AMG knobs) at the
+    # first pressure solve
     prev = os.environ.get("DFMI_HALO_OVERLAP")
     os.environ["DFMI_HALO_OVERLAP"] = "1" if overlap else "0"
+    for k, v in (env or {}).items():
+        os.environ[k] = v
     th = [threading.Thread(target=work, args=(r,)) for r in range(nr)]
     for x in th:
         x.start()
     for x in th:
         x.join(timeout=300)
+    for k in (env or {}):
+        os.environ.pop(k, None)
     if prev is None:
         os.environ.pop("DFMI_HALO_OVERLAP", None)
     else:
@@ -129,6 +134,7 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
     # all ranks agree on solver iteration counts (rank-ordered global reductions)
     for r in range(1, nr):
         assert out[r]["stats"]["p"][0] == out[0]["stats"]["p"][0]
+    glob["p_iters"] = out[0]["stats"]["p"][0]
     if orc is not None:
         ref["oracle"] = {n: orc[n] for n in ("T", "p", "rho", "he", "U", "Y")}
     return ref, glob
@@ -298,3 +304,30 @@ def test_overlapped_halo_walls_two_steps():
     for n in ("T", "p", "rho", "U", "Y"):
         e = rel_err(glob[n], ref[n])
         assert e < 1e-9, (n, e)
+
+
+@pytest.mark.parametrize("env", [{"DFMI_AMG_HALO_L0": "0"}, {"DFMI_AMG_GLOBAL": "1"},
+                                 {"DFMI_AMG_GLOBAL": "1", "DFMI_AMG_HALO_L0": "0"}], ids=["blockjacobi", "global", "global-bj"])
+def test_decomposed_amg_variants_match_oracle(env):
+    """the decomposed-AMG variants (level 0 smoothed with its processor couplings -- the default -- or
+    block-Jacobi; the opt-in agglomerated coarsest level of all ranks) precondition the same PCG: one outer
+    iteration matches the single-domain run and the oracle on a mesh with coarse levels on every rank (768
+    cells per rank, 2 x 2 x 2)"""
+    ref, glob = _run(24, 16, 16, (2, 2, 2), env=env)
+    for n in ("T", "p", "rho", "he", "U", "Y"):
+        e = rel_err(glob[n], ref[n])
+        assert e < 1e-9, (n, e)
+        e = rel_err(glob[n], ref["oracle"][n])
+        assert e < 1e-9, ("oracle", n, e)
+
+
+def test_halo_coupled_level0_needs_fewer_pcg_iterations():
+    """the V-cycle's level 0 with its processor couplings (default) against block-Jacobi across ranks: the same
+    solution, fewer p-iterations (2 x 2 x 2 ranks of 16^3)"""
+    ref, hal = _run(32, 32, 32, (2, 2, 2), n_steps=2)
+    _, bj = _run(32, 32, 32, (2, 2, 2), n_steps=2, env={"DFMI_AMG_HALO_L0": "0"})
+    print("p-iterations: halo-coupled", hal["p_iters"], "block-Jacobi", bj["p_iters"])
+    assert hal["p_iters"] < bj["p_iters"], (hal["p_iters"], bj["p_iters"])
+    for n in ("T", "p", "rho", "he", "U", "Y"):
+        assert rel_err(hal[n], ref[n]) < 1e-9, n
+        assert rel_err(bj[n], ref[n]) < 1e-9, n
