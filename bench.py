@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
-PMC_FILE = "r02_pmc_traffic.json"
+PMC_FILE = "r03_pmc_traffic.json"
 
 MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species table made by dfmi.transport_fit
     "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),

@@ -32,7 +32,7 @@ EOF
   [ $rc -eq 0 ] || exit $rc
 done
 if [ -z "$SKIP_PROF" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-flame ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-flame --alt-steps 0 ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
   rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python scripts/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.csv 2>&1; head -30 gpurun_out/prof_summary.csv
 fi
