@@ -251,11 +251,33 @@ __global__ void k_react_count(int C, const double* __restrict__ T, double Tr, in
   __syncthreads();
   if (threadIdx.x == 0) bc[blockIdx.x] = s;
 }
-__global__ void k_react_scan(int nb, int* __restrict__ bc, int* __restrict__ total) {
-  if (threadIdx.x != 0) return;
-  int a = 0;
-  for (int i = 0; i < nb; ++i) { const int v = bc[i]; bc[i] = a; a += v; }
-  *total = a;
+// exclusive scan of the per-block counts in one 1024-thread workgroup (chunks of 1024, wave prefix sums)
+__global__ void __launch_bounds__(1024) k_react_scan(int nb, int* __restrict__ bc, int* __restrict__ total) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + t;
+    const int v = i < nb ? bc[i] : 0;
+    int incl = v;   // inclusive prefix within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int wo = 0;
+    for (int k = 0; k < w; ++k) wo += wsum[k];
+    const int c0 = carry;
+    if (i < nb) bc[i] = c0 + wo + incl - v;
+    __syncthreads();
+    if (t == 1023) carry = c0 + wo + incl;
+    __syncthreads();
+  }
+  if (t == 0) *total = carry;
 }
 __global__ void k_react_scatter(int C, const double* __restrict__ T, double Tr, const int* __restrict__ boff,
                                 int* __restrict__ idx) {
@@ -383,7 +405,7 @@ void dnn_prepare(Ctx& x) {
   if (d.bc.n < (size_t)nb + 1) d.bc.alloc(nb + 1);
   if (d.idx.n < (size_t)C) d.idx.alloc(C);
   hipLaunchKernelGGL(k_react_count, dim3(nb), dim3(CB), 0, x.stream, C, x.f("T"), d.T_react, d.bc.p);
-  hipLaunchKernelGGL(k_react_scan, dim3(1), dim3(64), 0, x.stream, nb, d.bc.p, d.bc.p + nb);
+  hipLaunchKernelGGL(k_react_scan, dim3(1), dim3(1024), 0, x.stream, nb, d.bc.p, d.bc.p + nb);
   hipLaunchKernelGGL(k_react_scatter, dim3(nb), dim3(CB), 0, x.stream, C, x.f("T"), d.T_react, d.bc.p, d.idx.p);
   DFMI_HIP(hipGetLastError());
   d.nr_host.ensure(1);
