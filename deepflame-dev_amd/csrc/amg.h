@@ -48,6 +48,12 @@ struct Amg {
   // the post-sweep include the halo columns (the PCG residual and diagonal exchanged, the prolongated
   // correction exchanged before the post-sweep) instead of dropping them (block-Jacobi)
   bool halo_l0 = false;
+  // level 0 read face-wise (FaceOp; one rank, hex box, symmetric p: solve_pcg sets dfo each solve, the fp32
+  // copies of its face and slot coefficients are rounded here) instead of from the ELL values
+  bool face = false;
+  FaceOp<double> dfo;
+  FaceOp<float> ffo;
+  DevBuf<float> fup, fbc;
   const double* dS_full = nullptr;        // this solve's level-0 diagonal incl. the exchanged halo entries [C + H]
   DevBuf<double> hy;                      // prolongated level-0 iterate incl. halo [C + H]
   bool global = false;

@@ -65,24 +65,29 @@ __global__ void k_round_f32(long n, const double* __restrict__ a, float* __restr
 }
 
 // x = omega b / D (first sweep from zero); r = b - A x   (columns >= n: other ranks, dropped)
-template <int WT, class T, class TB>
+template <int WT, class T, class TB, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, ColView col,
                                                     const T* __restrict__ val, const T* __restrict__ D,
                                                     const TB* __restrict__ b, T omega,
-                                                    T* __restrict__ x, T* __restrict__ r, const double* act) {
+                                                    T* __restrict__ x, T* __restrict__ r, const double* act,
+                                                    FaceOp<T> fo = {}) {
   __shared__ int s_ct[CT_MAX];
-  col.stage(s_ct);
+  if (!FF) col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   const int c = xcd_block() * blockDim.x + threadIdx.x;
   if (c >= n || (act && *act == 0.0)) return;
   const T bc = (T)b[c];
   const T xc = omega * bc / D[c];
   T y = D[c] * xc;
-  const int rb = col.row(c);
+  if constexpr (FF) {
+    face_row(fo, c, [&](int j, T a) { if (j < n) y += a * (omega * (T)b[j] / D[j]); });
+  } else {
+    const int rb = col.row(c);
 #pragma unroll
-  for (int k = 0; k < W; ++k) {
-    const int j = col.get(s_ct, rb, n, k, c);
-    if (j < n) y += val[(long)k * n + c] * (omega * (T)b[j] / D[j]);
+    for (int k = 0; k < W; ++k) {
+      const int j = col.get(s_ct, rb, n, k, c);
+      if (j < n) y += val[(long)k * n + c] * (omega * (T)b[j] / D[j]);
+    }
   }
   x[c] = xc;
   r[c] = bc - y;
@@ -288,15 +293,15 @@ __global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __
 
 // y = x + s P xc; out = y + omega (b - A y) / D; optional block partials of b.out (level 0: r.z,
 // formed in double from the values actually stored)
-template <int WT, class T, class TB, class TO>
+template <int WT, class T, class TB, class TO, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, ColView col,
                                                         const T* __restrict__ val, const T* __restrict__ D,
                                                         const TB* __restrict__ b, const T* __restrict__ x,
                                                         const int* __restrict__ agg, const T* __restrict__ xc,
                                                         T omega, T sc, TO* __restrict__ out, double* partial,
-                                                        const double* act) {
+                                                        const double* act, FaceOp<T> fo = {}) {
   __shared__ int s_ct[CT_MAX];
-  col.stage(s_ct);
+  if (!FF) col.stage(s_ct);
   const int W = WT > 0 ? WT : W_;
   if (act && *act == 0.0) return;   // uniform: no barrier below is reached by part of the block
   __shared__ double sh[TPB / 64];
@@ -304,11 +309,15 @@ __global__ void __launch_bounds__(TPB) k_prolong_smooth(int n, int W_, ColView c
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const T yc = x[c] + sc * xc[agg[c]];
     T ay = D[c] * yc;
-  const int rb = col.row(c);
+    if constexpr (FF) {
+      face_row(fo, c, [&](int j, T a) { if (j < n) ay += a * (x[j] + sc * xc[agg[j]]); });
+    } else {
+      const int rb = col.row(c);
 #pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col.get(s_ct, rb, n, k, c);
-      if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
+      for (int k = 0; k < W; ++k) {
+        const int j = col.get(s_ct, rb, n, k, c);
+        if (j < n) ay += val[(long)k * n + c] * (x[j] + sc * xc[agg[j]]);
+      }
     }
     const TB bc = b[c];
     const TO o = (TO)(yc + omega * ((T)bc - ay) / D[c]);
@@ -816,7 +825,17 @@ void amg_galerkin(Ctx& x, const double* val0, const double* D0) {
   if (a.fp32) {   // the level-0 smoother reads a single-precision copy of the solver's ELL operator
     AmgLevel& l0 = a.lv[0];
     KScope _ks(x, "k_round_f32");
-    hipLaunchKernelGGL(k_round_f32, dim3(2048), dim3(TPB), 0, x.stream, (long)l0.W * l0.n, val0, l0.fval.p);
+    if (a.face) {   // ... or of the face and slot coefficients the face-wise level 0 reads
+      const long nf = 3L * a.dfo.C, nb = std::max(x.B, 1);
+      if (a.fup.n < (size_t)nf) a.fup.alloc(nf);
+      if (a.fbc.n < (size_t)nb) a.fbc.alloc(nb);
+      hipLaunchKernelGGL(k_round_f32, dim3(2048), dim3(TPB), 0, x.stream, nf, a.dfo.up, a.fup.p);
+      if (x.B) hipLaunchKernelGGL(k_round_f32, dim3(256), dim3(TPB), 0, x.stream, (long)x.B, a.dfo.bc, a.fbc.p);
+      a.ffo = FaceOp<float>{1, a.dfo.nx, a.dfo.ny, a.dfo.nz, a.dfo.C, a.fup.p, a.fbc.p, a.dfo.csStart, a.dfo.csSlot,
+                            a.dfo.scol};
+    } else {
+      hipLaunchKernelGGL(k_round_f32, dim3(2048), dim3(TPB), 0, x.stream, (long)l0.W * l0.n, val0, l0.fval.p);
+    }
     hipLaunchKernelGGL(k_round_f32, dim3(512), dim3(TPB), 0, x.stream, (long)l0.n, D0, l0.fD.p);
     DFMI_HIP(hipGetLastError());
   }
@@ -882,6 +901,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   };
   // level 0: the solver rows (row classes where built); coarse levels: explicit columns
   auto COL = [&](int l) { return l == 0 ? col0 : ColView{a.lv[l].col.p, nullptr, nullptr, a.lv[l].W}; };
+  auto FO = [&]() -> FaceOp<T> { if constexpr (F) return a.ffo; else return a.dfo; };
   auto RAW = [&](int l) { return l == 0 ? col0.col : (const int*)a.lv[l].col.p; };
   auto BV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fb.p; else return a.lv[l].b.p; };
   auto XV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fx.p; else return a.lv[l].x.p; };
@@ -893,7 +913,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     {
       KScope _ks(x, "k_smooth_res");
       launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
-               DD(0), r, om, XV(0), RV(0), act);
+               DD(0), r, om, XV(0), RV(0), act, FaceOp<T>{});
     }
     {
       KScope _ks(x, "k_restrict");
@@ -919,7 +939,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
       KScope _ks(x, "k_prolong_smooth");
       launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
                f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p,
-               (const T*)(L == 2 ? XV(1) : XO(1)), om, sc, z, partial, act);
+               (const T*)(L == 2 ? XV(1) : XO(1)), om, sc, z, partial, act, FaceOp<T>{});
     }
     DFMI_HIP(hipGetLastError());
     return;
@@ -951,12 +971,15 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
       if (l == 0 && a.halo_l0)   // r and the diagonal carry the exchanged halo entries (solve_pcg)
         launch_w(f.W, g, x.stream, k_smooth_res_h<0, T>, k_smooth_res_h<6, T>, f.n, f.W, COL(0), VAL(0), DD(0), r,
                  a.dS_full, om, XV(0), RV(0), act);
+      else if (l == 0 && a.face)
+        hipLaunchKernelGGL((k_smooth_res<0, T, double, true>), g, dim3(TPB), 0, x.stream, f.n, f.W, COL(0), VAL(0),
+                           DD(0), r, om, XV(0), RV(0), act, FO());
       else if (l == 0)
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
-                 DD(0), r, om, XV(0), RV(0), act);
+                 DD(0), r, om, XV(0), RV(0), act, FaceOp<T>{});
       else
         launch_w(f.W, g, x.stream, k_smooth_res<0, T, T>, k_smooth_res<6, T, T>, f.n, f.W, COL(l), VAL(l), DD(l),
-                 (const T*)BV(l), om, XV(l), RV(l), act);
+                 (const T*)BV(l), om, XV(l), RV(l), act, FaceOp<T>{});
     }
     if (l == 0 && a.l0_sweeps > 1) {   // further pre-sweeps, the residual carried along
       T* ralt;
@@ -1017,13 +1040,17 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
       halo_update(x, &it, 1);
       launch_w(f.W, dim3(nblk), x.stream, k_post_smooth_h<0, T>, k_post_smooth_h<6, T>, f.n, f.W, COL(0), VAL(0), DD(0),
                r, (const double*)a.hy.p, om, z, partial, act);
+    } else if (l == 0 && a.face) {   // one post-sweep (face mode needs l0_sweeps == 1)
+      hipLaunchKernelGGL((k_prolong_smooth<0, T, double, double, true>), dim3(nblk), dim3(TPB), 0, x.stream, f.n, f.W,
+                         COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, XC(0), om, sc, z, partial,
+                         act, FO());
     } else if (l == 0) {
       // with ns post-sweeps the outputs alternate zt / z so that the last one lands in z
       const int ns = a.l0_sweeps;
       auto outk = [&](int k) { return ((ns - k) % 2 == 0) ? z : f.zt.p; };   // k = 1 .. ns
       launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
                f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p, XC(0), om, sc,
-               outk(1), ns == 1 ? partial : (double*)nullptr, act);
+               outk(1), ns == 1 ? partial : (double*)nullptr, act, FaceOp<T>{});
       for (int k = 2; k <= ns; ++k) {
         KScope _ks2(x, "k_jacobi_sweep");
         launch_w(f.W, dim3(nblk), x.stream, k_jacobi_sweep<0, T, double, double>, k_jacobi_sweep<6, T, double, double>,
@@ -1033,7 +1060,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     } else {
       launch_w(f.W, dim3(blocks_for(f.n, TPB)), x.stream, k_prolong_smooth<0, T, T, T>, k_prolong_smooth<6, T, T, T>,
                f.n, f.W, COL(l), VAL(l), DD(l), (const T*)BV(l), (const T*)XV(l), (const int*)f.agg.p,
-               XC(l), om, sc, XO(l), (double*)nullptr, act);
+               XC(l), om, sc, XO(l), (double*)nullptr, act, FaceOp<T>{});
       // the corrected x of this level feeds the next finer prolongation
       if constexpr (F) std::swap(f.fx, f.fxo); else std::swap(f.x, f.xo);
     }

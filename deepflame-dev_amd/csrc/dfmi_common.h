@@ -124,4 +124,38 @@ struct ColView {
   }
 };
 
+// The symmetric pressure operator read face-wise on a hex box in blockMesh order (FaceOp::on; the cell's
+// rows are the ELL's, checked at build_ell): faces from the computed (i, j, k) walk with their coefficient at
+// the owner-slot storage index (lower == upper for the laplacian), then the cell's coupled slots in slot
+// order with -boundaryCoeffs -- the ELL row's entries in the ELL's order without reading its 48 B of values
+// (the face array holds each coefficient once: 24 B per cell) or padding. T: fp64, or the V-cycle's fp32
+// copies (the ELL's rounding: (float) upper, -(float) bc).
+template <class T> struct FaceOp {
+  int on = 0;
+  int nx = 0, ny = 0, nz = 0;
+  long C = 0;
+  const T* up = nullptr;           // face coefficients [kslot][C]
+  const T* bc = nullptr;           // boundaryCoeffs [B]
+  const int* csStart = nullptr;    // coupled slots of each cell [C + 1] ...
+  const int* csSlot = nullptr;     // ... ascending slot index
+  const int* scol = nullptr;       // column of a coupled slot: cyclic partner cell, or C + halo index
+};
+template <class T, class FN> __device__ __forceinline__ void face_row(const FaceOp<T>& o, int c, FN&& fn) {
+  const int nx = o.nx, ny = o.ny, nxy = o.nx * o.ny;
+  const int C = (int)o.C;
+  const int t = c / nx, i = c - t * nx, k = t / ny, j = t - k * ny;
+  const int hxp = i < nx - 1, hyp = j < ny - 1;
+  if (k > 0) { const int q = c - nxy; fn(q, o.up[(hxp + hyp) * C + q]); }
+  if (j > 0) { const int q = c - nx; fn(q, o.up[hxp * C + q]); }
+  if (i > 0) fn(c - 1, o.up[c - 1]);
+  if (hxp) fn(c + 1, o.up[c]);
+  if (hyp) fn(c + nx, o.up[hxp * C + c]);
+  if (k < o.nz - 1) fn(c + nxy, o.up[(hxp + hyp) * C + c]);
+  const int e1 = o.csStart[c + 1];
+  for (int e = o.csStart[c]; e < e1; ++e) {
+    const int b = o.csSlot[e];
+    fn(o.scol[b], -o.bc[b]);
+  }
+}
+
 }  // namespace dfmi

@@ -223,6 +223,7 @@ struct Ctx {
     // DFMI_ROW_CLASSES=0: explicit columns everywhere)
     DevBuf<uint8_t> cls;
     DevBuf<int> ctab, stab;
+    DevBuf<int> csStart, csSlot, scol;   // coupled slots per cell and their columns (FaceOp)
     int ncls = 0;
     bool fv_classes = false;
     ColView cols() const {

@@ -362,14 +362,21 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys 
 // scal: 0 rz, 1 rz_prev, 2 alpha, 4 res0, 5 res, 6 active, 7 iters
 struct CV { double *dS, *rhs, *r, *z, *pa, *pb, *q, *xw; };
 
-template <int WT>
+template <int WT, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, ColView col,
-                                                 const double* __restrict__ val, CV v, double* partial) {
+                                                 const double* __restrict__ val, CV v, double* partial,
+                                                 FaceOp<double> fo = {}) {
   __shared__ int s_ct[CT_MAX];
-  col.stage(s_ct);
+  if (!FF) col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    const double ax = ell_mv<WT>(W, C, col, s_ct, val, v.dS[c], v.xw, c);
+    double ax;
+    if constexpr (FF) {
+      ax = v.dS[c] * v.xw[c];
+      face_row(fo, c, [&](int j, double a) { ax += a * v.xw[j]; });
+    } else {
+      ax = ell_mv<WT>(W, C, col, s_ct, val, v.dS[c], v.xw, c);
+    }
     const double rr = v.rhs[c] - ax;
     const double zz = rr / v.dS[c];
     v.r[c] = rr; v.z[c] = zz; v.pa[c] = 0.0; v.pb[c] = 0.0;
@@ -380,12 +387,12 @@ __global__ void __launch_bounds__(TPB) k_cg_init(long C, int W, ColView col,
 
 // prologue: rz, res, convergence, beta; p_new = z + beta p_old (own and, on the fly, neighbours);
 // q = A p_new; partial p_new.q
-template <int WT>
+template <int WT, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, ColView col,
                                                  const double* __restrict__ val, int it, int max_iter, double tol,
                                                  double abs_tol, Red red_rz, Red red_rr, double* scal, CV v,
                                                  const double* __restrict__ pold, double* __restrict__ pnew,
-                                                 double* partial, RowSet rs) {
+                                                 double* partial, RowSet rs, FaceOp<double> fo = {}) {
   if (it > 0 && scal[6] == 0.0) return;   // stopped earlier
   double a[1], b[1];
   red_sum<1>(red_rz, 0, a);
@@ -405,17 +412,21 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, ColView col,
   const double* z = v.z;
   const int Wr = WT > 0 ? WT : W;
   __shared__ int s_ct[CT_MAX];
-  col.stage(s_ct);
+  if (!FF) col.stage(s_ct);
   double acc[1] = {0.0};
   for_rows(C, rs, [&](int c) {
     const double pc = z[c] + beta * pold[c];
     pnew[c] = pc;
-    const int rb = col.row(c);
     double y = v.dS[c] * pc;
+    if constexpr (FF) {
+      face_row(fo, c, [&](int j, double a) { y += a * (z[j] + beta * pold[j]); });
+    } else {
+      const int rb = col.row(c);
 #pragma unroll
-    for (int k = 0; k < Wr; ++k) {
-      const int j = col.get(s_ct, rb, C, k, c);
-      y += val[k * C + c] * (z[j] + beta * pold[j]);
+      for (int k = 0; k < Wr; ++k) {
+        const int j = col.get(s_ct, rb, C, k, c);
+        y += val[k * C + c] * (z[j] + beta * pold[j]);
+      }
     }
     v.q[c] = y;
     acc[0] += pc * y;
@@ -454,13 +465,13 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
 // V-cycle's right-hand side, so the same pass forms x0 = omega r / D and res = r - A x0 in the V-cycle's
 // precision T; a neighbour's r_j is re-formed as r_j - alpha q_j (the expression the update stores), so
 // x0 and res are bitwise those of k_smooth_res on the stored r. Partials (0, r.r) as k_cg_x<false>.
-template <int WT, class T>
+template <int WT, class T, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col, Red red,
                                                      double* scal, double* __restrict__ x, CV v,
                                                      const double* __restrict__ pnew, double* __restrict__ rnew,
                                                      double* partial, const T* __restrict__ val0,
                                                      const T* __restrict__ D0, T omega, T* __restrict__ x0,
-                                                     T* __restrict__ res0) {
+                                                     T* __restrict__ res0, FaceOp<T> fo = {}) {
   if (scal[6] == 0.0) return;
   double pv[1];
   red_sum<1>(red, 0, pv);
@@ -469,7 +480,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
   if (leader()) { scal[2] = alpha; scal[1] = rz; }
   const int W = WT > 0 ? WT : W_;
   __shared__ int s_ct[CT_MAX];
-  col.stage(s_ct);
+  if (!FF) col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
@@ -479,11 +490,17 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
     const T bc = (T)rr;
     const T xc = omega * bc / D0[c];
     T y = D0[c] * xc;
-    const int rb = col.row(c);
+    if constexpr (FF) {
+      face_row(fo, c, [&](int j, T a) {
+        if (j < C) y += a * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
+      });
+    } else {
+      const int rb = col.row(c);
 #pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col.get(s_ct, rb, C, k, c);
-      if (j < C) y += val0[(long)k * C + c] * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
+      for (int k = 0; k < W; ++k) {
+        const int j = col.get(s_ct, rb, C, k, c);
+        if (j < C) y += val0[(long)k * C + c] * (omega * (T)(v.r[j] - alpha * v.q[j]) / D0[j]);
+      }
     }
     x0[c] = xc;
     res0[c] = bc - y;
@@ -947,6 +964,18 @@ void build_ell(Ctx& x) {
   x.ell.nb = (int)brow.size();
   if (brow.empty()) brow.push_back(0);
   x.ell.bflag.upload(bflag, x.stream);
+  {   // coupled slots per cell (the ELL's slot entries, ascending slot index) and their columns (FaceOp)
+    std::vector<int> cs(C + 1, 0), sl, scol(std::max(x.B, 1), 0);
+    for (int c = 0; c < C; ++c) {
+      for (auto& e : ent[c])
+        if (e.second < 0 && e.second != PAD) { sl.push_back(-e.second - 1); scol[-e.second - 1] = e.first; }
+      cs[c + 1] = (int)sl.size();
+    }
+    if (sl.empty()) sl.push_back(0);
+    x.ell.csStart.upload(cs, x.stream);
+    x.ell.csSlot.upload(sl, x.stream);
+    x.ell.scol.upload(scol, x.stream);
+  }
   x.ell.brow.upload(brow, x.stream);
   // hex box in blockMesh order (MeshView::hx, each_face<-1>): nx and nx ny from the face offsets, then every
   // cell's face entries checked against the computed walk (same faces, storage indices, order)
@@ -1236,8 +1265,18 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, 0); }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());
+  // the symmetric p operator read face-wise on a hex box (FaceOp, one rank; DFMI_P_FACEFORM=0: the ELL values)
+  const bool face = [&] {
+    const char* e = std::getenv("DFMI_P_FACEFORM");
+    return x.hex[0] > 0 && x.fslot && x.nranks == 1 && !halo_active(x) && !small_solve(x) && !(e && std::atoi(e) == 0);
+  }();
+  FaceOp<double> fo{};
+  if (face) fo = FaceOp<double>{1, x.hex[0], x.hex[1], x.hex[2], C, upper, bc, x.ell.csStart.p, x.ell.csSlot.p,
+                                x.ell.scol.p};
   if (amg) {
     if (!x.amg.ready) amg_setup(x);
+    x.amg.face = face && amg_l0_fusable(x) && x.amg.l0_sweeps == 1;
+    x.amg.dfo = fo;
     amg_galerkin(x, val, v.dS);
     if (x.amg.halo_l0) {   // the level-0 diagonal across processor faces, once per solve
       halo_vecs(x, {v.dS}, 1, Ce);
@@ -1268,7 +1307,8 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   dispatch_W(W, [&](auto wt) {
     constexpr int WT = decltype(wt)::value;
     KScope _ks(x, "k_cg_init");
-    hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, v, q2);
+    if (face) hipLaunchKernelGGL((k_cg_init<0, true>), g, bl, 0, x.stream, C, W, x.ell.cols(), val, v, q2, fo);
+    else hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, v, q2, fo);
   });
   DFMI_HIP(hipGetLastError());
   // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
@@ -1311,8 +1351,12 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_cg_spmv");
-        hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, it, cfg.max_iter, cfg.tol,
-                           cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1, rs);
+        if (face)
+          hipLaunchKernelGGL((k_cg_spmv<0, true>), g, bl, 0, x.stream, C, W, x.ell.cols(), val, it, cfg.max_iter,
+                             cfg.tol, cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1, rs, fo);
+        else
+          hipLaunchKernelGGL(k_cg_spmv<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, it, cfg.max_iter, cfg.tol,
+                             cfg.abs_tol, red_rz, red_rr, WS.scal.p, v, pold, pnew, q1, rs, fo);
       });
     });
     if (it >= cfg.max_iter) break;
@@ -1322,9 +1366,14 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_cg_x_smooth");   // its own timer name: tests assert the fused path ran
-        hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p, xsol, v,
-                           pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
-                           l0.fx.p, l0.fr.p);
+        if (x.amg.face)
+          hipLaunchKernelGGL((k_cg_x_smooth<0, float, true>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p,
+                             xsol, v, pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
+                             l0.fx.p, l0.fr.p, x.amg.ffo);
+        else
+          hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p, xsol,
+                             v, pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
+                             l0.fx.p, l0.fr.p, x.amg.ffo);
       });
       DFMI_HIP(hipGetLastError());
       std::swap(v.r, v.z);   // z was dead (k_cg_spmv has read it); the V-cycle writes the new z over the old r

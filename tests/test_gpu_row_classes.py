@@ -65,3 +65,14 @@ def test_hex_face_walk_bitwise_explicit_rows(periodic):
     assert a["iters"] == b["iters"] == c["iters"], (a["iters"], b["iters"], c["iters"])
     for k in ("p", "T", "rho", "he", "U", "Y"):
         assert np.array_equal(a[k], b[k]) and np.array_equal(a[k], c[k]), k
+
+
+@pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "walls"])
+def test_face_form_pressure_operator_bitwise_ell(periodic):
+    """the symmetric p operator read face-wise (FaceOp: PCG SpMVs and the fp32 AMG level 0 from the face and
+    slot coefficients) against the ELL values: the same entries in the same order, so bitwise"""
+    a = _run(1, periodic)
+    b = _run(1, periodic, {"DFMI_P_FACEFORM": "0"})
+    assert a["iters"] == b["iters"], (a["iters"], b["iters"])
+    for k in ("p", "T", "rho", "he", "U", "Y"):
+        assert np.array_equal(a[k], b[k]), k
