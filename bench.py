@@ -36,7 +36,7 @@ MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species 
 
 
 def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = None, W: int = 6,
-                      classes: bool = False, hex_walk: bool = False) -> float:
+                      classes: bool = False, hex_walk: bool = False, face_form: bool = False) -> float:
     """Bytes one unit of a kernel's work must move at minimum: every input element read once and every
     output element written once (fp64 values, int32 indices, int8 slot types), shared face/cell arrays
     counted ONCE per launch however many species use them. Units: one launch for the assembly/thermo
@@ -47,7 +47,8 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
     classes: the solver rows are decoded from row classes (dfmi_row_classes > 0), so the solver matrices'
     8 B of owner/neighbour ids per face become 1 B per cell. hex_walk: the assembly kernels compute their
     face and neighbour indices (dfmi_hex_dims), so only cbStart (4 B per cell) and the coupled slots'
-    9 B remain of the topology."""
+    9 B remain of the topology. face_form: the PCG reads the symmetric p operator face-wise (FaceOp): one
+    coefficient per face (8 B) and the coupled-slot list (4 B per cell) instead of both ELL halves."""
     Sa = S - 1                                     # solved species (inert excluded)
     Bc = B if Bc is None else Bc
     topo = (4.0 * C + 9.0 * Bc) if hex_walk else (12.0 * C + 12.0 * F + 9.0 * Bc)
@@ -78,6 +79,8 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
     if kernel == "k_u_hbya":
         # U (3), source (3), V in; HbyA (3) out; faces lower, upper; slots internal/boundaryCoeffs (3 each)
         return C * 56.0 + C * 24.0 + F * 16.0 + Bc * 48.0 + topo
+    if kernel == "k_cg_spmv" and face_form:
+        return C * 40.0 + C * 4.0 + F * 8.0 + Bc * 12.0
     if kernel == "k_cg_spmv":
         # fused PCG step p = z + beta p_old; q = A p: cells z, p_old, dS in, p, q out (40 B);
         # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
@@ -629,7 +632,8 @@ def main():
         # computed hex walk), the floor of this implementation's traffic
         per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc)
         per_impl = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc, classes=ncls > 0,
-                                     hex_walk=hexw)
+                                     hex_walk=hexw, face_form=hexw and world == 1
+                                     and os.environ.get("DFMI_P_FACEFORM", "1") != "0")
         total_bytes = per_unit * units[k]
         total_impl = per_impl * units[k]
         if k == "k_bcg_spmv":   # U's three components share one operator: its bytes count once per three systems
