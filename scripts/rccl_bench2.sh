@@ -1,17 +1,21 @@
 #!/bin/bash
-# bench.py --gpus 2 under torchrun on the box's one GPU over RCCL's socket transport (DFMI_RCCL_SPLIT_HOSTS),
-# halo overlap off and on: a functional check of the multi-GPU bench path and of the overlap's effect when
-# the wire is slow (not a scaling measurement).
+# bench.py --gpus 2 under torchrun on the box's one GPU over RCCL's socket transport (DFMI_RCCL_SPLIT_HOSTS):
+# a functional check of the multi-GPU bench path (not a scaling measurement) for the settings in VARS
+# ("name:ENV=V,ENV=V ..."; default: the halo-coupled AMG level 0 on and off).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for ov in 0 1; do
-  DFMI_HALO_OVERLAP=$ov DFMI_RCCL_SPLIT_HOSTS=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port $((29555 + ov)) bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-flame \
-    > gpurun_out/bench_rccl2_ov$ov.log 2>&1
-  rc=$?; echo "overlap $ov rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  python3 - "$ov" <<'PY'
+port=29555
+for v in ${VARS:-halo: bj:DFMI_AMG_HALO_L0=0}; do
+  name="${v%%:*}"; envs="${v#*:}"; port=$((port + 1))
+  ( for e in $(echo "$envs" | tr ',' ' '); do export "$e"; done
+    DFMI_RCCL_SPLIT_HOSTS=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-flame \
+      --alt-steps 0 > gpurun_out/bench_rccl2_$name.log 2>&1 )
+  rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python3 - "$name" <<'PY'
 import json, sys
-d = json.loads(open(f"gpurun_out/bench_rccl2_ov{sys.argv[1]}.log").read().strip().splitlines()[-1])
-print("overlap", sys.argv[1], round(d["ms_per_step"], 2), "ms/step", d["solver_iters"])
+d = json.loads([l for l in open(f"gpurun_out/bench_rccl2_{sys.argv[1]}.log") if l.startswith("{")][-1])
+print(sys.argv[1], round(d["ms_per_step"], 2), "ms/step", d["solver_iters"], "levels", d["amg_levels"][-2:],
+      "hex", d.get("hex_face_walk"), "classes", d.get("row_classes"))
 PY
 done
