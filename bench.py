@@ -611,7 +611,8 @@ def main():
             # moving < 1 % of the largest one's bytes are other workloads' (the 1D flame line's W = 2)
             ent = [v for key, v in tab.items()
                    if key.split("::")[-1].split("<")[0].rstrip("12") == fam or key.split("::")[-1].startswith(fam + "<")
-                   or key.split("::")[-1].split("(")[0] == fam + "_cell"]   # k_p_face's cell-walk form
+                   or key.split("::")[-1].split("(")[0] == fam + "_cell"   # k_p_face's cell-walk form
+                   or key.split("::")[-1].startswith(fam + "_brick<")]     # k_y_prep's LDS-staged form
             if not ent:
                 continue
             top = max(v["hbm_bytes_mean"] for v in ent)
