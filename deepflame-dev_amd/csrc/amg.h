@@ -33,6 +33,7 @@ struct Amg {
   int coarse_sweeps = 8;
   int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
   bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)
+  bool tail = false;       // levels L-2 and L-1 of the fp32 V-cycle in one workgroup (k_vtail)
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;

@@ -382,6 +382,99 @@ __global__ void __launch_bounds__(CTPB) k_coarsest(int n, int W, const int* __re
   for (int c = threadIdx.x; c < n; c += CTPB) x[c] = (TO)cur[c];
 }
 
+// The V-cycle's tail in ONE workgroup (Amg::tail): the padded level t = L - 2 (n <= TAIL_N cells, its rows
+// held in registers, four cells per thread, its vectors in LDS), its restriction, the coarsest level's sweeps
+// (LDS-resident as k_coarsest) and level t's prolongation + post-sweep -- the work of k_smooth_res_r8 +
+// k_coarsest + k_prolong_smooth on those levels, with their expressions in their order, so the corrected
+// level-t iterate written to xo is bitwise theirs. Three launches of ~6-8 us (latency: a few dependent
+// loads each, no bandwidth to speak of on <= 4096 cells) become one.
+constexpr int TAIL_N = 4096, TAIL_W = 8;
+template <int WT, class T>
+__global__ void __launch_bounds__(CTPB) k_vtail(int n, int W_, const int* __restrict__ col, const T* __restrict__ val,
+                                                const T* __restrict__ D, const T* __restrict__ b, int nc, int Wc,
+                                                const int* __restrict__ colc, const T* __restrict__ valc,
+                                                const T* __restrict__ Dc, T omega, T sc, int sweeps,
+                                                T* __restrict__ xo, const double* act) {
+  if (act && *act == 0.0) return;   // uniform
+  const int W = WT > 0 ? WT : W_;
+  constexpr int Q = TAIL_N / CTPB;
+  __shared__ T sb[TAIL_N], sD[TAIL_N], sx[TAIL_N];
+  __shared__ T xa[COARSEST], xb[COARSEST], sdc[COARSEST], sbc[COARSEST];
+  __shared__ T sv[LDS_ENT];
+  __shared__ int scl[LDS_ENT];
+  const int tid = threadIdx.x;
+  int cj[Q][TAIL_W];
+  T cv[Q][TAIL_W];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = q * CTPB + tid;
+    if (c >= n) continue;
+    sb[c] = b[c];
+    sD[c] = D[c];
+#pragma unroll
+    for (int k = 0; k < TAIL_W; ++k)
+      if (k < W) { cj[q][k] = col[(long)k * n + c]; cv[q][k] = val[(long)k * n + c]; }
+  }
+  for (int e = tid; e < nc * Wc; e += CTPB) { sv[e] = valc[e]; scl[e] = colc[e]; }
+  for (int c = tid; c < nc; c += CTPB) sdc[c] = Dc[c];
+  __syncthreads();
+  // down: one sweep from zero + residual, summed over each aligned group of 8 (k_smooth_res_r8)
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = q * CTPB + tid;
+    if (c >= n) continue;   // n % 8 == 0: a group of 8 lanes runs or skips together
+    const T bc = sb[c];
+    const T xc = omega * bc / sD[c];
+    T y = sD[c] * xc;
+#pragma unroll
+    for (int k = 0; k < TAIL_W; ++k) {
+      if (k >= W) break;
+      const int j = cj[q][k];
+      if (j < n) y += cv[q][k] * (omega * sb[j] / sD[j]);
+    }
+    sx[c] = xc;
+    const T r = bc - y;
+    T s = 0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) s += __shfl(r, m, 8);
+    if ((tid & 7) == 0) sbc[c >> 3] = s;
+  }
+  __syncthreads();
+  // coarsest: weighted-Jacobi sweeps from zero (k_coarsest)
+  for (int c = tid; c < nc; c += CTPB) xa[c] = omega * sbc[c] / sdc[c];
+  __syncthreads();
+  T* cur = xa;
+  T* nxt = xb;
+  for (int s = 1; s < sweeps; ++s) {
+    for (int c = tid; c < nc; c += CTPB) {
+      T y = sdc[c] * cur[c];
+      for (int k = 0; k < Wc; ++k) {
+        const int j = scl[k * nc + c];
+        if (j < nc) y += sv[k * nc + c] * cur[j];
+      }
+      nxt[c] = cur[c] + omega * (sbc[c] - y) / sdc[c];
+    }
+    __syncthreads();
+    T* t = cur; cur = nxt; nxt = t;
+  }
+  // up: y = x0 + sc P xc (aggregate of a padded cell: c >> 3), one post-sweep (k_prolong_smooth)
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = q * CTPB + tid;
+    if (c >= n) continue;
+    const T yc = sx[c] + sc * cur[c >> 3];
+    T ay = sD[c] * yc;
+#pragma unroll
+    for (int k = 0; k < TAIL_W; ++k) {
+      if (k >= W) break;
+      const int j = cj[q][k];
+      if (j < n) ay += cv[q][k] * (sx[j] + sc * cur[j >> 3]);
+    }
+    const T bc = sb[c];
+    xo[c] = yc + omega * (bc - ay) / sD[c];
+  }
+}
+
 // ---------------------------------------------------------------- agglomerated coarsest level (Amg::global)
 // rank's packed rows (nmax rows of wg values + the diagonal): local coarsest couplings (slots < wloc of the
 // level's own ELL; up to wc), the external couplings summed in double from the level-0 halo coefficients
@@ -816,6 +909,14 @@ void amg_setup(Ctx& x) {
   a.halo_l0 = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_HALO_L0", 1) != 0 && a.lv.size() >= 2 &&
               a.l0_sweeps == 1 && a.fused_coarse == 0 && a.coop_blocks == 0 && !a.use_graph;
   if (a.halo_l0) a.hy.alloc((size_t)C + x.H);
+  // the last two levels as one single-workgroup launch (k_vtail; DFMI_AMG_TAIL=0: the launch chain)
+  {
+    const int L = (int)a.lv.size();
+    a.tail = env_d("DFMI_AMG_TAIL", 1) != 0 && a.padded && a.fp32 && L >= 3 && a.lv[L - 2].n <= TAIL_N &&
+             a.lv[L - 2].n % 8 == 0 && a.lv[L - 2].W <= TAIL_W && a.lv[L - 1].n <= COARSEST &&
+             (size_t)a.lv[L - 1].n * a.lv[L - 1].W <= LDS_ENT && !a.global && a.coop_blocks == 0 &&
+             a.fused_coarse == 0;
+  }
   a.ready = true;
 }
 
@@ -944,8 +1045,11 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     DFMI_HIP(hipGetLastError());
     return;
   }
+  // the last two levels in one workgroup (k_vtail): the down loop stops above level L - 2
+  const bool tail = F && a.tail;
+  const int ldown = tail ? L - 2 : L - 1;
   // down: smooth from zero + residual, restrict
-  for (int l = 0; l + 1 < L; ++l) {
+  for (int l = 0; l < ldown; ++l) {
     AmgLevel& f = a.lv[l];
     const dim3 g(blocks_for(f.n, TPB));
     if ((l > 0 && a.fused_coarse >= 1) || a.fused_coarse >= 2) {   // one launch per level instead of two
@@ -1001,7 +1105,22 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   // smoothed redundantly), or this rank's own coarsest level
   T* gx = nullptr;
   if constexpr (F) gx = a.g_fx.p; else gx = a.g_x.p;
-  if (a.global && L > 1) {
+  if (tail) {
+    AmgLevel& f = a.lv[L - 2];
+    AmgLevel& c = a.lv[L - 1];
+    KScope _ks(x, "k_vtail");
+    if constexpr (!F) DFMI_CHECK(false, "k_vtail: fp32 V-cycle only");
+    else if (f.W == 6)
+      hipLaunchKernelGGL((k_vtail<6, T>), dim3(1), dim3(CTPB), 0, x.stream, f.n, f.W, RAW(L - 2), VAL(L - 2), DD(L - 2),
+                         (const T*)BV(L - 2), c.n, c.W, RAW(L - 1), VAL(L - 1), DD(L - 1), om, sc, a.coarse_sweeps,
+                         XO(L - 2), act);
+    else
+      hipLaunchKernelGGL((k_vtail<0, T>), dim3(1), dim3(CTPB), 0, x.stream, f.n, f.W, RAW(L - 2), VAL(L - 2), DD(L - 2),
+                         (const T*)BV(L - 2), c.n, c.W, RAW(L - 1), VAL(L - 1), DD(L - 1), om, sc, a.coarse_sweeps,
+                         XO(L - 2), act);
+    // the corrected iterate of level L - 2 feeds the next finer prolongation (as after k_prolong_smooth)
+    if constexpr (F) std::swap(f.fx, f.fxo); else std::swap(f.x, f.xo);
+  } else if (a.global && L > 1) {
     KScope _ks(x, "k_coarsest");
     hipLaunchKernelGGL(k_gc_bpack<T>, dim3(blocks_for(a.nmax, TPB)), dim3(TPB), 0, x.stream, a.nmax, a.nloc,
                        (const T*)BV(L - 1), a.g_bs.p);
@@ -1029,7 +1148,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     hipLaunchKernelGGL(k_dot_partial, dim3(nblk), dim3(TPB), 0, x.stream, x.C, r, (const double*)z, partial);
   }
   // up: prolongate the coarse correction + one smoothing sweep
-  for (int l = L - 2; l >= 0; --l) {
+  for (int l = tail ? L - 3 : L - 2; l >= 0; --l) {
     AmgLevel& f = a.lv[l];
     KScope _ks(x, "k_prolong_smooth");
     if (l == 0 && a.halo_l0) {   // prolongate, exchange the iterate, post-sweep with the processor columns
