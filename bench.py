@@ -652,7 +652,7 @@ def main():
                     "bytes_per_unit": per_unit, "avg_us": ms * 1e3 / nl, "total_ms": ms,
                     "impl_bytes": total_impl / nl, "frac_impl": achieved_impl / HBM_PEAK_GBS}
     hbm = {k: v for k, v in roofs.items() if v["bound"] == "hbm"}
-    primary = args.kernel if args.kernel != "auto" else max(hbm, key=lambda k: hbm[k]["total_ms"])
+    primary = args.kernel if args.kernel != "auto" else (max(hbm, key=lambda k: hbm[k]["total_ms"]) if hbm else None)
     out = {
         "metric": "cell-updates/s (dfLowMachFoam outer iter)",
         "value": value,
@@ -678,7 +678,7 @@ def main():
                    "traversal": args.traversal,
                    "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
                    else "single"},
-        "roofline": dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "
+        "roofline": None if primary is None else dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "
                          "WRITE_SIZE passes, mean per dispatch, gfx950 read correction)",
                          note=f"achieved = algorithmic bytes of the work done (active systems/iterations; SURVEY 8(d): "
                               f"int32 ids per face counted) / summed HIP-event kernel time over {args.roof_steps} extra "
@@ -716,7 +716,7 @@ def main():
         "finite": finite,
         "other_schemes": alt,
     }
-    if world == 1:   # the headline kernel against a measured copy peak as well as the datasheet's
+    if world == 1 and out["roofline"] is not None:   # the headline kernel against a measured copy peak as well
         peak_copy = ctx.hbm_copy_peak(4.0, 20)     # dfmi_hbm_copy_peak: 16-B vector streaming copy
         out["roofline"]["measured_copy_peak_GBs"] = peak_copy
         out["roofline"]["frac_of_measured_copy_peak"] = out["roofline"]["achieved"] / peak_copy
