@@ -34,10 +34,6 @@ struct Amg {
   int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
   bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)
   bool tail = false;       // levels L-2 and L-1 of the fp32 V-cycle in one workgroup (k_vtail)
-  // level 0's aggregates are the aligned 2x2x2 bricks of a one-rank hex box, numbered in member order: the
-  // fused PCG update (k_cg_x_smooth) visits cells brick by brick (BrickMap) and restricts to level 1 itself
-  bool brick0 = false;
-  BrickMap bmap;
   int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;

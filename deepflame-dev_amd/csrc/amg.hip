@@ -641,26 +641,6 @@ double env_d(const char* k, double d) { const char* v = std::getenv(k); return v
 // inside an aggregate is unchanged, so every restriction sums the same values in the same order.
 // On return fin_aggs / last_col hold the final fine -> coarse maps and the coarsest level's columns (they
 // are left untouched when the levels stay plain).
-// BrickMap of level 0 (Amg::brick0) when its aggregates are exactly the aligned 2x2x2 bricks of a one-rank hex box
-// with even dimensions, each listed in the brick's member order (ascending cell index); otherwise off
-BrickMap brick_map(const Ctx& x, const AmgCoarse& r) {
-  const int nx = x.hex[0], ny = x.hex[1], nz = x.hex[2];
-  if (nx <= 0 || x.nranks != 1 || nx % 2 || ny % 2 || nz % 2 || (long)nx * ny * nz != (long)r.agg.size()) return {};
-  const int nxy = nx * ny;
-  for (int k = 0; k < nz; k += 2)
-    for (int j = 0; j < ny; j += 2)
-      for (int i = 0; i < nx; i += 2) {
-        const int c0 = i + nx * j + nxy * k;
-        const int I = r.agg[c0];
-        if (r.mstart[I + 1] - r.mstart[I] != 8) return {};
-        for (int m = 0; m < 8; ++m) {
-          const int c = c0 + (m & 1) + nx * ((m >> 1) & 1) + nxy * (m >> 2);
-          if (r.agg[c] != I || r.members[r.mstart[I] + m] != c) return {};
-        }
-      }
-  return BrickMap{1, nx, ny};
-}
-
 void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vector<int>>& aggs,
                 std::vector<std::vector<int>>& fin_aggs, std::vector<int>& last_col) {
   Amg& a = x.amg;
@@ -694,7 +674,6 @@ void pad_levels(Ctx& x, const std::vector<int>& col0, const std::vector<std::vec
     amg_level_data(fcol, Wf, nf, nn[l + 1], r);
     AmgLevel& f = a.lv[l];
     AmgLevel& c = a.lv[l + 1];
-    if (l == 0) a.bmap = brick_map(x, r);
     f.agg.upload(r.agg, x.stream);
     f.mstart.upload(r.mstart, x.stream);
     f.members.upload(r.members, x.stream);
@@ -905,7 +884,6 @@ void amg_setup(Ctx& x) {
   DFMI_CHECK(!too_big(a.lv.back()) || a.lv.back().n <= 8, "AMG coarsening stalled above the coarsest-level capacity");
   a.padded = false;
   a.global = false;
-  a.bmap = BrickMap{};
   std::vector<std::vector<int>> fin_aggs = aggs;
   std::vector<int> last_col = fcol;
   if (env_d("DFMI_AMG_PADDED", 1) != 0) pad_levels(x, col, aggs, fin_aggs, last_col);
@@ -931,9 +909,6 @@ void amg_setup(Ctx& x) {
   a.halo_l0 = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_HALO_L0", 1) != 0 && a.lv.size() >= 2 &&
               a.l0_sweeps == 1 && a.fused_coarse == 0 && a.coop_blocks == 0 && !a.use_graph;
   if (a.halo_l0) a.hy.alloc((size_t)C + x.H);
-  // measured: k_cg_x_smooth 43 -> 60 us for the 8 us k_restrict it saves (the brick sums land as scattered 4-B
-  // stores in the renumbered level 1), so opt-in: DFMI_AMG_BRICK0=1
-  a.brick0 = a.bmap.on && a.padded && a.fp32 && a.lv.size() >= 2 && env_d("DFMI_AMG_BRICK0", 0) != 0;
   // the last two levels as one single-workgroup launch (k_vtail; DFMI_AMG_TAIL=0: the launch chain)
   {
     const int L = (int)a.lv.size();
@@ -1120,7 +1095,7 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
         std::swap(rcur, ralt);
       }
     }
-    if (!(l == 0 && l0_done && a.brick0)) {   // (brick0: the fused PCG update restricted level 0 already)
+    {
       KScope _ks(x, "k_restrict");
       hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
                          f.mstart.p, f.members.p, (const T*)rcur, BV(l + 1), act);

@@ -158,16 +158,4 @@ template <class T, class FN> __device__ __forceinline__ void face_row(const Face
   }
 }
 
-// Level-0 visiting order of the PCG update on a hex box whose AMG level 0 aggregates are the aligned 2x2x2
-// bricks (amg.hip: pad_levels checks): slot t -> cell with the brick's 8 cells on 8 consecutive lanes in
-// member order (x fastest, then y, then z), bricks in blockMesh order -- so the restriction to level 1 is an
-// 8-lane sum inside the kernel. on == 0: slot t is cell t.
-struct BrickMap { int on = 0, nx = 0, ny = 0; };
-__device__ __forceinline__ int brick_cell(const BrickMap& b, int t) {
-  if (!b.on) return t;
-  const int m = t & 7, q = t >> 3, hx = b.nx >> 1, hy = b.ny >> 1;
-  const int bx = q % hx, r = q / hx, by = r % hy, bz = r / hy;
-  return (2 * bx + (m & 1)) + b.nx * ((2 * by + ((m >> 1) & 1)) + b.ny * (2 * bz + (m >> 2)));
-}
-
 }  // namespace dfmi

@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(TPB) k_cg_spmv(long C, int W, ColView col,
 // preconditioner also z = r / dS (AMG computes z separately and writes r.z itself)
 template <bool JAC>
 __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, double* __restrict__ x, CV v,
-                                              const double* __restrict__ pnew, double* partial, BrickMap bm) {
+                                              const double* __restrict__ pnew, double* partial) {
   if (scal[6] == 0.0) return;
   double pv[1];
   red_sum<1>(red, 0, pv);
@@ -446,8 +446,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
   const double alpha = pv[0] != 0.0 ? rz / pv[0] : 0.0;
   if (leader()) { scal[2] = alpha; scal[1] = rz; }
   double acc[2] = {0.0, 0.0};
-  for (int t = xcd_block() * blockDim.x + threadIdx.x; t < C; t += gridDim.x * blockDim.x) {
-    const int c = brick_cell(bm, t);   // the visiting order of k_cg_x_smooth, so the partials are its
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
     const double rr = v.r[c] - alpha * v.q[c];
     v.r[c] = rr;
@@ -466,16 +465,13 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
 // V-cycle's right-hand side, so the same pass forms x0 = omega r / D and res = r - A x0 in the V-cycle's
 // precision T; a neighbour's r_j is re-formed as r_j - alpha q_j (the expression the update stores), so
 // x0 and res are bitwise those of k_smooth_res on the stored r. Partials (0, r.r) as k_cg_x<false>.
-// bm.on (Amg::brick0): cells visited brick by brick, and the residual restricted to level 1 here -- the 8-lane
-// sum in member order that k_restrict forms -- into b1[agg0[c]] instead of being stored.
 template <int WT, class T, bool FF = false>
 __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col, Red red,
                                                      double* scal, double* __restrict__ x, CV v,
                                                      const double* __restrict__ pnew, double* __restrict__ rnew,
                                                      double* partial, const T* __restrict__ val0,
                                                      const T* __restrict__ D0, T omega, T* __restrict__ x0,
-                                                     T* __restrict__ res0, FaceOp<T> fo, BrickMap bm,
-                                                     T* __restrict__ b1, const int* __restrict__ agg0) {
+                                                     T* __restrict__ res0, FaceOp<T> fo = {}) {
   if (scal[6] == 0.0) return;
   double pv[1];
   red_sum<1>(red, 0, pv);
@@ -486,9 +482,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
   __shared__ int s_ct[CT_MAX];
   if (!FF) col.stage(s_ct);
   double acc[2] = {0.0, 0.0};
-  // (bm.on: C % 8 == 0 and the stride is a multiple of 8, so a brick's 8 lanes run every iteration together)
-  for (int t = xcd_block() * blockDim.x + threadIdx.x; t < C; t += gridDim.x * blockDim.x) {
-    const int c = brick_cell(bm, t);
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
     const double rr = v.r[c] - alpha * v.q[c];
     rnew[c] = rr;   // not in place: neighbours read the old r
@@ -509,15 +503,7 @@ __global__ void __launch_bounds__(TPB) k_cg_x_smooth(long C, int W_, ColView col
       }
     }
     x0[c] = xc;
-    const T rs = bc - y;
-    if (bm.on) {
-      T sum = 0;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) sum += __shfl(rs, m, 8);
-      if ((t & 7) == 0) b1[agg0[c]] = sum;
-    } else {
-      res0[c] = rs;
-    }
+    res0[c] = bc - y;
   }
   block_partials<2>(acc, partial, 0);
 }
@@ -1360,8 +1346,6 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   // one rank: the update kernel also does the V-cycle's level-0 first sweep (DFMI_CG_FUSE=0: separate)
   const bool fuse_l0 = amg && x.nranks == 1 && !halo_active(x) && amg_l0_fusable(x) && [] {
     const char* e = std::getenv("DFMI_CG_FUSE"); return !(e && std::atoi(e) == 0); }();
-  // level-0 bricks (Amg::brick0): the update visits cells brick by brick, fused or not (the same partials)
-  const BrickMap bm = (amg && x.amg.brick0 && x.nranks == 1 && !halo_active(x)) ? x.amg.bmap : BrickMap{};
   for (int it = 0;; ++it) {
     const int np = spmv_with_halo(x, {v.z, pold}, 1, Ce, nblk, [&](RowSet rs) {
       dispatch_W(W, [&](auto wt) {
@@ -1385,11 +1369,11 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
         if (x.amg.face)
           hipLaunchKernelGGL((k_cg_x_smooth<0, float, true>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p,
                              xsol, v, pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
-                             l0.fx.p, l0.fr.p, x.amg.ffo, bm, x.amg.lv[1].fb.p, (const int*)l0.agg.p);
+                             l0.fx.p, l0.fr.p, x.amg.ffo);
         else
           hipLaunchKernelGGL((k_cg_x_smooth<WT, float>), g, bl, 0, x.stream, C, W, x.ell.cols(), red, WS.scal.p, xsol,
                              v, pnew, v.z, q2, (const float*)l0.fval.p, (const float*)l0.fD.p, (float)x.amg.omega,
-                             l0.fx.p, l0.fr.p, x.amg.ffo, bm, x.amg.lv[1].fb.p, (const int*)l0.agg.p);
+                             l0.fx.p, l0.fr.p, x.amg.ffo);
       });
       DFMI_HIP(hipGetLastError());
       std::swap(v.r, v.z);   // z was dead (k_cg_spmv has read it); the V-cycle writes the new z over the old r
@@ -1403,8 +1387,8 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     }
     {
       KScope _ks(x, "k_cg_x");
-      if (amg) hipLaunchKernelGGL(k_cg_x<false>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2, bm);
-      else hipLaunchKernelGGL(k_cg_x<true>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2, BrickMap{});
+      if (amg) hipLaunchKernelGGL(k_cg_x<false>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
+      else hipLaunchKernelGGL(k_cg_x<true>, g, bl, 0, x.stream, C, red, WS.scal.p, xsol, v, pnew, q2);
     }
     DFMI_HIP(hipGetLastError());
     reds(red_rz, red_rr, WS.scal.p + 6);
