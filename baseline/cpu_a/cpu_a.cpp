@@ -326,7 +326,7 @@ Stats bicgstab(const Sys& A, const double* b, double* xv, const SolverCfg& cfg) 
 }
 
 // ---- AMG (hierarchy from csrc/amg_graph.h, V-cycle as amg.hip's, fp64)
-constexpr double AMG_OMEGA = 0.85, AMG_OVERCORR = 1.35;
+constexpr double AMG_OMEGA = 0.9, AMG_OVERCORR = 1.35;
 constexpr int AMG_COARSE_SWEEPS = 8, AMG_COARSEST = 512;
 
 void amg_setup(Ctx& x) {

@@ -28,7 +28,7 @@ struct AmgLevel {
 struct Amg {
   bool ready = false;
   bool fp32 = true;
-  double omega = 0.85;
+  double omega = 0.9;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)
   int coarse_sweeps = 8;
   int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
