@@ -86,9 +86,14 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
         # matrix: per internal face lower/upper values + owner/neighbour ids (24 B, LDU minimum; the
         # ELL gather stores the same 2 x 12 B per face from the two cells' sides); coupled slots 12 B
         return C * 40.0 + mat + Bc * 12.0
-    if kernel == "k_bcg_spmv":
+    if kernel in ("k_bcg_spmv", "k_bcg_eo"):
         # mean of the two SpMVs of an iteration: v = A p reads dS, p, r0, writes v (32 B / cell);
-        # t = A s with s = r - alpha v formed on the fly reads dS, r, v, r0, writes t (40 B); matrix as above
+        # t = A s with s = r - alpha v formed on the fly reads dS, r, v, r0, writes t (40 B); matrix as above.
+        # k_bcg_eo (even-odd reduced BiCGStab, k_eo_a..d): one application of the Schur complement S = two
+        # half-row passes over the whole operator once; per iteration its four passes read dS twice (16 B),
+        # move 56 B of vectors per cell (w = H p: p in, w out; v = p - H w: w, p, r0 in, v out; w2 = H s:
+        # r, v in, w2 out; t = s - H w2: w2, r, v, r0 in, t out; each a half-length vector) and read the
+        # operator twice -- 2 x (36 B per cell + matrix), the bytes of the two full SpMVs it replaces
         return C * 36.0 + mat + Bc * 12.0
     if kernel == "k_thermo_cells":
         # T, he, p, Y (S) in; T, he, psi, rho, mu, alpha, rhoD (S), hai (S) out
@@ -96,7 +101,7 @@ def algorithmic_bytes(kernel: str, C: int, F: int, B: int, S: int, Bc: int = Non
     raise KeyError(kernel)
 
 
-SOLVER_KERNELS = ("k_bcg_spmv", "k_cg_spmv")
+SOLVER_KERNELS = ("k_bcg_spmv", "k_bcg_eo", "k_cg_spmv")
 ASSEMBLY_KERNELS = ("k_y_assemble_ell", "k_y_prep", "k_u_grad", "k_u_assemble", "k_e_assemble", "k_u_hbya", "k_p_face")
 ROOF_KERNELS = SOLVER_KERNELS + ASSEMBLY_KERNELS + ("k_thermo_cells",)
 
@@ -620,7 +625,10 @@ def main():
             nd = sum(v["dispatches"] for v in ent)
             pmc[fam] = {"hbm_bytes_mean": sum(v["hbm_bytes_mean"] * v["dispatches"] for v in ent) / nd}
     Bc = m.n_coupled_slots
-    units = {"k_bcg_spmv": 2.0 * (work["U"] + work["Y"] + work["E"]), "k_cg_spmv": work["p"]}
+    # BiCGStab: two operator applications per system-iteration, full SpMVs (k_bcg_spmv) or applications of
+    # the even-odd Schur complement (k_bcg_eo); only one of the two runs
+    units = {"k_bcg_spmv": 2.0 * (work["U"] + work["Y"] + work["E"]), "k_bcg_eo": 2.0 * (work["U"] + work["Y"] + work["E"]),
+             "k_cg_spmv": work["p"]}
     for k in ASSEMBLY_KERNELS + ("k_thermo_cells",):
         units[k] = float(ktime[k][1])              # one unit = one launch
     roofs = {}
@@ -637,7 +645,7 @@ def main():
                                      and os.environ.get("DFMI_P_FACEFORM", "1") != "0")
         total_bytes = per_unit * units[k]
         total_impl = per_impl * units[k]
-        if k == "k_bcg_spmv":   # U's three components share one operator: its bytes count once per three systems
+        if k in ("k_bcg_spmv", "k_bcg_eo"):   # U's three components share one operator: its bytes count once per three systems
             total_bytes -= 2.0 * work["U"] * (2.0 / 3.0) * (24.0 * m.n_faces + 12.0 * Bc)
             total_impl -= 2.0 * work["U"] * (2.0 / 3.0) * ((1.0 * m.n_cells + 16.0 * m.n_faces if ncls > 0 else
                                                              24.0 * m.n_faces) + 12.0 * Bc)

@@ -47,6 +47,10 @@ struct MeshView {
   int hx, hy, hz;
   const int* trav;          // optional traversal order of the per-cell gather kernels (thread t -> cell)
   const double *md, *bdv;   // C[nei] - C[own] [3][F] (face storage) and patch delta vectors [3][B] (limited schemes)
+  // even-odd solver layout (Ctx::Ell::eo): row index of cell c in the BiCGStab rows / vectors (first the
+  // colour-0 cells, then colour-1, each ascending); nullptr: natural order. Only the writers of the
+  // BiCGStab rows (k_ell_build for U/E, k_y_assemble_ell) read it.
+  const int* eopos;
 };
 
 // entry k of cell c's gather row: column j and coefficient source e (2 f + own for the face at storage f,
@@ -232,6 +236,21 @@ struct Ctx {
       if (ncls > 0) { v.cls = cls.p; v.tab = ctab.p; v.ntab = ncls * W; }
       return v;
     }
+    // even-odd (red-black) reduced BiCGStab (linsolve.hip): on a bipartite coupling graph (hex meshes) the
+    // rows are stored colour by colour -- colour-0 cells [0, ne), colour-1 cells [ne, C) -- and the solver
+    // iterates on the colour-1 Schur complement. eo_pos: cell -> row, eo_cell: row -> cell; eo_col: the
+    // ELL columns in row numbering (every entry points into the other colour), with its own row classes
+    int eo = 0, ne = 0;
+    DevBuf<int> eo_pos, eo_cell, eo_col, eo_ctab;
+    DevBuf<uint8_t> eo_cls;
+    int eo_ncls = 0;
+    std::vector<int> h_eo_pos;
+    ColView eo_cols() const {
+      ColView v;
+      v.col = eo_col.p; v.W = W;
+      if (eo_ncls > 0) { v.cls = eo_cls.p; v.tab = eo_ctab.p; v.ntab = eo_ncls * W; }
+      return v;
+    }
   } ell;
   bool halo_overlap = false;     // DFMI_HALO_OVERLAP=1: solver halo exchanges overlap the interior rows
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
@@ -269,6 +288,7 @@ struct Ctx {
     m.trav = trav.n ? trav.p : nullptr;
     m.hx = hex[0]; m.hy = hex[1]; m.hz = hex[2];
     m.md = md.p; m.bdv = bdv.p;
+    m.eopos = ell.ready && ell.eo ? ell.eo_pos.p : nullptr;
     return m;
   }
   double* f(const std::string& name) {

@@ -1471,6 +1471,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
+  const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
   const long C = m.C, B = m.B;
   double d1 = 0.0, d2 = 0.0;
   double dL[S], rc[S];
@@ -1492,7 +1493,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
       const double rn = rhoD[s * C + o2];
       const double UL = dcf * ((own ? interp_f(w, rc[s], rn) : interp_f(w, rn, rc[s])) * ms);
       dL[s] -= UL;
-      val[((long)ss * W + k) * C + c] = own ? Us - UL : Ls - UL;
+      val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
     }
     ++k;
   });
@@ -1519,7 +1520,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
       const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
       const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
       dg[s] += icv;
-      if (cp) val[((long)ss * W + k) * C + c] = -bcv;
+      if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
       else sr[s] += bcv;
     }
     if (cp) ++k;
@@ -1528,9 +1529,9 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
   for (int s = 0; s < S; ++s) {
     if (s == inert) continue;
     const int ss = s < inert ? s : s - 1;
-    for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + c] = 0.0;
-    dS[ss * Ce + c] = dg[s];
-    rhs[ss * Ce + c] = sr[s];
+    for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
+    dS[ss * Ce + pc] = dg[s];
+    rhs[ss * Ce + pc] = sr[s];
   }
 }
 
@@ -1804,6 +1805,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
     const double* __restrict__ bwY) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
+  const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
   const long C = m.C, B = m.B;
   const double vol = m.V[c];
   for (int s0 = 0; s0 < S; s0 += CH) {
@@ -1829,7 +1831,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
         const double rn = rhoD[s * C + o2];
         const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
         dL[j] -= UL;
-        val[((long)ss * W + k) * C + c] = own ? Us - UL : Ls - UL;
+        val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
       }
       ++k;
     });
@@ -1858,7 +1860,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
         const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
         const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
         dg[j] += icv;
-        if (cp) val[((long)ss * W + k) * C + c] = -bcv;
+        if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
         else sr[j] += bcv;
       }
       if (cp) ++k;
@@ -1869,9 +1871,9 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
       if (s >= S) break;
       if (s == inert) continue;
       const int ss = s < inert ? s : s - 1;
-      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + c] = 0.0;
-      dS[ss * Ce + c] = dg[j];
-      rhs[ss * Ce + c] = sr[j];
+      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
+      dS[ss * Ce + pc] = dg[j];
+      rhs[ss * Ce + pc] = sr[j];
     }
   }
 }
