@@ -354,6 +354,7 @@ int dfmi_init_constant_fields_internal(dfmi_ctx* ctx, const double* sf, const do
     x.dc.upload(dd, x.stream);
     x.V.upload(volume, x.C, x.stream);
     DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.have_md = mesh_distance != nullptr;
     x.have_geom = true;
   });
 }
@@ -452,6 +453,8 @@ static void parse_scheme(const std::string& term, const std::string& text, int& 
 int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme) {
   return guard([&] {
     Ctx& x = ctx->x;
+    // the patch kinds (processor patches) are known only after the boundary initialisation
+    DFMI_CHECK(x.have_bgeom, "call dfmi_init_constant_fields_boundary before dfmi_set_scheme");
     const std::string t(term ? term : ""), s(scheme ? scheme : "");
     int kind;
     double k;

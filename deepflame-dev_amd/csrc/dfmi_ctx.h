@@ -186,6 +186,7 @@ struct Ctx {
   double rdt = 0;
   int inert = -1;
   bool have_sizes = false, have_topo = false, have_geom = false, have_bgeom = false;
+  bool have_md = false;           // mesh_distance was given (the limited schemes' d; zeros otherwise)
   std::vector<int> psize, poff, pkind, cyc_nbr, peer;   // pkind: 0 plain, 1 cyclic, 2 processor
   std::vector<int> h_bfc, h_own, h_nei;
   // topology

@@ -485,7 +485,7 @@ __global__ void k_llv_w_slot(MeshView m, const int8_t* __restrict__ ty, double t
   const int t = ty[b];
   const double ph = bphi[b];
   double lim = 1.0;
-  if (bc_coupled(t) && m.sprim[b]) {   // cyclic (processor patches are rejected at dfmi_set_scheme)
+  if (bc_coupled(t) && m.sprim[b] && m.partner[b] >= 0) {   // cyclic (processor patches are rejected on the host)
     const int c = m.bfc[b], pc = m.partner[b];
     const double dv[3] = {m.bdv[b], m.bdv[B + b], m.bdv[2 * B + b]};
     const double vP[3] = {U[c], U[C + c], U[2 * C + c]}, vN[3] = {U[pc], U[C + pc], U[2 * C + pc]};
@@ -2085,7 +2085,7 @@ static void scheme_checks(Ctx& x, bool limited) {
   bool coupled = false;
   for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
   DFMI_CHECK(!limited || !coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");
-  DFMI_CHECK(!limited || x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
+  DFMI_CHECK(!limited || x.have_md, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
 }
 
 void u_assemble(Ctx& x) {
@@ -2097,6 +2097,8 @@ void u_assemble(Ctx& x) {
   halo_fields(x, {"tauU"});   // fvc_grad_vector_correctBC_processor (dfMatrixOpBase.cu:1366-1389)
   if (llv) {   // div(phi,U) limitedLinearV weights from this grad(U)
     scheme_checks(x, true);
+    for (int p = 0; p < x.P; ++p)   // dfmi_set_scheme refuses it too; checked again here, where it is launched
+      DFMI_CHECK(x.pkind[p] != 2, "div(phi,U) limitedLinearV on a decomposed mesh (processor patches) is not supported");
     if (x.fields.count("dbg_gradU"))
       DFMI_HIP(hipMemcpyAsync(x.f("dbg_gradU"), gout, 9 * sizeof(double) * x.C, hipMemcpyDeviceToDevice, x.stream));
     double* w = scheme_buf(x, "U_w", x.Fs, 1, true);
@@ -2250,7 +2252,7 @@ static void e_scheme_terms(Ctx& x) {
     double* g = scheme_buf(x, "gradK", x.C, 3);
     double* bg = scheme_buf(x, "boundary_gradK", x.B, 3);
     if (lim) {
-      DFMI_CHECK(x.md.p, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
+      DFMI_CHECK(x.have_md, "limited schemes need mesh_distance (dfmi_init_constant_fields_internal)");
       bool coupled = false;
       for (int p = 0; p < x.P; ++p) coupled |= x.pkind[p] != 0;
       DFMI_CHECK(!coupled || x.have_bdelta, "limited schemes on a mesh with coupled patches need dfmi_init_boundary_delta");

@@ -88,9 +88,14 @@ int dfmi_init_boundary_delta(dfmi_ctx* ctx, const double* boundary_delta);
  *   "div(phi,Yi_h)"       "upwind" (default) | "limitedLinear <k>" | "limitedLinear01 <k>"  (Yi and he)
  *   "div(phi,K)"          "linear" (default) | "upwind" | "limitedLinear <k>" | "limitedLinear01 <k>"
  *   "div(hDiffCorrFlux)"  "linear" (default) | "cubic"
+ *   "div(phi,U)"          "linear" (default) | "limitedLinearV <k>"  (the 1D flame, test/Tu500K-Phi1/system/fvSchemes)
  * a leading "Gauss" is accepted, e.g. the reference cases' "Gauss limitedLinear01 1" / "Gauss cubic"
- * (test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver/system/fvSchemes:32-40). Limited schemes on
- * decomposed meshes (processor patches) are an error for div(phi,Yi_h). */
+ * (test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver/system/fvSchemes:32-40). Call it after
+ * dfmi_init_constant_fields_boundary (the patch kinds must be known). On decomposed meshes (processor
+ * patches) every term's schemes are supported except div(phi,U) limitedLinearV, which is an error (here
+ * and again when the UEqn is assembled). Limited schemes need the mesh_distance argument of
+ * dfmi_init_constant_fields_internal (a NULL there makes them an error at the first assembly) and, on
+ * meshes with coupled patches, dfmi_init_boundary_delta. */
 int dfmi_set_scheme(dfmi_ctx* ctx, const char* term, const char* scheme);
 
 /* ---- cell renumbering (the role of OpenFOAM's renumberMesh; run once on the host before

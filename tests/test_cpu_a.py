@@ -100,7 +100,7 @@ def test_default_solvers_converge_and_amg_beats_jacobi():
     assert rel <= 1e-5 and it_amg > 0
     for e in ("U", "Y", "E"):
         it, r0, rel = ctx.solver_stats(e)
-        assert rel <= 1e-5 or it == 20, e
+        assert rel <= 1e-5 and 0 < it < 20, (e, it, rel)   # converged inside the AmgX limit (amgxUOptions: 20)
     from dfmi import case
     case.push_state(ctx, st)
     ctx.set_preconditioner("p", "jacobi")

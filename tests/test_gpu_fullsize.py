@@ -1,5 +1,6 @@
 """BASELINE config 3 at its full size (128^3 = 2,097,152 cells, the reference TGV fields tiled, Burke 9
-species, ROS3 chemistry), checked through properties that do not need the oracle at this size:
+species, ROS3 chemistry, the convection schemes the bench runs -- the case's fvSchemes -- and the GPU reference's
+upwind/linear), checked through properties that do not need the oracle at this size:
 
 - determinism: the same state stepped twice gives bitwise identical fields (no floating-point atomics,
   fixed-order reductions) -- the property that makes the bitwise oracle tests meaningful at scale;
@@ -18,9 +19,11 @@ from conftest import GOLDEN, ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _headline(n=128):
+def _headline(n=128, schemes="case"):
+    """the bench's workload: its mesh, state, chemistry and convection schemes (bench.py --schemes: the
+    case's own fvSchemes -- limitedLinear01 / limitedLinear / cubic -- or the GPU reference's upwind/linear)"""
     sys.path.insert(0, ROOT)
-    from bench import MECHS, reference_fields
+    from bench import MECHS, reference_fields, case_schemes, gpu_schemes
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi.kinetics import parse_mechanism
@@ -30,7 +33,8 @@ def _headline(n=128):
     t = read_thermo_table(os.path.join(GOLDEN, MECHS["burke9"][1]), ym["species"])
     m = hex_box(n, n, n, lengths=(2 * np.pi * 1e-3,) * 3)
     ctx = Context(0)
-    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6)
+    case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6,
+                       schemes=case_schemes() if schemes == "case" else gpu_schemes())
     ctx.chem_set_mechanism(parse_mechanism(os.path.join(GOLDEN, MECHS["burke9"][0])))
     ctx.chem_set_options(1, rtol=1e-6, atol=1e-10)
     f = reference_fields(m, ym["species"])
@@ -49,19 +53,23 @@ def _assert_converged(ctx):
         assert it < cap and rel <= 1e-5, (e, it, r0, rel)
 
 
-def test_full_size_steps_are_deterministic_and_conservative():
+@pytest.mark.parametrize("schemes", ["case", "gpu"])
+def test_full_size_steps_are_deterministic_and_conservative(schemes):
     from dfmi import case
-    ctx, m, t = _headline()
+    ctx, m, t = _headline(schemes=schemes)
     C, S = m.n_cells, t.S
     ctx.time_step(2)                                   # develop the state a little
     st = case.pull_state(ctx, m, S)
     runs = []
+    ctx.kernel_timer("k_bcg_eo")
     for _ in range(2):
         case.push_state(ctx, st)
         ctx.set_field("chem_stats", np.zeros((3, C)))
         ctx.time_step(2)
         runs.append({n: ctx.get_field(n, (C,)) for n in ("T", "p", "rho", "he")} |
                     {"U": ctx.get_field("U", (3, C)), "Y": ctx.get_field("Y", (S, C))})
+    assert ctx.kernel_time("k_bcg_eo")[1] > 0          # the even-odd BiCGStab ran (the 2-colourable box)
+    ctx.kernel_timer("")
     for k in runs[0]:
         assert np.array_equal(runs[0][k], runs[1][k]), k
     T, Y = runs[0]["T"], runs[0]["Y"]

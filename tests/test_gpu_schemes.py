@@ -188,3 +188,41 @@ def test_limited_v_rejected_on_processor_patches():
     ctx = Context(0)
     with pytest.raises(DfmiError, match="decomposed"):
         case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6, schemes={"div(phi,U)": "limitedLinearV 1"})
+
+
+def test_scheme_contract_errors():
+    """dfmi_set_scheme needs the boundary initialisation (it checks the patch kinds: limitedLinearV on a
+    processor patch is refused), and a limited scheme with no mesh_distance is an error, not a silent
+    upwind (the limiter's d would be 0)."""
+    import ctypes as C
+    from dfmi.lib import Context, DfmiError, _dp
+    from dfmi.mesh import hex_box
+    from dfmi import case
+    from test_gpu_parity import _mech
+    ym, t = _mech("burke9")
+    m = hex_box(6, 5, 4, lengths=(2 * np.pi * 1e-3,) * 3)
+    pt = case.default_patch_types(m)
+    ctx = Context(0)
+    rows, cols = m.proc_rows_cols()
+    ctx.set_constant_values(m.n_cells, m.n_cells, m.n_faces, m.n_boundary_slots, m.n_patches, int(rows.size),
+                            m.patch_sizes, t.S, 1e6)
+    ctx.set_cyclic_info(m.cyclic_neighbour())
+    ctx.set_constant_indexes(m.owner, m.neighbour, rows, cols, m.global_offset)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (m.sf, m.mag_sf, m.weight, m.delta_coeffs, m.volume)]
+    # mesh_distance = NULL (the ABI accepts it)
+    ctx._call("dfmi_init_constant_fields_internal", ctx.h, *[_dp(a) for a in arrs], None)
+    with pytest.raises(DfmiError, match="dfmi_init_constant_fields_boundary"):
+        ctx.set_scheme("div(phi,U)", "Gauss limitedLinearV 1")
+    bsf, bmag, bdc, bw, bfc = m.boundary_arrays()
+    ctx.init_constant_fields_boundary(bsf, bmag, bdc, bw, bfc, pt["calculated"], pt["extrapolated"])
+    ctx.init_boundary_delta(m.boundary_delta())
+    ctx.set_scheme("div(phi,Yi_h)", "Gauss limitedLinear01 1")
+    for f in ("U", "p", "he", "K", "Y", "T", "rho"):
+        ctx.set_patch_types(f, pt[f])
+    ctx.set_inert_index(ym["species"].index("N2"))
+    ctx.thermo_set_coeffs(t)
+    fl = case.tgv_fields(m, ym["species"], kernel_radius=1.2e-3)
+    case.init_state(ctx, m, t.S, fl["T"], fl["p"], fl["U"], fl["Y"])
+    with pytest.raises(DfmiError, match="mesh_distance"):
+        ctx.time_step(2)
+    ctx.close()
