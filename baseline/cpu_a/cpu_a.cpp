@@ -1153,5 +1153,7 @@ int dfmi_dnn_stats(dfmi_ctx*, int*, double*) { return guard([&] { throw Error("d
 int dfmi_kernel_timer(dfmi_ctx*, const char*) { return guard([&] { throw Error("dfmi (CPU-A): no kernels"); }); }
 int dfmi_kernel_time(dfmi_ctx*, double*, int*) { return guard([&] { throw Error("dfmi (CPU-A): no kernels"); }); }
 int dfmi_kernel_time_named(dfmi_ctx*, const char*, double*, int*) { return guard([&] { throw Error("dfmi (CPU-A): no kernels"); }); }
+int dfmi_comm_timer(dfmi_ctx*, int) { return guard([&] { throw Error("dfmi (CPU-A): one rank, no communication"); }); }
+int dfmi_comm_report(dfmi_ctx*, char*, int, int*) { return guard([&] { throw Error("dfmi (CPU-A): one rank, no communication"); }); }
 
 }  // extern "C"

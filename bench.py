@@ -444,6 +444,42 @@ def config4_line(m, T, U, p, steps=3, warmup=1):
             "steps": steps, "reacting_cells": nr, "solver_iters": iters}
 
 
+def comm_block(local, step_ms, steps, world, rank):
+    """The multi-GPU line's communication block: every rank's per-exchange-point accounting
+    (dfmi_comm_report: HIP-event time of the transport calls -- ncclSend/ncclRecv groups of the halo
+    exchanges, ncclAllGather of the solver reductions -- and the bytes each rank sends) over the roofline
+    pass, gathered to rank 0. Per point: calls and bytes per step, time per step (max / mean over ranks);
+    totals against the step time of the same pass. DESIGN.md 7 states the rule the overlap decision follows."""
+    import torch.distributed as dist
+    every = [None] * world
+    dist.all_gather_object(every, {"rank": rank, "points": local, "step_ms": step_ms})
+    if rank != 0:
+        return None
+    names = sorted({k for e in every for k in e["points"]})
+    pts = {}
+    for k in names:
+        ms = [e["points"].get(k, {}).get("ms", 0.0) / steps for e in every]
+        by = [e["points"].get(k, {}).get("bytes", 0.0) / steps for e in every]
+        calls = [e["points"].get(k, {}).get("calls", 0) / steps for e in every]
+        pts[k] = {"calls_per_step": max(calls), "bytes_per_step_max": max(by),
+                  "bytes_per_call": max(by) / max(max(calls), 1e-30),
+                  "ms_per_step_max": max(ms), "ms_per_step_mean": sum(ms) / world}
+    tot = [sum(v.get("ms", 0.0) for v in e["points"].values()) / steps for e in every]
+    halo = [sum(v.get("ms", 0.0) for n, v in e["points"].items() if not n.startswith("allgather")) / steps for e in every]
+    solver = [sum(v.get("ms", 0.0) for n, v in e["points"].items()
+                  if n.split(" ")[0] in ("bicgstab", "pcg") or n.startswith("allgather")) / steps for e in every]
+    step = max(e["step_ms"] for e in every)
+    return {"source": "dfmi_comm_report: HIP events around every transport call on the stream it ran on, "
+                      f"{steps} roofline-pass steps (kernel timers armed too)",
+            "overlap": os.environ.get("DFMI_HALO_OVERLAP", "0"),
+            "step_ms": step,
+            "comm_ms_per_step": {"max": max(tot), "per_rank": tot},
+            "halo_ms_per_step_max": max(halo), "allgather_ms_per_step_max": max(tot[i] - halo[i] for i in range(world)),
+            "solver_comm_ms_per_step_max": max(solver),
+            "fraction_of_step": max(tot) / step if step > 0 else None,
+            "points": pts}
+
+
 def chem_step_stats(ctx, C):
     """Integrator steps per cell of the last chemistry solve and how evenly 64-lane waves are loaded:
     a wave costs its slowest lane, so efficiency = mean cost / mean of per-wave max cost, in natural
@@ -565,9 +601,17 @@ def main():
     work_pre = {e: ctx.solver_work(e, reset=True) for e in ("U", "Y", "E", "p")}
     if args.chem == "dnn":
         ctx.dnn_stats()
+    if world > 1:
+        ctx.comm_timer(True)                       # per-exchange-point transport time and bytes (this pass only)
+    tr0 = time.perf_counter()
     for _ in range(args.roof_steps):
         ctx.time_step(args.ncorr)
     ctx.sync()
+    roof_ms = (time.perf_counter() - tr0) / max(args.roof_steps, 1) * 1e3
+    comm = None
+    if world > 1:
+        comm = comm_block(ctx.comm_report(), roof_ms, args.roof_steps, world, rank)
+        ctx.comm_timer(False)
     ktime = {k: ctx.kernel_time(k) for k in ROOF_KERNELS}
     work = {e: ctx.solver_work(e) for e in ("U", "Y", "E", "p")}
     chem_ms, chem_n = ctx.kernel_time("k_chem") if args.chem == "ode" else (0.0, 0)
@@ -724,6 +768,8 @@ def main():
         "finite": finite,
         "other_schemes": alt,
     }
+    if comm is not None:
+        out["comm"] = comm
     if world == 1 and out["roofline"] is not None:   # the headline kernel against a measured copy peak as well
         peak_copy = ctx.hbm_copy_peak(4.0, 20)     # dfmi_hbm_copy_peak: 16-B vector streaming copy
         out["roofline"]["measured_copy_peak_GBs"] = peak_copy

@@ -1229,6 +1229,7 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const
                double* partial, int nblk, const double* active, bool l0_done) {
   Amg& a = x.amg;
   DFMI_CHECK(!l0_done || amg_l0_fusable(x), "AMG: level-0 sweep fused on an unsupported configuration");
+  CommTag _ct(x, x.comm.tag + " amg");
   auto direct = [&] {
     if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
     else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);

@@ -620,6 +620,24 @@ int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {
   });
 }
 
+int dfmi_comm_timer(dfmi_ctx* ctx, int on) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.comm.reset();
+    x.comm.on = on != 0;
+    x.comm.tag.clear();
+  });
+}
+
+int dfmi_comm_report(dfmi_ctx* ctx, char* buf, int len, int* needed) {
+  return guard([&] {
+    const std::string r = comm_report(ctx->x);
+    if (needed) *needed = (int)r.size() + 1;
+    if (buf && len > 0) std::snprintf(buf, len, "%s", r.c_str());
+  });
+}
+
 int dfmi_kernel_timer(dfmi_ctx* ctx, const char* kernels) {
   return guard([&] {
     Ctx& x = ctx->x;

@@ -175,6 +175,31 @@ struct KernelTimer {
   }
 };
 
+// Communication accounting per exchange point (dfmi_comm_timer / dfmi_comm_report): every transport call
+// of a halo exchange (ncclSend/ncclRecv group) or an all-gather, HIP events around it on the stream it is
+// issued on (the compute stream, or the halo's comm stream for overlapped exchanges), with the bytes this
+// rank sends, keyed by the exchange point that issued it (Ctx::comm.tag, set by the callers: the field
+// names of a boundary-field exchange, the solver and its vectors). The reference's counterparts are the
+// per-field NCCL groups of dfMatrixOpBase.cu:441-485 / 2402-2491, timed only by its TIME_GPU host ticks.
+struct CommStats {
+  bool on = false;
+  std::string tag;
+  struct Entry { long calls = 0; double bytes = 0; std::vector<std::pair<hipEvent_t, hipEvent_t>> ev; };
+  std::map<std::string, Entry> pts;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  hipEvent_t next() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      DFMI_HIP(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  void reset() { pts.clear(); used = 0; }
+  ~CommStats() { for (auto e : pool) (void)hipEventDestroy(e); }
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -269,6 +294,7 @@ struct Ctx {
   std::map<std::string, StatSnap> stat_snap;
   DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
+  CommStats comm;
   DevBuf<int> trav;   // dfmi_set_traversal: the order threads visit cells in the gather kernels (empty: natural)
   int hex[3] = {0, 0, 0};   // MeshView::hx/hy/hz (build_ell)
   ~Ctx();
@@ -420,8 +446,22 @@ void halo_update(Ctx& x, const HaloItem* items, int n);
 bool halo_overlap(const Ctx& x);
 void halo_begin(Ctx& x, const HaloItem* items, int n);
 void halo_end(Ctx& x);
+// the exchange point of the halo / all-gather calls made while it lives (communication accounting)
+struct CommTag {
+  Ctx& x;
+  std::string prev;
+  bool set;
+  CommTag(Ctx& c, const std::string& t) : x(c), set(c.comm.on) { if (set) { prev = x.comm.tag; x.comm.tag = t; } }
+  ~CommTag() { if (set) x.comm.tag = prev; }
+};
 inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
   if (!halo_active(x)) return;
+  std::string tag;
+  if (x.comm.on) {
+    tag = "fields";
+    for (const char* n : names) { tag += ' '; tag += n; }
+  }
+  CommTag _ct(x, tag);
   std::vector<HaloItem> it;
   for (const char* n : names) {
     const Field& f = x.fields.at(n);
@@ -432,6 +472,7 @@ inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
 }
 // allgather of `count` doubles per rank: recv[r * count + i]
 void halo_allgather(Ctx& x, const double* send, double* recv, long count);
+std::string comm_report(Ctx& x);   // JSON of the communication accounting (CommStats)
 void halo_setup(Ctx& x);   // builds the exchange lists after dfmi_set_comm_info / dfmi_set_comm_local
 void halo_init_rccl(Ctx& x, const void* uid, int nranks, int rank);
 void halo_init_local(Ctx& x, int hub_id, int nranks, int rank);

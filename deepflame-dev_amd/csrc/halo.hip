@@ -191,7 +191,18 @@ void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<d
     DFMI_HIP(hipGetLastError());
     h.off.resize(h.peers.size()); h.cnt.resize(h.peers.size());
     for (size_t i = 0; i < h.peers.size(); ++i) { h.off[i] = (long)kk * h.pf_off[i]; h.cnt[i] = (long)kk * h.pf_cnt[i]; }
-    h.tr->sendrecv(x, st, h.sbuf.p, h.rbuf.p, h.peers, h.off, h.cnt);
+    if (x.comm.on) {
+      auto& e = x.comm.pts[x.comm.tag.empty() ? std::string("halo") : x.comm.tag];
+      hipEvent_t a = x.comm.next(), b = x.comm.next();
+      DFMI_HIP(hipEventRecord(a, st));
+      h.tr->sendrecv(x, st, h.sbuf.p, h.rbuf.p, h.peers, h.off, h.cnt);
+      DFMI_HIP(hipEventRecord(b, st));
+      e.ev.push_back({a, b});
+      e.calls += 1;
+      for (long c : h.cnt) e.bytes += 8.0 * (double)c;
+    } else {
+      h.tr->sendrecv(x, st, h.sbuf.p, h.rbuf.p, h.peers, h.off, h.cnt);
+    }
     {
       KScope _ks(x, timed ? "k_halo_unpack" : nullptr);
       hipLaunchKernelGGL(k_unpack, g, dim3(256), 0, st, x.H, kk, a, to_slots ? h.recv_slots.p : nullptr, x.C, h.h_off.p,
@@ -258,7 +269,36 @@ void halo_end(Ctx& x) {
 
 void halo_allgather(Ctx& x, const double* send, double* recv, long count) {
   DFMI_CHECK(x.halo && x.nranks > 1, "halo_allgather without a communicator");
+  if (!x.comm.on) { x.halo->tr->allgather(x, send, recv, count); return; }
+  auto& e = x.comm.pts["allgather " + (x.comm.tag.empty() ? std::string("-") : x.comm.tag)];
+  hipEvent_t a = x.comm.next(), b = x.comm.next();
+  DFMI_HIP(hipEventRecord(a, x.stream));
   x.halo->tr->allgather(x, send, recv, count);
+  DFMI_HIP(hipEventRecord(b, x.stream));
+  e.ev.push_back({a, b});
+  e.calls += 1;
+  e.bytes += 8.0 * (double)count;
+}
+
+// {"point": {"calls": n, "bytes": b, "ms": t}, ...} of the exchanges since dfmi_comm_timer (synchronises)
+std::string comm_report(Ctx& x) {
+  DFMI_HIP(hipStreamSynchronize(x.stream));
+  if (x.halo && x.halo->cs) DFMI_HIP(hipStreamSynchronize(x.halo->cs));
+  std::string out = "{";
+  bool first = true;
+  for (auto& kv : x.comm.pts) {
+    double ms = 0.0;
+    for (auto& pr : kv.second.ev) {
+      float t = 0.f;
+      DFMI_HIP(hipEventElapsedTime(&t, pr.first, pr.second));
+      ms += t;
+    }
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "\"calls\": %ld, \"bytes\": %.0f, \"ms\": %.6f}", kv.second.calls, kv.second.bytes, ms);
+    out += (first ? "\"" : ", \"") + kv.first + "\": {" + buf;
+    first = false;
+  }
+  return out + "}";
 }
 
 // Exchange lists from the processor patches (called once the communicator exists).

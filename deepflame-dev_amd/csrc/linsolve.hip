@@ -1509,6 +1509,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     double *v_, *d_, *r_;
     bicg_layout(x, nsys, &v_, &d_, &r_);
   }
+  CommTag _ct(x, std::string("bicgstab ") + eqn);
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
@@ -1652,6 +1653,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
                      double* bxsol, const SolverCfg& cfg) {
   (void)bxsol;
   if (!x.ell.ready) build_ell(x);
+  CommTag _ct(x, std::string("pcg ") + eqn);
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);

@@ -72,6 +72,8 @@ SIGNATURES = {
     "dfmi_hex_dims": [_P, _IP, _IP, _IP],
     "dfmi_correct_boundary": [_P, C.c_char_p],
     "dfmi_kernel_timer": [_P, C.c_char_p],
+    "dfmi_comm_timer": [_P, C.c_int],
+    "dfmi_comm_report": [_P, C.c_char_p, C.c_int, _IP],
     "dfmi_kernel_time": [_P, _DP, _IP],
     "dfmi_kernel_time_named": [_P, C.c_char_p, _DP, _IP],
     "dfmi_chem_set_mechanism": [_P, C.c_int, _IP, _IP, _DP],
@@ -371,6 +373,19 @@ class Context:
 
     def time_step(self, n_corr=2):
         self._call("dfmi_time_step", self.h, int(n_corr))
+
+    def comm_timer(self, on: bool = True):
+        """reset and arm (or disarm) the per-exchange-point communication accounting"""
+        self._call("dfmi_comm_timer", self.h, int(bool(on)))
+
+    def comm_report(self) -> dict:
+        """{exchange point: {"calls", "bytes" (sent by this rank), "ms" (HIP-event time of the transport calls)}}"""
+        import json
+        need = C.c_int()
+        self._call("dfmi_comm_report", self.h, None, 0, C.byref(need))
+        buf = C.create_string_buffer(max(need.value, 1) + 64)
+        self._call("dfmi_comm_report", self.h, buf, len(buf), C.byref(need))
+        return json.loads(buf.value.decode() or "{}")
 
     def kernel_timer(self, kernel: str):
         """Arm HIP-event timing of every launch of `kernel` on this context's stream."""

@@ -253,6 +253,17 @@ int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting);
 /* reacting cells of the last inference; algorithmic hidden-layer GEMM flops since the last call */
 int dfmi_dnn_stats(dfmi_ctx* ctx, int* n_reacting, double* gemm_flops);
 
+/* ---- communication accounting per exchange point (multi-rank runs). The reference issues one NCCL group
+ * per field and processor patch (dfMatrixOpBase.cu:441-485, dispatch :2402-2491; comm set up at
+ * dfNcclBase.cu:23-65) and times only whole equations (TIME_GPU, dfMatrixOpBase.H:42-82). on != 0 resets
+ * and arms: every halo exchange (one ncclSend/ncclRecv group per exchange point) and every all-gather is
+ * bracketed by HIP events on the stream it runs on and its bytes sent counted, keyed by the exchange point
+ * ("fields rho", "bicgstab Y", "pcg p amg", "allgather pcg p", ...); on == 0 disarms. */
+int dfmi_comm_timer(dfmi_ctx* ctx, int on);
+/* synchronise and write {"point": {"calls": n, "bytes": b, "ms": t}, ...} (JSON) into buf (len bytes);
+ * *needed = the length it takes including the terminator */
+int dfmi_comm_report(dfmi_ctx* ctx, char* buf, int len, int* needed);
+
 /* ---- kernel timing (the reference's TICK_START_EVENT / TICK_END_EVENT cudaEvent pairs,
  * src_gpu/dfMatrixOpBase.H:46-60): arm HIP-event timing of every launch of one kernel
  * (name as in the source, e.g. "k_y_assemble"; "" disarms), recorded on the context stream */

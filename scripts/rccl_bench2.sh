@@ -17,5 +17,11 @@ import json, sys
 d = json.loads([l for l in open(f"gpurun_out/bench_rccl2_{sys.argv[1]}.log") if l.startswith("{")][-1])
 print(sys.argv[1], round(d["ms_per_step"], 2), "ms/step", d["solver_iters"], "levels", d["amg_levels"][-2:],
       "hex", d.get("hex_face_walk"), "classes", d.get("row_classes"))
+c = d.get("comm")
+if c:
+    print("  comm ms/step max", round(c["comm_ms_per_step"]["max"], 3), "of", round(c["step_ms"], 2),
+          "halo", round(c["halo_ms_per_step_max"], 3), "allgather", round(c["allgather_ms_per_step_max"], 3))
+    for k, v in sorted(c["points"].items(), key=lambda kv: -kv[1]["ms_per_step_max"])[:12]:
+        print(f"    {k:34s} calls/step {v['calls_per_step']:6.1f}  KB/call {v['bytes_per_call'] / 1e3:9.1f}  ms/step {v['ms_per_step_max']:.3f}")
 PY
 done
