@@ -168,6 +168,27 @@ void allocate_fields(Ctx& x) {
   if (!x.solver.count("p")) x.solver["p"] = SolverCfg{1000, 1e-5, 0.0, 1};                            // amgxpOptions
 }
 
+// Term-sensitivity study knobs (DFMI_CPUA_STUDY, comma list; unset in every product / bench / test run):
+// no_diffAlphaD, no_hDiffCorrFlux, no_dpdt drop that EEqn term; ddtcorr=<s> scales pEqn's ddtCorr flux
+// (pEqn.H:21-25). scripts/tgv2d_terms.py tabulates each one's effect on test/corrtest.cpp:52-56.
+bool study(const char* knob) {
+  const char* e = std::getenv("DFMI_CPUA_STUDY");
+  return e && std::strstr(e, knob) != nullptr;
+}
+// "<name>=<s>": scale a term by s (1 when absent)
+double study_scale(const char* name) {
+  const char* e = std::getenv("DFMI_CPUA_STUDY");
+  const std::string key = std::string(name) + "=";
+  const char* at = e ? std::strstr(e, key.c_str()) : nullptr;
+  return at ? std::atof(at + key.size()) : 1.0;
+}
+void scale_field(Ctx& x, const char* name, long n, double s) {
+  if (s == 1.0) return;
+  double* v = x.f(name);
+  for (long i = 0; i < n; ++i) v[i] *= s;
+}
+double g_ddtcorr_scale = 1.0;
+
 // register every array with the oracle restatement (its registry is process-global)
 void bind(Ctx& x) {
   CHECK(x.have_bgeom, "mesh not fully initialised");
@@ -188,6 +209,10 @@ void bind(Ctx& x) {
   for (auto& kv : x.fields) orc_set_d(kv.first.c_str(), kv.second.v.data());
   for (auto& kv : x.work) orc_set_d(kv.first.c_str(), kv.second.data());
   orc(orc_set_thermo(x.S, x.W.data(), x.nasa.data(), x.visc.data(), x.cond.data(), x.bdiff.data()), "thermo");
+  if (const char* e = std::getenv("DFMI_CPUA_STUDY"); e && std::strstr(e, "ddtcorr=")) {
+    g_ddtcorr_scale = std::atof(std::strstr(e, "ddtcorr=") + 8);
+    orc_set_d("study_ddtcorr_scale", &g_ddtcorr_scale);
+  }
 }
 
 void require_ready(Ctx& x) {
@@ -676,6 +701,18 @@ void do_Y(Ctx& x) {
   CHECK(x.mode != 2, "DNN chemistry is a GPU-path feature");
   orc(orc_conv_weights(), "div(phi,Yi_h) weights");
   orc(orc_y_prep(), "YEqn prep");
+  if (study("no_diffAlphaD")) {
+    std::fill_n(x.f("diffAlphaD"), x.C, 0.0);
+    std::fill_n(x.f("boundary_diffAlphaD"), x.B, 0.0);
+  }
+  if (study("no_hDiffCorrFlux")) {
+    std::fill_n(x.f("hDiffCorrFlux"), 3 * x.C, 0.0);
+    std::fill_n(x.f("boundary_hDiffCorrFlux"), 3 * x.B, 0.0);
+  }
+  scale_field(x, "diffAlphaD", x.C, study_scale("dAD"));
+  scale_field(x, "boundary_diffAlphaD", x.B, study_scale("dAD"));
+  scale_field(x, "hDiffCorrFlux", 3 * x.C, study_scale("hdcf"));
+  scale_field(x, "boundary_hDiffCorrFlux", 3 * x.B, study_scale("hdcf"));
   orc(orc_y_assemble(), "YEqn");
   const long C = x.C, F = x.F, B = x.B;
   double* Y = x.f("Y");
@@ -692,7 +729,12 @@ void do_Y(Ctx& x) {
 void do_E(Ctx& x) {
   orc(orc_energy_gradient(), "energy gradient");
   orc(orc_correct_bc("he", "boundary_he", "ptype_he", 1), "he boundary");
+  if (study("no_dpdt")) std::fill_n(x.f("dpdt"), x.C, 0.0);
+  const double sd = study_scale("dpdt");   // scaled for this EEqn only (pEqn rewrites dpdt from p)
+  std::vector<double> keep;
+  if (sd != 1.0) { keep.assign(x.f("dpdt"), x.f("dpdt") + x.C); scale_field(x, "dpdt", x.C, sd); }
   orc(orc_e_assemble(), "EEqn");
+  if (sd != 1.0) std::copy(keep.begin(), keep.end(), x.f("dpdt"));
   solve(x, "E", x.w("out_lower"), x.w("out_upper"), x.w("out_diag"), x.w("out_source"), x.w("out_internal_coeffs"),
         x.w("out_boundary_coeffs"), "he", x.f("he"), true);
   orc(orc_correct_bc("he", "boundary_he", "ptype_he", 1), "he boundary");

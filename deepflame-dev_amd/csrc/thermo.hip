@@ -164,15 +164,13 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   }
 }
 
-// WV: waves per SIMD the register allocation must leave room for (S = 9: 172 VGPRs -> 2 waves by the compiler's
-// own choice; 3 fits in 167 VGPRs with 20 B/lane of spill)
-int thermo_waves() {
-  static const int w = [] { const char* e = std::getenv("DFMI_THERMO_WAVES"); return e ? std::atoi(e) : 0; }();
-  return w;
-}
+// Register budget: S <= 9 is compiled for 3 waves per SIMD (S = 9: 167 VGPRs with 20 B/lane of spill, against the
+// compiler's own 172 VGPRs / 2 waves): k_thermo_cells<9> 506-508 -> 460-462 us on the 2M headline
+// (profiles/r04_thermo_waves_ab.json, two runs each). Larger register-resident mechanisms keep the compiler's choice.
+template <int S> constexpr int thermo_wv() { return S <= 9 ? 3 : 1; }
 
-template <int S, int WV>
-__global__ void __launch_bounds__(256, WV) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
+template <int S>
+__global__ void __launch_bounds__(256, thermo_wv<S>()) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
     const double* __restrict__ p, const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho,
     double* __restrict__ mu, double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
@@ -673,14 +671,9 @@ void thermo_correct(Ctx& x, bool from_T) {
 #define CALL(NS)                                                                                                   \
   do {                                                                                                            \
     if (x.C > 0) { KScope _ks(x, "k_thermo_cells");                                                              \
-      if (thermo_waves() == 3)                                                                                      \
-        hipLaunchKernelGGL((k_thermo_cells<NS, 3>), dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t,     \
-                           (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"), \
-                           x.f("alpha"), x.f("rhoD"), x.f("hai"));                                                \
-      else                                                                                                          \
-        hipLaunchKernelGGL((k_thermo_cells<NS, 1>), dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t,     \
-                           (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"), \
-                           x.f("alpha"), x.f("rhoD"), x.f("hai")); }                                              \
+      hipLaunchKernelGGL((k_thermo_cells<NS>), dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t,          \
+                         (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"),   \
+                         x.f("alpha"), x.f("rhoD"), x.f("hai")); }                                              \
     DFMI_HIP(hipGetLastError());                                                                                  \
     if (x.B > 0) hipLaunchKernelGGL(k_thermo_slots<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t,  \
                        x.st("T"), (int)from_T, x.f("T"), x.f("he"), x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), \

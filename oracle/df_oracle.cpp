@@ -706,6 +706,7 @@ void p_eqn_assemble(const M& m) {
   double *rf = d("out_rhorAUf"), *brf = d("out_boundary_rhorAUf");
   double *ph = d("out_phiHbyA"), *bph = d("out_boundary_phiHbyA");
   const double small_ = 1e-15;    // OpenFOAM 'small' in ddtScheme::fvcDdtPhiCoeff
+  const double* dscale = has("study_ddtcorr_scale") ? d("study_ddtcorr_scale") : nullptr;
   // rhorAUf = fvc::interpolate(rho*rAU)
   std::vector<double> rr(C), rUo(3L * C);
   #pragma omp parallel for schedule(static)
@@ -727,6 +728,7 @@ void p_eqn_assemble(const M& m) {
                                    m.sf(2, f) * interp_f(w, rUo[2L * C + o], rUo[2L * C + n]));
     double coeff = 1.0 - std::min(std::fabs(phiCorr) / (std::fabs(phi_old[f]) + small_), 1.0);
     double ddtCorr = coeff * m.rdt * phiCorr;
+    if (dscale) ddtCorr = ddtCorr * *dscale;   // sensitivity study only (CPU-A DFMI_CPUA_STUDY ddtcorr=)
     double fl = m.sf(0, f) * interp_f(w, H[o], H[n]) + m.sf(1, f) * interp_f(w, H[C + o], H[C + n]) +
                 m.sf(2, f) * interp_f(w, H[2L * C + o], H[2L * C + n]);
     ph[f] = interp_f(w, rho[o], rho[n]) * fl + rf[f] * ddtCorr;
@@ -745,7 +747,7 @@ void p_eqn_assemble(const M& m) {
     double phiCorr = bphi_old[b] - (m.bsf(0, b) * ruo[0] + m.bsf(1, b) * ruo[1] + m.bsf(2, b) * ruo[2]);
     double coeff = fixes_value(tu) ? 0.0 : 1.0 - std::min(std::fabs(phiCorr) / (std::fabs(bphi_old[b]) + small_), 1.0);
     double fl = m.bsf(0, b) * Hb[0] + m.bsf(1, b) * Hb[1] + m.bsf(2, b) * Hb[2];
-    bph[b] = rb * fl + brf[b] * (coeff * m.rdt * phiCorr);
+    bph[b] = rb * fl + brf[b] * (dscale ? (coeff * m.rdt * phiCorr) * *dscale : coeff * m.rdt * phiCorr);
   });
   // fvm::laplacian(rhorAUf, p), symmetric
   std::vector<double> UL(F);
