@@ -32,6 +32,7 @@
 #include <vector>
 
 #define DFMI_HD   // the generated kinetics run on the host here
+#define DFMI_OPAQUE(v, q)   // scheduling barrier of the device build only
 #pragma GCC diagnostic push
 #pragma GCC diagnostic ignored "-Wunused-variable"
 #include "../../deepflame-dev_amd/csrc/chem_gen_burke9.inc"
@@ -563,7 +564,7 @@ unsigned long long fnv(unsigned long long h, const void* p, size_t n) {
 
 template <class G>
 int chem_cells(Ctx& x, double dt, const double* rho_rr) {
-  constexpr int S = G::S;
+  constexpr int S = G::S, SA = G::SA;   // active species: the integrated state (chem.hip k_chem_gen)
   constexpr double g = 0.43586652150845899941601945119356;
   constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
                    c32 = 0.92076794298330791242156818474003e1;
@@ -596,33 +597,35 @@ int chem_cells(Ctx& x, double dt, const double* rho_rr) {
         if (steps + rejects >= max_steps) { steps = -1; break; }
         if (t + h > dt) h = dt - t;
         const double hg = h * g, rh = 1.0 / h;
-        double f0[S], A[S * S];
+        double f0[SA], A[SA * SA];
         G::wdot(T, k, y, f0);
-        for (int e = 0; e < S * S; ++e) A[e] = 0.0;
+        for (int e = 0; e < SA * SA; ++e) A[e] = 0.0;
         G::jac(T, k, y, A);
-        for (int e = 0; e < S * S; ++e) A[e] = (e % (S + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
+        for (int e = 0; e < SA * SA; ++e) A[e] = (e % (SA + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
         bool ok = G::factor(A);
-        double err = 0.0, yn[S];
+        double err = 0.0, yn[SA];
         if (ok) {
-          double k1[S], k2[S], k3[S], y2[S], f2[S];
-          for (int i = 0; i < S; ++i) k1[i] = hg * f0[i];
+          double k1[SA], k2[SA], k3[SA], y2[S], f2[SA];
+          for (int a = 0; a < SA; ++a) k1[a] = hg * f0[a];
           G::solve(A, k1);
-          for (int i = 0; i < S; ++i) y2[i] = y[i] + k1[i];
+          for (int i = 0; i < S; ++i) y2[i] = y[i];
+          for (int a = 0; a < SA; ++a) y2[G::ACT[a]] = y[G::ACT[a]] + k1[a];
           G::wdot(T, k, y2, f2);
-          for (int i = 0; i < S; ++i) k2[i] = hg * (f2[i] + c21 * rh * k1[i]);
+          for (int a = 0; a < SA; ++a) k2[a] = hg * (f2[a] + c21 * rh * k1[a]);
           G::solve(A, k2);
-          for (int i = 0; i < S; ++i) k3[i] = hg * (f2[i] + rh * (c31 * k1[i] + c32 * k2[i]));
+          for (int a = 0; a < SA; ++a) k3[a] = hg * (f2[a] + rh * (c31 * k1[a] + c32 * k2[a]));
           G::solve(A, k3);
-          for (int i = 0; i < S; ++i) {
-            yn[i] = y[i] + k1[i] + m2 * k2[i] + m3 * k3[i];
-            const double e = (e1 * k1[i] + e2 * k2[i] + e3 * k3[i]) / (sc[i] + rtol * std::fmax(std::fabs(y[i]), std::fabs(yn[i])));
+          for (int a = 0; a < SA; ++a) {
+            const int i = G::ACT[a];
+            yn[a] = y[i] + k1[a] + m2 * k2[a] + m3 * k3[a];
+            const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) / (sc[i] + rtol * std::fmax(std::fabs(y[i]), std::fabs(yn[a])));
             err += e * e;
           }
           err = std::sqrt(err / S);
           if (!(err == err)) ok = false;
         }
         if (ok && err <= 1.0) {
-          for (int i = 0; i < S; ++i) y[i] = yn[i];
+          for (int a = 0; a < SA; ++a) y[G::ACT[a]] = yn[a];
           t += h;
           ++steps;
           const double fac = err > 0.0 ? 0.9 * std::pow(err, -1.0 / 3.0) : 5.0;

@@ -535,17 +535,23 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wunused-variable"
 #define DFMI_HD __device__   // the generated kinetics are plain C++; here they run on the device
+// value v passes through an empty asm that also reads q: the same value, but not available before q
+#define DFMI_OPAQUE(v, q) asm volatile("" : "+v"(v) : "v"(q))
 #include "chem_gen_burke9.inc"
 #include "chem_gen_es80.inc"
 #pragma clang diagnostic pop
 
-template <class G>
-__global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restrict__ perm, const double* __restrict__ Tf,
-                                                    const double* __restrict__ pf, const double* __restrict__ rhof,
-                                                    const double* __restrict__ Yf, double dt, double rtol, double atol,
-                                                    double Tmin, int max_steps, double* __restrict__ RR,
-                                                    double* __restrict__ stats, int* __restrict__ fail) {
-  constexpr int S = G::S;
+// The integrated state is the mechanism's active species (G::SA; a third-body-only species such as N2 keeps its
+// concentration and rides along in y) -- bitwise the full-state integration: the dropped rows and columns
+// only ever multiply or add exact zeros (chem_codegen.py). RK: the rate constants are computed inline, next to
+// their reaction, in every rates / rates_jac call (two per step) instead of once per cell and held across the
+// step loop (48 doubles for Burke 9); the same values and sums, bitwise.
+template <class G, bool RK, int WV>
+__global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __restrict__ perm,
+    const double* __restrict__ Tf, const double* __restrict__ pf, const double* __restrict__ rhof,
+    const double* __restrict__ Yf, double dt, double rtol, double atol, double Tmin, int max_steps,
+    double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail) {
+  constexpr int S = G::S, SA = G::SA;
   constexpr double g = 0.43586652150845899941601945119356;
   constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
                    c32 = 0.92076794298330791242156818474003e1;
@@ -554,18 +560,20 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
   if (t >= n) return;
   const long c = perm ? perm[t] : t;
-  const double T = Tf[c], rho_rr = rhof[c];
-  double Y0[S], y[S], sc[S];
+  const double T = Tf[c];
+  double y[S];
+  double rho;
+  {
+    double Y0[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) Y0[i] = Yf[(long)i * n + c];
-  const double rho = reactor_state<S>(T, pf[c], Y0, G::W, y);
-#pragma unroll
-  for (int i = 0; i < S; ++i) sc[i] = atol * rho / G::W[i];
+    for (int i = 0; i < S; ++i) Y0[i] = Yf[(long)i * n + c];
+    rho = reactor_state<S>(T, pf[c], Y0, G::W, y);
+  }
   int steps = 0, rejects = 0;
   double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
-    double k[G::NK];
-    G::consts(T, k);
+    double kh[G::NK];   // held across the loop unless RK (then unused)
+    if constexpr (!RK) G::consts(T, kh);
     // first step: the size the previous solve of this cell ended with (OpenFOAM's per-cell deltaTChem)
     const double hp = stats[2 * n + c];
     double t = 0.0, h = hp > 0.0 ? fmin(dt, hp) : dt;
@@ -573,41 +581,52 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
       if (steps + rejects >= max_steps) { steps = -1; break; }
       if (t + h > dt) h = dt - t;
       const double hg = h * g, rh = 1.0 / h;
-      double f0[S], A[S * S];
-      G::wdot(T, k, y, f0);
+      double f0[SA], A[SA * SA];
 #pragma unroll
-      for (int e = 0; e < S * S; ++e) A[e] = 0.0;
-      G::jac(T, k, y, A);
+      for (int e = 0; e < SA * SA; ++e) A[e] = 0.0;
+      if constexpr (RK) {
+        G::rates_jac(T, y, f0, A);
+      } else {
+        G::wdot(T, kh, y, f0);
+        G::jac(T, kh, y, A);
+      }
 #pragma unroll
-      for (int e = 0; e < S * S; ++e) A[e] = (e % (S + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
+      for (int e = 0; e < SA * SA; ++e) A[e] = (e % (SA + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
       bool ok = G::factor(A);
-      double err = 0.0, yn[S];
+      double err = 0.0, yn[SA];
       if (ok) {
-        double k1[S], k2[S], k3[S], y2[S], f2[S];
+        double k1[SA], k2[SA], k3[SA], y2[S], f2[SA];
 #pragma unroll
-        for (int i = 0; i < S; ++i) k1[i] = hg * f0[i];
+        for (int a = 0; a < SA; ++a) k1[a] = hg * f0[a];
         G::solve(A, k1);
 #pragma unroll
-        for (int i = 0; i < S; ++i) y2[i] = y[i] + k1[i];
-        G::wdot(T, k, y2, f2);
+        for (int i = 0; i < S; ++i) y2[i] = y[i];
 #pragma unroll
-        for (int i = 0; i < S; ++i) k2[i] = hg * (f2[i] + c21 * rh * k1[i]);
+        for (int a = 0; a < SA; ++a) y2[G::ACT[a]] = y[G::ACT[a]] + k1[a];
+        if constexpr (RK) {
+          G::rates(T, y2, f2);
+        } else {
+          G::wdot(T, kh, y2, f2);
+        }
+#pragma unroll
+        for (int a = 0; a < SA; ++a) k2[a] = hg * (f2[a] + c21 * rh * k1[a]);
         G::solve(A, k2);
 #pragma unroll
-        for (int i = 0; i < S; ++i) k3[i] = hg * (f2[i] + rh * (c31 * k1[i] + c32 * k2[i]));
+        for (int a = 0; a < SA; ++a) k3[a] = hg * (f2[a] + rh * (c31 * k1[a] + c32 * k2[a]));
         G::solve(A, k3);
 #pragma unroll
-        for (int i = 0; i < S; ++i) {
-          yn[i] = y[i] + k1[i] + m2 * k2[i] + m3 * k3[i];
-          const double e = (e1 * k1[i] + e2 * k2[i] + e3 * k3[i]) / (sc[i] + rtol * fmax(fabs(y[i]), fabs(yn[i])));
-          err += e * e;   // weighted RMS error norm (KPP / CVODE)
+        for (int a = 0; a < SA; ++a) {
+          const int i = G::ACT[a];
+          yn[a] = y[i] + k1[a] + m2 * k2[a] + m3 * k3[a];
+          const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) / (atol * rho / G::W[i] + rtol * fmax(fabs(y[i]), fabs(yn[a])));
+          err += e * e;   // weighted RMS error norm (KPP / CVODE) over all S species (inactive terms are 0)
         }
         err = sqrt(err / S);
         if (!(err == err)) ok = false;
       }
       if (ok && err <= 1.0) {
 #pragma unroll
-        for (int i = 0; i < S; ++i) y[i] = yn[i];
+        for (int a = 0; a < SA; ++a) y[G::ACT[a]] = yn[a];
         t += h;
         ++steps;
         const double fac = err > 0.0 ? 0.9 * pow(err, -1.0 / 3.0) : 5.0;
@@ -620,10 +639,11 @@ __global__ void __launch_bounds__(LANES) k_chem_gen(long n, const int* __restric
     }
     if (steps >= 0) hnext = h;
   }
+  const double rho_rr = rhof[c];   // Y0 and rho_rr re-read here rather than held through the integration
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double Yn = y[i] * G::W[i] / rho;
-    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho_rr / dt : 0.0;
+    RR[(long)i * n + c] = T >= Tmin ? (Yn - Yf[(long)i * n + c]) * rho_rr / dt : 0.0;
   }
   stats[c] = steps;
   stats[n + c] = rejects;
@@ -701,14 +721,19 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   }
   if (h.generated) {
     KScope _ks(x, "k_chem");
-    if (h.generated == 1)
-      hipLaunchKernelGGL(k_chem_gen<ChemGen_burke9>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
-                         x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats,
-                         h.fail.p);
-    else
-      hipLaunchKernelGGL(k_chem_gen<ChemGen_es80>, g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"),
-                         x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats,
-                         h.fail.p);
+    // DFMI_CHEM_RECOMP=0: rate constants held across the step loop (k_chem_gen<G, false, 1>); DFMI_CHEM_WAVES=2:
+    // the inline-constant form compiled for two waves per SIMD (A/B)
+    static const bool rk = [] { const char* e = std::getenv("DFMI_CHEM_RECOMP"); return e && std::atoi(e) != 0; }();
+    static const int wv = [] { const char* e = std::getenv("DFMI_CHEM_WAVES"); return e ? std::atoi(e) : 1; }();
+#define GEN(G, RK, WV) hipLaunchKernelGGL((k_chem_gen<G, RK, WV>), g, dim3(LANES), 0, x.stream, (long)x.C, perm,  \
+                                          x.f("T"), x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin,          \
+                                          h.max_steps, x.f("RR"), stats, h.fail.p)
+    if (h.generated == 1) {
+      if (!rk) GEN(ChemGen_burke9, false, 1); else if (wv == 2) GEN(ChemGen_burke9, true, 2); else GEN(ChemGen_burke9, true, 1);
+    } else {
+      if (!rk) GEN(ChemGen_es80, false, 1); else if (wv == 2) GEN(ChemGen_es80, true, 2); else GEN(ChemGen_es80, true, 1);
+    }
+#undef GEN
     DFMI_HIP(hipGetLastError());
     chem_fail_snapshot(x);
     return;

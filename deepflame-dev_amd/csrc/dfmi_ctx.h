@@ -438,6 +438,7 @@ struct HaloItem {
   int ncomp;
   long cstride, dstride;
   bool to_slots;
+  bool split = false;   // the source vector is stored in the even-odd row order (Ell::eo): send value[eo_pos[cell]]
 };
 bool halo_active(const Ctx& x);
 void halo_update(Ctx& x, const HaloItem* items, int n);
@@ -473,6 +474,8 @@ inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
 // allgather of `count` doubles per rank: recv[r * count + i]
 void halo_allgather(Ctx& x, const double* send, double* recv, long count);
 std::string comm_report(Ctx& x);   // JSON of the communication accounting (CommStats)
+std::vector<int> halo_peers_of(const Ctx& x);   // neighbour rank of every halo index (processor face)
+void halo_set_split(Ctx& x);   // the send map of split (even-odd) vectors, after build_ell decided the layout
 void halo_setup(Ctx& x);   // builds the exchange lists after dfmi_set_comm_info / dfmi_set_comm_local
 void halo_init_rccl(Ctx& x, const void* uid, int nranks, int rank);
 void halo_init_local(Ctx& x, int hub_id, int nranks, int rank);

@@ -125,6 +125,8 @@ struct Halo {
   std::vector<int> peers;                   // ascending
   std::vector<long> pf_off, pf_cnt;         // per peer: first halo index, faces
   DevBuf<int> send_cells, recv_slots, h_off, h_cnt;   // per halo index
+  std::vector<int> h_cells;                 // send_cells on the host
+  DevBuf<int> send_pos;                     // eo_pos[send_cells]: rows of split (even-odd) vectors
   DevBuf<double> sbuf, rbuf;
   std::vector<long> off, cnt;               // per peer, in doubles, for the current exchange
   // overlapped exchanges (halo_begin / halo_end): pack, transfer and unpack run on their own stream
@@ -175,8 +177,10 @@ __global__ void k_unpack(int H, int K, PackArgs a, const int* __restrict__ slots
 // pack, send/receive and unpack on stream st (x.stream: in order with the compute; the comm stream:
 // overlapped, the kernel timers are not used there)
 void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<double*>& dst, bool to_slots,
-              hipStream_t st) {
+              hipStream_t st, bool split = false) {
   Halo& h = *x.halo;
+  DFMI_CHECK(!split || h.send_pos.n == h.send_cells.n, "halo: split vectors before halo_set_split");
+  const int* sc = split ? h.send_pos.p : h.send_cells.p;
   const bool timed = st == x.stream;
   const int K = (int)src.size();
   for (int k0 = 0; k0 < K; k0 += MAXK) {
@@ -186,7 +190,7 @@ void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<d
     dim3 g(blocks_for(x.H, 256), kk);
     {
       KScope _ks(x, timed ? "k_halo_pack" : nullptr);
-      hipLaunchKernelGGL(k_pack, g, dim3(256), 0, st, x.H, kk, a, h.send_cells.p, h.h_off.p, h.h_cnt.p, h.sbuf.p);
+      hipLaunchKernelGGL(k_pack, g, dim3(256), 0, st, x.H, kk, a, sc, h.h_off.p, h.h_cnt.p, h.sbuf.p);
     }
     DFMI_HIP(hipGetLastError());
     h.off.resize(h.peers.size()); h.cnt.resize(h.peers.size());
@@ -212,11 +216,14 @@ void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<d
   }
 }
 
-void collect(const HaloItem* items, int n, std::vector<const double*>& src, std::vector<double*>& dst, bool& slots) {
+void collect(const HaloItem* items, int n, std::vector<const double*>& src, std::vector<double*>& dst, bool& slots,
+             bool& split) {
   slots = true;
+  split = false;
   for (int i = 0; i < n; ++i) {
-    if (i == 0) slots = items[i].to_slots;
+    if (i == 0) { slots = items[i].to_slots; split = items[i].split; }
     DFMI_CHECK(items[i].to_slots == slots, "halo_update: mixed slot / vector destinations");
+    DFMI_CHECK(items[i].split == split, "halo_update: mixed cell / even-odd row orders");
     for (int k = 0; k < items[i].ncomp; ++k) {
       src.push_back(items[i].cell + k * items[i].cstride);
       dst.push_back(items[i].dst + k * items[i].dstride);
@@ -231,9 +238,9 @@ void halo_update(Ctx& x, const HaloItem* items, int n) {
   DFMI_CHECK(!x.halo->pending, "halo_update while an overlapped exchange is in flight");
   std::vector<const double*> src;
   std::vector<double*> dst;
-  bool slots = true;
-  collect(items, n, src, dst, slots);
-  if (!src.empty()) exchange(x, src, dst, slots, x.stream);
+  bool slots = true, split = false;
+  collect(items, n, src, dst, slots, split);
+  if (!src.empty()) exchange(x, src, dst, slots, x.stream, split);
 }
 
 bool halo_overlap(const Ctx& x) { return halo_active(x) && x.halo_overlap; }
@@ -251,11 +258,11 @@ void halo_begin(Ctx& x, const HaloItem* items, int n) {
   }
   std::vector<const double*> src;
   std::vector<double*> dst;
-  bool slots = true;
-  collect(items, n, src, dst, slots);
+  bool slots = true, split = false;
+  collect(items, n, src, dst, slots, split);
   DFMI_HIP(hipEventRecord(h.ev_start, x.stream));
   DFMI_HIP(hipStreamWaitEvent(h.cs, h.ev_start, 0));
-  if (!src.empty()) exchange(x, src, dst, slots, h.cs);
+  if (!src.empty()) exchange(x, src, dst, slots, h.cs, split);
   DFMI_HIP(hipEventRecord(h.ev_done, h.cs));
   h.pending = true;
 }
@@ -343,6 +350,8 @@ void halo_setup(Ctx& x) {
   x.H = (int)cells.size();
   if (x.H == 0) { cells.push_back(0); slots.push_back(0); hoff.push_back(0); hcnt.push_back(1); }
   h.send_cells.upload(cells, x.stream); h.recv_slots.upload(slots, x.stream);
+  h.h_cells = cells;
+  h.send_pos.release();
   h.sbuf.alloc((size_t)std::max(x.H, 1) * MAXK);   // sized once: peers may still read it asynchronously
   h.rbuf.alloc((size_t)std::max(x.H, 1) * MAXK);
   h.h_off.upload(hoff, x.stream); h.h_cnt.upload(hcnt, x.stream);
@@ -363,6 +372,25 @@ void halo_setup(Ctx& x) {
                    " disagree (" + std::to_string(all[(size_t)x.rank * R + q]) + " vs " +
                    std::to_string(all[(size_t)q * R + x.rank]) + ")");
   x.ell.ready = false;   // solver columns now include halo entries
+}
+
+std::vector<int> halo_peers_of(const Ctx& x) {
+  std::vector<int> pr(std::max(x.H, 0), -1);
+  if (!x.halo) return pr;
+  const Halo& h = *x.halo;
+  for (size_t i = 0; i < h.peers.size(); ++i)
+    for (long k = 0; k < h.pf_cnt[i]; ++k) pr[h.pf_off[i] + k] = h.peers[i];
+  return pr;
+}
+
+void halo_set_split(Ctx& x) {
+  Halo& h = *x.halo;
+  const std::vector<int>& pos = x.ell.h_eo_pos;
+  DFMI_CHECK(x.ell.eo && (int)pos.size() == x.C, "halo_set_split: no even-odd layout");
+  std::vector<int> sp(h.h_cells.size());
+  for (size_t i = 0; i < sp.size(); ++i) sp[i] = x.H > 0 ? pos[h.h_cells[i]] : 0;
+  h.send_pos.upload(sp, x.stream);
+  DFMI_HIP(hipStreamSynchronize(x.stream));
 }
 
 // ---- communicator creation (used by capi.cpp)

@@ -1088,10 +1088,10 @@ template <class F> void dispatch_W(int W, F&& f) {
   }
 }
 
-void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce) {
+void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce, bool split = false) {
   if (!halo_active(x)) return;
   std::vector<HaloItem> it;
-  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false});
+  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false, split});
   halo_update(x, it.data(), (int)it.size());
 }
 
@@ -1284,19 +1284,26 @@ void build_ell(Ctx& x) {
       if (ok) { x.hex[0] = nx; x.hex[1] = ny; x.hex[2] = nz; }
     }
   }
-  // even-odd layout of the BiCGStab rows (k_eo_*): one rank, no halo, not the one-workgroup small solves,
-  // and a coupling graph that 2-colours -- every ELL entry couples the other colour (cyclic partners
-  // included; a periodic direction of odd extent does not colour and keeps the Jacobi path).
-  // DFMI_BCG_EO=0: off
+  // even-odd layout of the BiCGStab rows (k_eo_*): not the one-workgroup small solves, and a coupling graph
+  // that 2-colours -- every ELL entry couples the other colour (cyclic partners included; a periodic direction
+  // of odd extent does not colour and keeps the Jacobi path). Several ranks: each rank's (connected) local
+  // graph is coloured, the colours across every processor face are exchanged, and the ranks' flips are solved
+  // from the all-gathered relations so that every processor face couples the two colours too -- the same
+  // decision on every rank. DFMI_BCG_EO=0: off
   x.ell.eo = 0;
   x.ell.eo_ncls = 0;
   x.ell.h_eo_pos.clear();
-  if (const char* e = std::getenv("DFMI_BCG_EO"); !(e && std::atoi(e) == 0) && x.nranks == 1 && !halo_active(x) &&
-                                                  !small_solve(x) && C >= 2) {
-    std::vector<int> colr(C, -1), q;
-    bool bip = true;
+  const bool multi = x.nranks > 1 && x.halo != nullptr;
+  if (const char* e = std::getenv("DFMI_BCG_EO");
+      !(e && std::atoi(e) == 0) && !small_solve(x) && (multi || !halo_active(x))) {
+    std::vector<int> colr(C, 0), q;
+    std::vector<char> seen(C, 0);
+    bool bip = C >= 2;
+    int ncomp = 0;
     for (int c0 = 0; c0 < C && bip; ++c0) {
-      if (colr[c0] >= 0) continue;
+      if (seen[c0]) continue;
+      ++ncomp;
+      seen[c0] = 1;
       colr[c0] = 0;
       q.assign(1, c0);
       for (size_t h = 0; h < q.size() && bip; ++h) {
@@ -1304,15 +1311,76 @@ void build_ell(Ctx& x) {
         for (int k = 0; k < W; ++k) {
           if (src[(size_t)k * C + c] == PAD) continue;
           const int j = col[(size_t)k * C + c];
+          if (j >= C && multi) continue;   // a processor column: checked across ranks below
           if (j < 0 || j >= C || j == c) { bip = false; break; }
-          if (colr[j] < 0) { colr[j] = 1 - colr[c]; q.push_back(j); }
+          if (!seen[j]) { seen[j] = 1; colr[j] = 1 - colr[c]; q.push_back(j); }
           else if (colr[j] == colr[c]) { bip = false; break; }
         }
       }
     }
     int ne = 0;
     for (int c = 0; c < C; ++c) ne += colr[c] == 0;
-    if (bip && ne > 0 && ne < C) {
+    bip = bip && ne > 0 && ne < C;
+    if (multi) {
+      // colour of the cell across every processor face -> per peer the flip relation f_rank ^ f_peer this rank
+      // needs (one value for all its faces with that peer, else 2); all-gathered with a local ok flag
+      const int R = x.nranks;
+      const long Ce = (long)C + x.H;
+      std::vector<double> cd(Ce, 0.0);
+      for (int c = 0; c < C; ++c) cd[c] = colr[c];
+      DevBuf<double> dcd;
+      dcd.upload(cd, x.stream);
+      if (halo_active(x)) {
+        HaloItem it{dcd.p, dcd.p, 1, Ce, Ce, false};
+        halo_update(x, &it, 1);
+      }
+      DFMI_HIP(hipMemcpyAsync(cd.data(), dcd.p, Ce * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      const std::vector<int> peer = halo_peers_of(x);
+      std::vector<double> row(R + 1, -1.0);
+      row[R] = (bip && ncomp == 1) ? 1.0 : 0.0;
+      for (int c = 0; c < C; ++c)
+        for (int k = 0; k < W; ++k) {
+          const int j = col[(size_t)k * C + c];
+          if (src[(size_t)k * C + c] == PAD || j < C) continue;
+          const int pr = peer[j - C];
+          const double d = (double)(1 ^ colr[c] ^ (int)cd[j]);
+          if (row[pr] < 0) row[pr] = d;
+          else if (row[pr] != d) row[pr] = 2.0;
+        }
+      DevBuf<double> sb, rb;
+      sb.upload(row, x.stream);
+      rb.alloc((size_t)R * (R + 1));
+      halo_allgather(x, sb.p, rb.p, R + 1);
+      std::vector<double> all((size_t)R * (R + 1));
+      DFMI_HIP(hipMemcpyAsync(all.data(), rb.p, all.size() * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+      DFMI_HIP(hipStreamSynchronize(x.stream));
+      bool ok = true;
+      for (int r = 0; r < R; ++r) ok = ok && all[(size_t)r * (R + 1) + R] == 1.0;
+      std::vector<int> f(R, -1);
+      for (int r0 = 0; r0 < R && ok; ++r0) {   // flips: BFS over the rank graph, the same on every rank
+        if (f[r0] >= 0) continue;
+        f[r0] = 0;
+        std::vector<int> rq(1, r0);
+        for (size_t a = 0; a < rq.size() && ok; ++a) {
+          const int r = rq[a];
+          for (int qr = 0; qr < R && ok; ++qr) {
+            const double d = all[(size_t)r * (R + 1) + qr], d2 = all[(size_t)qr * (R + 1) + r];
+            if (d < 0) continue;
+            if (d > 1.5 || (d2 >= 0 && d2 != d)) { ok = false; break; }
+            const int fq = f[r] ^ (int)d;
+            if (f[qr] < 0) { f[qr] = fq; rq.push_back(qr); }
+            else if (f[qr] != fq) ok = false;
+          }
+        }
+      }
+      bip = ok;
+      if (ok && f[x.rank] == 1) {
+        for (int c = 0; c < C; ++c) colr[c] ^= 1;
+        ne = C - ne;
+      }
+    }
+    if (bip) {
       const int no = C - ne;
       std::vector<int> pos(C), cell(C);
       for (int c = 0, a = 0, o = ne; c < C; ++c) {
@@ -1323,23 +1391,28 @@ void build_ell(Ctx& x) {
       for (int c = 0; c < C; ++c) {
         const int i = pos[c];
         for (int k = 0; k < W; ++k) {
+          const int j = col[(size_t)k * C + c];
           int jj;
           if (src[(size_t)k * C + c] == PAD)   // value 0: any row of the other colour (the same offset where possible)
             jj = colr[c] == 0 ? ne + std::min(i, no - 1) : std::min(i - ne, ne - 1);
-          else jj = pos[col[(size_t)k * C + c]];
+          else jj = j >= C ? j : pos[j];        // processor columns keep their halo index C + h
           ecol[(size_t)k * C + i] = jj;
         }
       }
       x.ell.eo_pos.upload(pos, x.stream);
       x.ell.eo_cell.upload(cell, x.stream);
       x.ell.eo_col.upload(ecol, x.stream);
-      // row classes of the reordered rows (column offsets only: the solver reads no sources)
+      // row classes of the reordered rows (column offsets only: the solver reads no sources; halo columns
+      // stay explicit)
       std::map<std::vector<int>, int> ids;
       std::vector<uint8_t> cls(C);
       std::vector<int> key(W);
       bool ok = true;
       for (int i = 0; i < C && ok; ++i) {
-        for (int k = 0; k < W; ++k) key[k] = ecol[(size_t)k * C + i] - i;
+        for (int k = 0; k < W; ++k) {
+          const int jj = ecol[(size_t)k * C + i];
+          key[k] = jj >= C ? CEXPL : jj - i;
+        }
         auto it = ids.find(key);
         if (it == ids.end()) {
           if (ids.size() >= 255) { ok = false; break; }
@@ -1358,6 +1431,7 @@ void build_ell(Ctx& x) {
       x.ell.h_eo_pos = pos;
       x.ell.ne = ne;
       x.ell.eo = 1;
+      if (multi) halo_set_split(x);
     }
   }
   // row classes: per cell the W (column offset, source code) pairs; coupled slots keep explicit sources
@@ -1547,7 +1621,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, smap, b.xw, eopos); }
   DFMI_HIP(hipGetLastError());
-  if (x.ell.eo) {   // the reduced system (one rank, no halo: build_ell decided)
+  if (x.ell.eo) {   // the reduced system (build_ell decided; several ranks: split-vector halos, gathered sums)
     const int ne = x.ell.ne, no = (int)C - ne;
     const int hb = std::min(blocks_for(std::max(ne, no), TPB), MAX_BLOCKS);
     const dim3 gh(hb, nsys);
@@ -1557,18 +1631,27 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     double* pR = pR3 + (size_t)nsys * hb * 3;      // (||D r||^2, 0): the update
     double* pV = pR + (size_t)nsys * hb * 2;       // r0.v
     double* pT = pV + (size_t)nsys * hb;           // (t.s, t.t, r0.t, r0.s)
-    const Red rI{pI, hb, 1, (long)hb}, rR3{pR3, hb, 3, (long)hb * 3}, rR{pR, hb, 2, (long)hb * 2},
-        rV{pV, hb, 1, (long)hb}, rT{pT, hb, 4, (long)hb * 4};
+    // exchange points (several ranks): every kernel that gathers across a processor face reads the other
+    // colour's rows of the vector it gathers, exchanged just before it
+    auto hx = [&](std::initializer_list<double*> v) { halo_vecs(x, v, nsys, Ce, true); };
+    hx({b.xw});
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_init");
       hipLaunchKernelGGL(k_eo_init_e<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, b, pI);
+    });
+    const Red rI = L.after(pI, 1, 1, hb);
+    hx({b.p});
+    dispatch_W(W, [&](auto wt) {
+      constexpr int WT = decltype(wt)::value;
+      KScope _ks(x, "k_bcg_init");
       hipLaunchKernelGGL(k_eo_init_o<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, b, pR3);
     });
     DFMI_HIP(hipGetLastError());
+    Red red = L.after(pR3, 3, 0, hb);
     Poller poll(x, WS.scal.p, nsys);
-    Red red = rR3;
     for (int it = 0;; ++it) {
+      hx({b.p});
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_eo");
@@ -1576,17 +1659,32 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
                            cfg.abs_tol, rI, red, WS.scal.p, b);
       });
       if (it >= cfg.max_iter) break;
+      hx({b.p});
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
-        { KScope _ks(x, "k_bcg_eo"); hipLaunchKernelGGL(k_eo_b<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pV); }
-        { KScope _ks(x, "k_bcg_eo"); hipLaunchKernelGGL(k_eo_c<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, rV, WS.scal.p, b); }
-        { KScope _ks(x, "k_bcg_eo"); hipLaunchKernelGGL(k_eo_d<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pT); }
+        KScope _ks(x, "k_bcg_eo");
+        hipLaunchKernelGGL(k_eo_b<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pV);
       });
+      const Red rV = L.after(pV, 1, 0, hb);
+      hx({b.r, b.v});
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_bcg_eo");
+        hipLaunchKernelGGL(k_eo_c<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, rV, WS.scal.p, b);
+      });
+      hx({b.t});
+      dispatch_W(W, [&](auto wt) {
+        constexpr int WT = decltype(wt)::value;
+        KScope _ks(x, "k_bcg_eo");
+        hipLaunchKernelGGL(k_eo_d<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pT);
+      });
+      const Red rT = L.after(pT, 4, 0, hb);
       { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_eo_xp, gh, bl, 0, x.stream, Ce, ne, no, rT, WS.scal.p, b, pR); }
       DFMI_HIP(hipGetLastError());
-      red = rR;
+      red = L.after(pR, 2, 0, hb);
       if ((it + 1) % 2 == 0 && poll.snapshot_and_test()) break;
     }
+    hx({b.xw});
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_eo_final");
