@@ -28,6 +28,8 @@ sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
 PMC_FILE = "r03_pmc_traffic.json"
+PMC_FLOPS_FILE = "r04_pmc_flops.json"   # scripts/pmc_flops.sh: FP64 FLOPs per dispatch (SQ_INSTS_VALU_FLOPS_FP64)
+FP64_PEAK_TFS = 78.6                    # MI355X FP64 vector peak
 
 MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species table made by dfmi.transport_fit
     "burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
@@ -668,6 +670,17 @@ def main():
             ent = [v for v in ent if v["hbm_bytes_mean"] >= 0.01 * top]
             nd = sum(v["dispatches"] for v in ent)
             pmc[fam] = {"hbm_bytes_mean": sum(v["hbm_bytes_mean"] * v["dispatches"] for v in ent) / nd}
+    # FP64 FLOPs per dispatch of the VALU-bound kernels (thermo, chemistry) from the committed PMC pass of the same
+    # workload: their roofline is counted FLOPs / the FP64 vector peak, not bytes / the HBM peak
+    flops_tab = {}
+    fl_path = os.path.join(ROOT, "profiles", PMC_FLOPS_FILE)
+    if os.path.exists(fl_path) and n == 128 and world == 1:
+        for key, v in json.load(open(fl_path)).items():
+            short = key.split("::")[-1]
+            for fam in ("k_thermo_cells", "k_chem"):
+                if short.startswith(fam + "<") or short.startswith(fam + "_gen<"):
+                    if v["flops"] > flops_tab.get(fam, {}).get("flops", -1.0):
+                        flops_tab[fam] = {"flops": v["flops"], "kernel": key}
     Bc = m.n_coupled_slots
     # BiCGStab: two operator applications per system-iteration, full SpMVs (k_bcg_spmv) or applications of
     # the even-odd Schur complement (k_bcg_eo); only one of the two runs
@@ -696,13 +709,22 @@ def main():
         achieved = total_bytes / (ms / 1e3) / 1e9
         achieved_impl = total_impl / (ms / 1e3) / 1e9
         tr = pmc.get(k)
-        roofs[k] = {"kernel": k, "bound": "hbm" if k != "k_thermo_cells" else "fp64-valu",
+        roofs[k] = {"kernel": k, "bound": "hbm",
                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS,
                     "traffic": tr["hbm_bytes_mean"] if tr else None,
                     "algorithmic_bytes": total_bytes / nl, "launches": nl, "work_units": units[k],
                     "bytes_per_unit": per_unit, "avg_us": ms * 1e3 / nl, "total_ms": ms,
                     "impl_bytes": total_impl / nl, "frac_impl": achieved_impl / HBM_PEAK_GBS}
+        if k == "k_thermo_cells":   # FP64-VALU bound: counted FLOPs against the FP64 vector peak
+            fl = flops_tab.get(k)
+            tfs = fl["flops"] * nl / (ms / 1e3) / 1e12 if fl else None
+            roofs[k].update({"bound": "fp64-valu", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS, "achieved": tfs,
+                             "frac": tfs / FP64_PEAK_TFS if tfs is not None else None,
+                             "flops_per_launch": fl["flops"] if fl else None,
+                             "flops_source": f"profiles/{PMC_FLOPS_FILE} (SQ_INSTS_VALU_FLOPS_FP64 + _TRANS, mean per dispatch)"
+                             if fl else "no PMC FLOP counts for this workload",
+                             "hbm_achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS})
     hbm = {k: v for k, v in roofs.items() if v["bound"] == "hbm"}
     primary = args.kernel if args.kernel != "auto" else (max(hbm, key=lambda k: hbm[k]["total_ms"]) if hbm else None)
     out = {
@@ -737,8 +759,9 @@ def main():
                               "steps after the timed region (the headline runs with no events armed); algorithmic_bytes "
                               "and traffic are per launch; impl_bytes / frac_impl: the bytes this implementation must "
                               "move (gather rows decoded from row classes: 1 B per cell instead of the ids)"),
-        "rooflines": {k: {kk: v[kk] for kk in ("bound", "achieved", "frac", "traffic", "algorithmic_bytes", "avg_us",
-                                               "launches", "impl_bytes", "frac_impl")} for k, v in roofs.items()},
+        "rooflines": {k: {kk: v[kk] for kk in ("bound", "unit", "peak", "achieved", "frac", "traffic", "algorithmic_bytes",
+                                               "avg_us", "launches", "impl_bytes", "frac_impl", "flops_per_launch",
+                                               "hbm_frac") if kk in v} for k, v in roofs.items()},
         "solver_iters": {e: s[0] for e, s in stats.items()},
         "solver_work_roof_pass": work,
         "solver_work_run": {"system_iterations": {e: work_pre[e] + work[e] for e in work},
@@ -757,6 +780,13 @@ def main():
         "chemistry": ({"integrator": "ROS3 Rosenbrock (order 3, adaptive), rtol 1e-6 atol 1e-10",
                        "chem_integrations_per_s": m.n_cells * world * chem_n / (chem_ms / 1e3) if chem_n else None,
                        "k_chem_ms_per_step": chem_ms / max(chem_n, 1),
+                       "valu_roofline": ({"bound": "fp64-valu", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS,
+                                          "flops_per_launch": flops_tab["k_chem"]["flops"],
+                                          "achieved": flops_tab["k_chem"]["flops"] * chem_n / (chem_ms / 1e3) / 1e12,
+                                          "frac": flops_tab["k_chem"]["flops"] * chem_n / (chem_ms / 1e3) / 1e12 / FP64_PEAK_TFS,
+                                          "kernel": flops_tab["k_chem"]["kernel"],
+                                          "flops_source": f"profiles/{PMC_FLOPS_FILE}"}
+                                         if "k_chem" in flops_tab and chem_n else None),
                        "k_bin_ms_per_step": bin_ms / max(chem_n, 1),
                        **chem_step_stats(ctx, m.n_cells)} if args.chem == "ode" else None),
         "dnn": ({"reacting_cells": n_react, "gemm_launches": gemm_n, "gemm_ms_total": gemm_ms,

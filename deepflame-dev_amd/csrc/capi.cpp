@@ -192,23 +192,61 @@ void do_U(Ctx& x) {
                  x.f("U"), x.C, x.solver["U"]);
   u_post_solve(x);
 }
-void do_Y(Ctx& x) {
+// YEqn up to its assembled rows: the chemistry source, the preparation terms and the rows (no host
+// synchronisation inside, so dfmi_time_step can issue it on the side stream beside the UEqn)
+void do_Y_front(Ctx& x) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
+  YWs _yw(x);
   // chemistry->solve(deltaT) before YEqn (YEqn.H); the thermo density of that call is rho before this
   // step's rhoEqn, i.e. rho_old (dfChemistryModel.C:87,771; the GPU reference passes d_rho_old, dfYEqn.cu:449)
   if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt, "rho_old");
   else if (x.chem.mode == 2) dnn_solve(x, "rho_old");   // chemistrySolver_GPU.Inference (YEqn_GPU.H)
   y_prep(x);
+  // production path: the assembly writes the solver's ELL rows directly (no LDU round trip)
+  double *val, *dS, *rhs;
+  bicg_layout(x, x.S - 1, &val, &dS, &rhs);
+  y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
+}
+void do_Y_back(Ctx& x) {
+  YWs _yw(x);
   Matrix& A = x.mY;
   std::vector<int> map;
   for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
-  // production path: the assembly writes the solver's ELL rows directly (no LDU round trip)
-  double *val, *dS, *rhs;
-  bicg_layout(x, (int)map.size(), &val, &dS, &rhs);
-  y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
   solve_bicgstab(x, "Y", (int)map.size(), map.data(), A.lower, x.Fs, A.upper, x.Fs, A.diag, x.C, A.source, x.C, A.ic,
                  A.bc, x.B, "Y", x.f("Y"), x.C, x.solver["Y"], true);
   y_post_solve(x);
+}
+void do_Y(Ctx& x) {
+  do_Y_front(x);
+  do_Y_back(x);
+}
+
+// The chemistry and the YEqn preparation/assembly read nothing the UEqn writes (T, p, Y, rho_old, phi, the
+// thermo's transport from the last correctThermo) and the UEqn nothing they write, so on one rank they run on
+// the side stream while the UEqn assembles and solves on the main one: the VALU-bound chemistry beside the
+// memory-bound UEqn. Both are issued before the UEqn's convergence polls block the host. Several ranks keep
+// one stream (every RCCL operation of a rank stays ordered on one communicator). DFMI_STEP_OVERLAP=0: off.
+bool step_overlap(const Ctx& x) {
+  static const bool on = [] { const char* e = std::getenv("DFMI_STEP_OVERLAP"); return !(e && std::atoi(e) == 0); }();
+  return on && x.nranks == 1 && !halo_active(x);
+}
+void do_U_Y(Ctx& x) {
+  if (!step_overlap(x)) { do_U(x); do_Y(x); return; }
+  if (!x.stream2) {
+    DFMI_HIP(hipStreamCreateWithFlags(&x.stream2, hipStreamNonBlocking));
+    DFMI_HIP(hipEventCreateWithFlags(&x.ev_fork, hipEventDisableTiming));
+    DFMI_HIP(hipEventCreateWithFlags(&x.ev_join, hipEventDisableTiming));
+  }
+  DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
+  DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_fork, 0));
+  {
+    OnStream _os(x, x.stream2);
+    do_Y_front(x);
+    DFMI_HIP(hipEventRecord(x.ev_join, x.stream2));
+  }
+  do_U(x);
+  DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_join, 0));
+  do_Y_back(x);
 }
 void do_E(Ctx& x) {
   e_assemble(x);
@@ -588,8 +626,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     copy_old(x);                    // preTimeStep
     if (x.chem.mode == 2) dnn_prepare(x);   // reacting cells of this step's T (read after the UEqn polls)
     rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
-    do_U(x);                        // UEqn
-    do_Y(x);                        // YEqn
+    do_U_Y(x);                      // UEqn, YEqn (one rank: the chemistry and YEqn assembly beside the UEqn)
     do_E(x);                        // EEqn
     thermo_correct(x, false);       // correctThermo
     for (int i = 0; i < n_corr; ++i) {   // pEqn_GPU.H
@@ -706,6 +743,7 @@ int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
       if (!x.fields.count("dbg_gradY")) alloc_field(x, "dbg_gradY", x.C, 3 * x.S, false);
       y_prep(x); y_assemble(x);
     } else if (e == "Y_ell") {        // production: fused assembly straight into the solver rows
+      YWs _yw(x);
       std::vector<int> map;
       for (int s = 0; s < x.S; ++s) if (s != x.inert) map.push_back(s);
       double *val, *dS, *rhs;
@@ -713,6 +751,7 @@ int dfmi_assemble(dfmi_ctx* ctx, const char* eqn) {
       y_prep(x);
       y_assemble_ell(x, x.ell.W, (long)x.C + x.H, val, dS, rhs);
     } else if (e == "Y_ell_ref") {    // LDU assembly folded by the generic solver gather
+      YWs _yw(x);
       y_prep(x); y_assemble(x);
       bicg_rows_from_ldu_Y(x);
     } else if (e == "E") { conv_weights(x); e_assemble(x); }   // EEqn inspected on its own: fresh div(phi,Yi_h) weights
@@ -755,6 +794,7 @@ int dfmi_get_solver_rows(dfmi_ctx* ctx, const char* eqn, const char* part, doubl
   return guard([&] {
     Ctx& x = ctx->x;
     DFMI_CHECK(std::string(eqn) == "Y", "solver rows are inspectable for the YEqn batch only");
+    YWs _yw(x);
     bicg_rows_get(x, x.S - 1, part, host, count);
   });
 }

@@ -287,7 +287,14 @@ struct Ctx {
     DevBuf<int> sysmap;
     PinnedBuf<double> poll;          // two convergence snapshots (linsolve.hip: Poller)
     hipEvent_t ev[2] = {nullptr, nullptr};
-  } ws;
+  } ws, ws_y;
+  // the YEqn batch has its own solver workspace (its rows are assembled while the UEqn solve may still be
+  // running on the other stream, dfmi_time_step); linsolve.hip reaches the current one through sws()
+  bool ws_is_y = false;
+  SolverWs& sws() { return ws_is_y ? ws_y : ws; }
+  // side stream of the time step (dfmi_time_step: chemistry + YEqn preparation beside the UEqn) and its events
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // final solver state of the last solve of each equation, copied asynchronously at the end of the
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
@@ -346,6 +353,21 @@ struct Ctx {
     DFMI_CHECK(it != ptype.end(), "patch types not set for field '" + field + "'");
     return it->second;
   }
+};
+
+// The YEqn workspace (Ctx::ws_y) for the scope's solver calls.
+struct YWs {
+  Ctx& x;
+  bool prev;
+  explicit YWs(Ctx& c) : x(c), prev(c.ws_is_y) { x.ws_is_y = true; }
+  ~YWs() { x.ws_is_y = prev; }
+};
+// Launches of the scope go to stream s (the launchers all read Ctx::stream).
+struct OnStream {
+  Ctx& x;
+  hipStream_t prev;
+  OnStream(Ctx& c, hipStream_t s) : x(c), prev(c.stream) { x.stream = s; }
+  ~OnStream() { x.stream = prev; }
 };
 
 // Records a start/end event pair around a launch when `name` is the armed kernel.

@@ -146,6 +146,10 @@ Ctx::~Ctx() {
   halo_destroy(halo);
   halo = nullptr;
   for (auto& e : ws.ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : ws_y.ev) if (e) (void)hipEventDestroy(e);
+  if (stream2) { (void)hipStreamSynchronize(stream2); (void)hipStreamDestroy(stream2); }
+  if (ev_fork) (void)hipEventDestroy(ev_fork);
+  if (ev_join) (void)hipEventDestroy(ev_join);
 }
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }

@@ -1065,10 +1065,10 @@ struct Launch {
     if (np == 0) np = nblk;
     if (x.nranks == 1) return Red{partial, np, NV, (long)np * NV};
     const size_t per = (size_t)nsys * 4;   // up to 4 values per system per slot
-    if (x.ws.red_local.n < 2 * per) x.ws.red_local.alloc(2 * per);
-    if (x.ws.red_all.n < 2 * per * x.nranks) x.ws.red_all.alloc(2 * per * x.nranks);
-    double* loc = x.ws.red_local.p + slot * per;
-    double* all = x.ws.red_all.p + slot * per * x.nranks;
+    if (x.sws().red_local.n < 2 * per) x.sws().red_local.alloc(2 * per);
+    if (x.sws().red_all.n < 2 * per * x.nranks) x.sws().red_all.alloc(2 * per * x.nranks);
+    double* loc = x.sws().red_local.p + slot * per;
+    double* all = x.sws().red_all.p + slot * per * x.nranks;
     if (NV == 1) hipLaunchKernelGGL(k_red_local<1>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
     else if (NV == 2) hipLaunchKernelGGL(k_red_local<2>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
     else if (NV == 3) hipLaunchKernelGGL(k_red_local<3>, dim3(nsys), dim3(TPB), 0, x.stream, partial, np, loc);
@@ -1131,19 +1131,19 @@ struct Poller {
   const double* scal;
   int nsys, slot = 0, pending = -1;
   Poller(Ctx& c, const double* s, int n) : x(c), scal(s), nsys(n) {
-    x.ws.poll.ensure((size_t)2 * n * NSCAL);
-    for (auto& e : x.ws.ev)
+    x.sws().poll.ensure((size_t)2 * n * NSCAL);
+    for (auto& e : x.sws().ev)
       if (!e) DFMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   // snapshot now; true when the previous snapshot shows every system stopped
   bool snapshot_and_test() {
-    double* dst = x.ws.poll.p + (size_t)slot * nsys * NSCAL;
+    double* dst = x.sws().poll.p + (size_t)slot * nsys * NSCAL;
     DFMI_HIP(hipMemcpyAsync(dst, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-    DFMI_HIP(hipEventRecord(x.ws.ev[slot], x.stream));
+    DFMI_HIP(hipEventRecord(x.sws().ev[slot], x.stream));
     bool done = false;
     if (pending >= 0) {
-      DFMI_HIP(hipEventSynchronize(x.ws.ev[pending]));
-      const double* h = x.ws.poll.p + (size_t)pending * nsys * NSCAL;
+      DFMI_HIP(hipEventSynchronize(x.sws().ev[pending]));
+      const double* h = x.sws().poll.p + (size_t)pending * nsys * NSCAL;
       done = true;
       for (int s = 0; s < nsys; ++s) done = done && h[s * NSCAL + 6] == 0.0;
     }
@@ -1492,11 +1492,11 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 12 + 64;
-  if (x.ws.buf.n < need) { x.ws.buf.alloc(need); x.ws.buf.zero(x.stream); }   // no stale NaN under a 0 coefficient
+  if (x.sws().buf.n < need) { x.sws().buf.alloc(need); x.sws().buf.zero(x.stream); }   // no stale NaN under a 0 coefficient
   const long N = nsys * Ce;
-  *dS = x.ws.buf.p;
-  *rhs = x.ws.buf.p + N;
-  *val = x.ws.buf.p + BCG_VECS * N;
+  *dS = x.sws().buf.p;
+  *rhs = x.sws().buf.p + N;
+  *val = x.sws().buf.p + BCG_VECS * N;
 }
 
 // the YEqn rows the production path writes straight from the assembly (y_assemble_ell), rebuilt here
@@ -1509,12 +1509,12 @@ void bicg_rows_from_ldu_Y(Ctx& x) {
   double *val, *dS, *rhs;
   bicg_layout(x, nsys, &val, &dS, &rhs);
   const long C = x.C, Ce = (long)x.C + x.H;
-  x.ws.sysmap.upload(map.data(), nsys, x.stream);
+  x.sws().sysmap.upload(map.data(), nsys, x.stream);
   Matrix& A = x.mY;
   Sys q{A.lower, A.upper, A.diag, A.source, A.ic, A.bc, x.Fs, x.Fs, C, C, x.B, x.f("Y"), C};
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
   hipLaunchKernelGGL(k_ell_build, dim3(nblk, nsys), dim3(TPB), 0, x.stream, x.view(), x.st("Y"), q,
-                     (const int*)x.ws.sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs, 0,
+                     (const int*)x.sws().sysmap.p, x.ell.W, x.ell.src.p, Ce, val, dS, rhs, 0,
                      x.ell.eo ? (const int*)x.ell.eo_pos.p : nullptr);
   DFMI_HIP(hipGetLastError());
 }
@@ -1587,7 +1587,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
-  auto& WS = x.ws;
+  auto& WS = x.sws();
   if (WS.scal.n < (size_t)nsys * NSCAL) WS.scal.alloc((size_t)nsys * NSCAL);
   const int* smap = nullptr;
   if (sys_map_host) {
@@ -1755,7 +1755,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
-  auto& WS = x.ws;
+  auto& WS = x.sws();
   const size_t need = 8 * Ce + (size_t)W * C + (size_t)nblk * 6 + 64;
   if (WS.buf.n < need) WS.buf.alloc(need);
   if (WS.scal.n < NSCAL) WS.scal.alloc(NSCAL);
@@ -1826,17 +1826,17 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     if (amg && x.nranks > 1) {
       // several ranks: both sums (r.r from the update, r.z from the V-cycle) go out in ONE all-gather
       // of three values per rank instead of two collectives per iteration
-      if (x.ws.red_local.n < 8) x.ws.red_local.alloc(8);
-      if (x.ws.red_all.n < (size_t)8 * x.nranks) x.ws.red_all.alloc((size_t)8 * x.nranks);
-      double* loc = x.ws.red_local.p;
+      if (x.sws().red_local.n < 8) x.sws().red_local.alloc(8);
+      if (x.sws().red_all.n < (size_t)8 * x.nranks) x.sws().red_all.alloc((size_t)8 * x.nranks);
+      double* loc = x.sws().red_local.p;
       hipLaunchKernelGGL(k_red_local<2>, dim3(1), dim3(TPB), 0, x.stream, q2, nblk, loc);
       if (x.amg.halo_l0) halo_vecs(x, {v.r}, 1, Ce);   // the V-cycle's level 0 reads the residual across ranks
       amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, act);
       hipLaunchKernelGGL(k_red_local<1>, dim3(1), dim3(TPB), 0, x.stream, q3, nblk, loc + 2);
       DFMI_HIP(hipGetLastError());
-      halo_allgather(x, loc, x.ws.red_all.p, 3);
-      rr = Red{x.ws.red_all.p + 1, x.nranks, 3, 0};
-      rz = Red{x.ws.red_all.p + 2, x.nranks, 3, 0};
+      halo_allgather(x, loc, x.sws().red_all.p, 3);
+      rr = Red{x.sws().red_all.p + 1, x.nranks, 3, 0};
+      rz = Red{x.sws().red_all.p + 2, x.nranks, 3, 0};
       return;
     }
     Red r2 = L.after(q2, 2, 0);

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Per-kernel FP64 work from scripts/pmc_flops.sh's SQ pass (mean per dispatch):
+  flops      = SQ_INSTS_VALU_FLOPS_FP64 + SQ_INSTS_VALU_FLOPS_FP64_TRANS (the counters' own lane-level FLOP count)
+  flops_inst = 64 (ADD + MUL + TRANS) + 128 FMA instructions (every lane active; a cross-check)
+  python scripts/pmc_flops_summary.py <counter_collection.csv> <out.json>"""
+import collections
+import csv
+import json
+import sys
+
+
+def main(path, out):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {}
+    for k, cs in agg.items():
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        n = max(len(v) for v in cs.values())
+        g = lambda c: m.get(c, 0.0)
+        res[k] = {"dispatches": n, **{c: m[c] for c in sorted(m)},
+                  "flops": g("SQ_INSTS_VALU_FLOPS_FP64") + g("SQ_INSTS_VALU_FLOPS_FP64_TRANS"),
+                  "flops_inst": 64.0 * (g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_MUL_F64") + g("SQ_INSTS_VALU_TRANS_F64"))
+                  + 128.0 * g("SQ_INSTS_VALU_FMA_F64")}
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["flops"])[:12]:
+        print(f"{v['flops'] / 1e9:10.2f} GFLOP/dispatch ({v['flops_inst'] / 1e9:8.2f} by instructions)  {k}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

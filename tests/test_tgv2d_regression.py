@@ -8,7 +8,9 @@ Tolerance 0.5 % of the value. The reference's numbers come from OpenFOAM-7 + Can
 with GAMG / PBiCGStab at relTol 0.01; our solves are tight. Measured (profiles/r03_tgv2d_*.json): CPU-A
 within 0.31 % at every point; the GPU path's upwind/linear schemes instead of the case's deviate 0.53 % at
 t = 2e-4 s; loosening our solvers to 1e-2 moves the values by <= 0.06 %, the chemistry tolerance
-(1e-6/1e-10 vs 1e-9/1e-15) by < 1e-5.
+(1e-6/1e-10 vs 1e-9/1e-15) by < 1e-5. Term-by-term attribution (profiles/r04_tgv2d_terms.json):
+the residual's shape over the five samples matches a 0.5 % difference in the species-enthalpy diffusion terms
+(diffAlphaD / hDiffCorrFlux) and no other term; no formula difference was found, so the 0.5 % stays.
 """
 import json
 import os
