@@ -1009,10 +1009,11 @@ __global__ void k_kinetic_slots(int B, const double* __restrict__ bU, double* __
 // corrected boundary gradients -> boundary sumYDiffError / hDiffCorrFlux.
 // the rest of k_y_prep for cell c once its face and slot sums are in: gradients / V, sumYDiffError,
 // hDiffCorrFlux, diffAlphaD, and the non-coupled slots' boundary fields (shared with the brick kernel)
+// (hc: the cell's own hai values, held by the caller)
 template <int S>
 __device__ __forceinline__ void y_prep_tail(const MeshView& m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
     const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
-    const double* __restrict__ hai, const double* __restrict__ bhai, double* __restrict__ sumE,
+    const double (&hc)[S], const double* __restrict__ bhai, double* __restrict__ sumE,
     double* __restrict__ bsumE, double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD,
     double* __restrict__ gout, int c, double (&g)[S][3], const double (&lap)[S], const double (&yc)[S]) {
   const long C = m.C, B = m.B;
@@ -1041,7 +1042,7 @@ __device__ __forceinline__ void y_prep_tail(const MeshView& m, const int8_t* __r
   for (int k = 0; k < 3; ++k) {
     double a = 0.0;
 #pragma unroll
-    for (int s = 0; s < S; ++s) a += hai[s * C + c] * (rd[s] * g[s][k] - yc[s] * se[k]);
+    for (int s = 0; s < S; ++s) a += hc[s] * (rd[s] * g[s][k] - yc[s] * se[k]);
     hd[k] = a;
   }
 #pragma unroll
@@ -1139,7 +1140,10 @@ __global__ void __launch_bounds__(TPB) k_y_prep(MeshView m, const int8_t* __rest
       lap[s] += v;
     }
   });
-  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hai, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
+  double hc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) hc[s] = hai[s * C + c];
+  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hc, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
 }
 
 // k_y_prep on a hex box in blockMesh order (MeshView::hx), one YBX x YBY x YBZ brick of cells per
@@ -1231,10 +1235,183 @@ __global__ void __launch_bounds__(TPB) k_y_prep_brick(MeshView m, const int8_t* 
       lap[s] += v;
     }
   });
-  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hai, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
+  double hc[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) hc[s] = hai[s * C + c];
+  y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hc, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, yc);
 }
 // species per staged chunk: all (S <= 5) or about half (LDS 2 SC YNB doubles: 9 species -> 5 = 52 KiB)
 constexpr int ybrick_sc(int S) { return S <= 5 ? S : (S + 1) / 2; }
+
+// k_y_prep on a hex box in blockMesh order, z-marching (2.5D blocking): one ZTX x ZTY column tile of cells
+// per workgroup walks a segment of kz planes, one thread per column. Per plane the tile's Y_s, hai_s and
+// alpha and the plane's face halo (one ring of 2 ZTX + 2 ZTY cells) are staged in LDS once, so every cell
+// value is read from HBM once (plus the ring, shared in L2 with the tiles beside it that the XCD runs at the
+// same time, and one extra plane per segment) -- the brick kernel re-read 288 halo cells per 256.
+// The z faces are evaluated ONCE: a cell's +z face (its last face) is computed from the next plane's
+// values, which the thread has already loaded into registers for the next plane's staging, and carried in
+// registers (Sf, the interpolated Y_s and the laplacian term) to serve as the next cell's -z face (its
+// first); the same values with the opposite sign, as the face loop of k_y_prep<S, -1> forms them. The x/y
+// faces read both cells from LDS and their geometry by coalesced loads of the owner's face slots (the
+// neighbour-side copy is the adjacent lane's line, an L1/L2 hit): evaluating those twice costs FP64 issue,
+// not HBM bytes. The cell's own values stay in registers through the tail (no hai re-read). Faces, their
+// order and every product are those of k_y_prep<S, -1>: results are bitwise the face walk's.
+constexpr int ZTX = 16, ZTY = 16, ZPX = ZTX + 2, ZNP = ZPX * (ZTY + 2);
+static_assert(ZTX * ZTY == TPB, "one thread per tile column");
+template <int S, int MINB>
+__global__ void __launch_bounds__(TPB, MINB) k_y_prep_zm(MeshView m, int kz, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
+    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
+    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
+    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
+    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
+  __shared__ double sY[S][ZNP], sH[S][ZNP], sA[ZNP];
+  const int nx = m.hx, ny = m.hy, nz = m.hz, nxy = nx * ny;
+  const int ntx = nx / ZTX, nty = ny / ZTY;
+  const int bid = xcd_block();
+  const int tx = bid % ntx, tt = bid / ntx, ty = tt % nty, seg = tt / nty;
+  const int k0 = seg * kz, k1 = min(nz, k0 + kz);
+  if (k0 >= nz) return;   // whole workgroup
+  const int t = threadIdx.x, li = t % ZTX, lj = t / ZTX;
+  const int i = tx * ZTX + li, j = ty * ZTY + lj;
+  const int me = (li + 1) + ZPX * (lj + 1);
+  const long C = m.C, F = m.F, B = m.B;
+  const int hxp = i < nx - 1, hyp = j < ny - 1;
+  const int cxy = i + nx * j;
+  // the ring cell staged by thread t < 2 (ZTX + ZTY): LDS index hl (-1: none / outside the box), column hg
+  int hl = -1, hg = 0;
+  if (t < 2 * (ZTX + ZTY)) {
+    int a, b;
+    if (t < ZTY) { a = -1; b = t; }
+    else if (t < 2 * ZTY) { a = ZTX; b = t - ZTY; }
+    else if (t < 2 * ZTY + ZTX) { a = t - 2 * ZTY; b = -1; }
+    else { a = t - 2 * ZTY - ZTX; b = ZTY; }
+    const int gi = tx * ZTX + a, gj = ty * ZTY + b;
+    if (gi >= 0 && gi < nx && gj >= 0 && gj < ny) { hl = (a + 1) + ZPX * (b + 1); hg = gi + nx * gj; }
+  }
+  double nY[S], nH[S], nA;   // the own column's next plane (staged at the next step; the +z neighbour now)
+  auto load_own = [&](int k, double (&y)[S], double (&h)[S], double& a) {
+    const long c = cxy + (long)nxy * k;
+    a = alpha[c];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { y[s] = Y[s * C + c]; h[s] = hai[s * C + c]; }
+  };
+  // the carried z face: Sf, interpolated Y_s and laplacian term of the +z face of the cell below
+  double zs0 = 0.0, zs1 = 0.0, zs2 = 0.0, zy[S], zv[S];
+  auto zface = [&](long f, auto yo, auto ho, double ao, const double (&yn)[S], const double (&hn)[S], double an) {
+    const double w = m.w[f], ms = m.magSf[f], dcf = m.dc[f];
+    zs0 = m.Sf[f]; zs1 = m.Sf[F + f]; zs2 = m.Sf[2 * F + f];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const double ys = yo(s);
+      zy[s] = interp_f(w, ys, yn[s]);
+      const double gam = interp_f(w, ao * ho(s), an * hn[s]);
+      zv[s] = gam * ms * (dcf * (yn[s] - ys));
+    }
+  };
+  load_own(k0, nY, nH, nA);
+  if (k0 > 0) {   // the segment's first -z face, from the plane below
+    double pY[S], pH[S], pA;
+    load_own(k0 - 1, pY, pH, pA);
+    zface((long)(hxp + hyp) * C + cxy + (long)nxy * (k0 - 1), [&](int s) { return pY[s]; }, [&](int s) { return pH[s]; },
+          pA, nY, nH, nA);
+  }
+  for (int k = k0; k < k1; ++k) {
+    const int c = cxy + nxy * k;
+    __syncthreads();   // every thread done with the previous plane's neighbour values
+#pragma unroll
+    for (int s = 0; s < S; ++s) { sY[s][me] = nY[s]; sH[s][me] = nH[s]; }
+    sA[me] = nA;
+    if (hl >= 0) {
+      const long hc = hg + (long)nxy * k;
+      sA[hl] = alpha[hc];
+#pragma unroll
+      for (int s = 0; s < S; ++s) { sY[s][hl] = Y[s * C + hc]; sH[s][hl] = hai[s * C + hc]; }
+    }
+    const double ac = nA;
+    if (k + 1 < nz) {   // the next plane's Y and alpha in flight across the barrier and the x/y faces (its hai
+      const long cn = c + nxy;   // is loaded at the +z face: registers)
+      nA = alpha[cn];
+#pragma unroll
+      for (int s = 0; s < S; ++s) nY[s] = Y[s * C + cn];
+    }
+    __syncthreads();
+    // the cell's own values are read back from its LDS slot where needed (registers: the accumulators, the
+    // next plane and the carried face fill the 256 of two waves per SIMD)
+    auto yc = [&](int s) { return sY[s][me]; };
+    auto hc = [&](int s) { return sH[s][me]; };
+    double g[S][3], lap[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0; }
+    if (k > 0) {   // -z: the carried face (owner below)
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        g[s][0] -= zs0 * zy[s]; g[s][1] -= zs1 * zy[s]; g[s][2] -= zs2 * zy[s];
+        lap[s] -= zv[s];
+      }
+    }
+    auto face = [&](long f, int lo, bool own) {
+      const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
+      const double ms = m.magSf[f], dcf = m.dc[f];
+      const double an = sA[lo];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const double yn = sY[s][lo];
+        const double ahn = an * sH[s][lo];
+        const double ycs = yc(s), ahc = ac * hc(s);
+        const double yf = own ? interp_f(w, ycs, yn) : interp_f(w, yn, ycs);
+        const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
+        const double gam = own ? interp_f(w, ahc, ahn) : interp_f(w, ahn, ahc);
+        const double dy = own ? yn - ycs : ycs - yn;
+        const double v = gam * ms * (dcf * dy);
+        if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
+        else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
+      }
+    };
+    if (j > 0) face((long)hxp * C + c - nx, me - ZPX, false);
+    if (i > 0) face(c - 1, me - 1, false);
+    if (hxp) face(c, me + 1, true);
+    if (hyp) face((long)hxp * C + c, me + ZPX, true);
+    if (k < nz - 1) {   // +z: evaluated once, carried to the cell above
+#pragma unroll
+      for (int s = 0; s < S; ++s) nH[s] = hai[s * C + c + nxy];
+      zface((long)(hxp + hyp) * C + c, yc, hc, ac, nY, nH, nA);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        g[s][0] += zs0 * zy[s]; g[s][1] += zs1 * zy[s]; g[s][2] += zs2 * zy[s];
+        lap[s] += zv[s];
+      }
+    }
+    each_slot(m, tyY, c, [&](int b, int tb) {
+      const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const double yf = bface(m, tb, Y + s * C, bY + s * B, b, c);
+        g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
+        const double ahc = ac * hc(s), ycs = yc(s);
+        double v;
+        if (bc_coupled(tb)) {
+          const int pc = m.partner[b];
+          const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
+          v = interp_b(m.bw[b], ahc, an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - ycs));
+        } else {
+          const double sng = (tb == FIXED_VALUE || tb == CALCULATED || tb == FIXED_ENERGY || bc_mixed(tb)) ? m.bdc[b] * (bY[s * B + b] - ycs) : 0.0;
+          v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
+        }
+        lap[s] += v;
+      }
+    });
+    double ycv[S], hcv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { ycv[s] = yc(s); hcv[s] = hc(s); }
+    y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hcv, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, ycv);
+  }
+}
+// planes per workgroup segment: about two workgroups per CU over the whole box, at least 4 planes
+inline int yzm_kz(int nx, int ny, int nz) {
+  const int tiles = (nx / ZTX) * (ny / ZTY);
+  const int nseg = std::max(1, std::min(512 / std::max(1, tiles), nz / 4));
+  return (nz + nseg - 1) / nseg;
+}
 
 // k_y_prep, species-outer over the solver's gather rows (hex meshes, W = 6): the cell's six faces'
 // indices, geometry and neighbour alpha are loaded once up front, then each species loads its twelve
@@ -2302,9 +2479,28 @@ void y_prep(Ctx& x) {
   const int bmode = eb ? std::atoi(eb) : 1;
   const int brick = (face_hex(x) && !x.trav.n && x.hex[0] % YBX == 0 && x.hex[1] % YBY == 0 && x.hex[2] % YBZ == 0 &&
                      bmode > 0) ? (bmode == 2 ? 2 : 1) : 0;
+  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YPREP_ZM=0: off)
+  const char* ez = std::getenv("DFMI_YPREP_ZM");
+  const int zmode = ez ? std::atoi(ez) : 1;   // 1: two workgroups per CU (launch bound), 2: the compiler's choice
+  const bool zm = face_hex(x) && !x.trav.n && x.hex[0] % ZTX == 0 && x.hex[1] % ZTY == 0 && zmode > 0;
+  const int zkz = zm ? yzm_kz(x.hex[0], x.hex[1], x.hex[2]) : 0;
+  const int zgrid = zm ? (x.hex[0] / ZTX) * (x.hex[1] / ZTY) * ((x.hex[2] + zkz - 1) / zkz) : 0;
 #define CALL(NS)                                                                                                     \
   do {                                                                                                               \
-    if (prep_rows)                                                                                                   \
+    if (zm && !prep_rows) {                                                                                          \
+      KScope _ks(x, "k_y_prep");                                                                                     \
+      if (zmode == 2)                                                                                                \
+        hipLaunchKernelGGL((k_y_prep_zm<NS, 1>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.f("Y"),  \
+               x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"),  \
+               x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),     \
+               x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                             \
+      else                                                                                                           \
+        hipLaunchKernelGGL((k_y_prep_zm<NS, 2>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.f("Y"),  \
+               x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"),  \
+               x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),     \
+               x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                             \
+      DFMI_HIP(hipGetLastError());                                                                                   \
+    } else if (prep_rows)                                                                                            \
       LAUNCH_AS("k_y_prep", (k_y_prep_rows<NS>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
              x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
              x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
