@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256, 2)
 // which puts each ds_read_b128 lane group ({0-3,12-15,20-27}, ... : rows 0-15 of a 16-row block at two
 // adjacent logical chunks) on 16 distinct 16-B bank slots; DMA pieces are 8 rows x 128 B (1 KiB contiguous,
 // the swizzle applied on the source address).
-template <bool GELU>
+template <bool GELU, bool IL>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_w(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                  long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
@@ -315,6 +315,23 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     };
+    // pieces of the above for the interleaved schedule: MFMAs q0, q0 + 1 (q -> column block q / 8, row block
+    // q % 8), one fragment read (B blocks first), one DMA piece (A rows, then W rows)
+    auto mfma_pair = [&](const half8 (&af)[8], const half8 (&bf)[4], int q0) {
+#pragma unroll
+      for (int q = q0; q < q0 + 2; ++q)
+        if (q / 8 < JL) acc[q % 8][q / 8] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[q % 8], bf[q / 8], acc[q % 8][q / 8], 0, 0, 0);
+    };
+    auto frag_one = [&](int buf, int kh, int q, half8 (&af)[8], half8 (&bf)[4]) {
+      const _Float16* la = lds + buf * STAGE + fo[kh];
+      if (q < 4) bf[q] = *reinterpret_cast<const half8*>(la + TILE_A + (wn + 16 * q) * BKW);
+      else af[q - 4] = *reinterpret_cast<const half8*>(la + (wm + 16 * (q - 4)) * BKW);
+    };
+    auto stage_piece = [&](int buf, int k0, int p) {
+      _Float16* la = lds + buf * STAGE;
+      if (p < 4) glds16(pa[p] + k0, la + (wave * 32 + p * 8) * BKW);
+      else glds16(pw[p - 4] + k0, la + TILE_A + (wave * 32 + (p - 4) * 8) * BKW);
+    };
     // no scalar (kernel-argument) load left outstanding into the loop: with one pending, the compiler can only
     // wait lgkmcnt(0), which would also wait for the K-half-1 reads issued before the K-half-0 MFMAs
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -330,159 +347,45 @@ __global__ void __launch_bounds__(512, 1)
       // K-half 0's reads (issued a K half of MFMAs ago) are done: waiting for them BEFORE issuing the next
       // 12 (the LGKM counter holds 15) lets the K-half-0 MFMAs start with the K-half-1 reads in flight
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      frag_reads(cur, 1, a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(a0, b0);
+      if constexpr (!IL) frag_reads(cur, 1, a1, b1);
+      if constexpr (IL) {   // one read between every two MFMAs (the reads' issue hidden among them)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          if (q < 12) frag_one(cur, 1, q, a1, b1);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_pair(a0, b0, 2 * q);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(a0, b0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       // my reads of tile kt retired, my DMAs of tile kt+1 landed; after the barrier: everyone's
       __builtin_amdgcn_s_waitcnt(0);        // vmcnt(0) lgkmcnt(0)
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + 2 < nk) stage(cur, (kt + 2) * BKW);
-      frag_reads(cur ^ 1, 0, a0, b0);   // unconditional (the last tile's reads hit a stale stage, unused)
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(a1, b1);
-    }
-  };
-  switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
-    case 4: kloop(std::integral_constant<int, 4>{}); break;
-    case 3: kloop(std::integral_constant<int, 3>{}); break;
-    case 2: kloop(std::integral_constant<int, 2>{}); break;
-    case 1: kloop(std::integral_constant<int, 1>{}); break;
-    default: kloop(std::integral_constant<int, 0>{}); break;
-  }
-  // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
-  __syncthreads();
-  _Float16* cs = lds;
+      if constexpr (IL) {
+        // the two tiles past the end re-stage the last tile (in bounds, never read; drained before the epilogue)
+        // so the region has no branch and the 8 DMAs and 12 reads interleave with the 32 MFMAs
+        const int kn = min(kt + 2, nk - 1) * BKW;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
-    const bool live = col < N;
-    const float bv = live ? bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rl = wm + 16 * i + 4 * g + e;
-        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
-        if (GELU) v = gelu_fast2(v);
-        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
-        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
+        for (int q = 0; q < 16; ++q) {
+          if (q < 8) stage_piece(cur, kn, q);
+          if (q < 12) frag_one(cur ^ 1, 0, q, a0, b0);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_pair(a1, b1, 2 * q);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        if (kt + 2 < nk) stage(cur, (kt + 2) * BKW);
+        frag_reads(cur ^ 1, 0, a0, b0);   // unconditional (the last tile's reads hit a stale stage, unused)
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(a1, b1);
       }
-  }
-  __syncthreads();
-#pragma unroll 4
-  for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
-    const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
-    const int row = m0 + rl, col = n0 + ch * 8;
-    if (row < M && col < ldc)
-      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
-  }
-}
-
-// vmcnt(n) with lgkmcnt(0) as one s_waitcnt immediate (gfx9 layout: vmcnt [3:0] + [15:14], expcnt [6:4],
-// lgkmcnt [11:8]); a builtin, not inline asm, so the compiler's own wait insertion sees it
-#define DFMI_WAIT_VM_LGKM0(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x70)
-
-// Ring variant of the wide-layer GEMM: the same 256 x 256 block tile and 8 waves, the K dimension staged in
-// 32-deep stages (A 256 x 32 + W 256 x 32 = 32 KiB) through an NST-stage LDS ring, NST - 1 stages in flight
-// while one feeds the MFMAs (NST = 4: 96 KiB of DMA in flight per CU against 64 KiB for the two 64-deep
-// stages above -- the wide kernel's DMA latency, not the MFMA, set its pace). One barrier per stage, in the
-// middle of the stage's 32 MFMAs: per stage s each wave runs the 16 MFMAs of columns 0-1 on fragments read
-// before, waits for its DMAs of stage s+1 and its reads of s, barrier, DMAs stage s+NST into s's slot, reads
-// stage s+1's fragments, runs the 16 MFMAs of columns 2-3 of stage s. 64-B LDS rows (swz16).
-template <bool GELU, int NST>
-__global__ void __launch_bounds__(512, 1)
-    k_mlp_gemm_r(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
-                 long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
-  constexpr int BMW = 256, BNW = 256, NT = 512;
-  constexpr int TILE_A = BMW * BK, STAGE = TILE_A + BNW * BK;   // halves: 16 + 16 KiB per stage
-  constexpr int CLD = BNW + 8;
-  constexpr int LDS_H = NST * STAGE > BMW * CLD ? NST * STAGE : BMW * CLD;
-  static_assert(LDS_H * 2 <= 160 * 1024, "LDS");
-  using f32x4 = __attribute__((ext_vector_type(4))) float;
-  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
-  const int z = blockIdx.z;
-  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
-  const int ntn = (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
-  const int orig = blockIdx.x;
-  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int m0 = (wg / ntn) * BMW, n0 = (wg % ntn) * BNW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // staging: wave w fills A rows and W rows [32 w, 32 w + 32), 16 rows (64 B each) per DMA
-  const _Float16* pa[2];
-  const _Float16* pw[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = wave * 32 + i * 16 + (lane >> 2), ch = swz16(row, lane & 3);
-    pa[i] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
-    pw[i] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    _Float16* la = lds + buf * STAGE;
-    _Float16* lw = la + TILE_A;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(pa[i] + k0, la + (wave * 32 + i * 16) * BK);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(pw[i] + k0, lw + (wave * 32 + i * 16) * BK);
-  };
-  constexpr int DMA_PER_STAGE = 4;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
-  const int r = lane & 15, g = lane >> 4;
-  const int fo = r * BK + swz16(r, g) * 8;   // swz16 depends on (row >> 2) & 3 only: the same for rows 16 i + r
-  auto frag_reads = [&](int buf, half8 (&af)[8], half8 (&bf)[4]) {
-    const _Float16* la = lds + buf * STAGE + fo;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(la + TILE_A + (wn + 16 * j) * BK);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const half8*>(la + (wm + 16 * i) * BK);
-  };
-  const int ns = K / BK;
-  auto kloop = [&](auto jl_c) {
-    constexpr int JL = decltype(jl_c)::value;
-    auto mfmas = [&](const half8 (&af)[8], const half8 (&bf)[4], auto j0_c) {
-      constexpr int J0 = decltype(j0_c)::value;
-#pragma unroll
-      for (int j = J0; j < J0 + 2 && j < JL; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    };
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // no scalar load outstanding into the loop (lgkmcnt(0))
-#pragma unroll
-    for (int s = 0; s < NST; ++s)
-      if (s < ns) stage(s, s * BK);
-    if (ns >= NST) DFMI_WAIT_VM_LGKM0(DMA_PER_STAGE * (NST - 1));
-    else __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    half8 a0[8], b0[4], a1[8], b1[4];
-    frag_reads(0, a0, b0);
-    int buf = 0;
-    // one stage: MFMAs of (af, bf) around the barrier, the next stage's fragments read into (an, bn)
-    auto step = [&](int s, const half8 (&af)[8], const half8 (&bf)[4], half8 (&an)[8], half8 (&bn)[4]) {
-      mfmas(af, bf, std::integral_constant<int, 0>{});
       __builtin_amdgcn_sched_barrier(0);
-      // my DMAs of stage s+1 landed (stages s+2 .. s+NST-1 stay in flight), my reads of stage s retired
-      if (s + NST <= ns) DFMI_WAIT_VM_LGKM0(DMA_PER_STAGE * (NST - 2));
-      else __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + NST < ns) stage(buf, (s + NST) * BK);
-      buf = buf + 1 == NST ? 0 : buf + 1;
-      frag_reads(buf, an, bn);   // unconditional (past the last stage it reads a stale slot, unused)
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(af, bf, std::integral_constant<int, 2>{});
-    };
-    for (int s = 0; s < ns; s += 2) {   // ns even (K % 64 == 0): the fragment registers ping-pong, no copies
-      step(s, a0, b0, a1, b1);
-      step(s + 1, a1, b1, a0, b0);
     }
+    __builtin_amdgcn_s_waitcnt(0);   // no DMA in flight into the LDS the epilogue reuses
   };
   switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
     case 4: kloop(std::integral_constant<int, 4>{}); break;
@@ -711,7 +614,7 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   d.last_reacting = nr;
   if (nr == 0) return;
   const int chunk = std::min(nr, d.chunk);
-  static const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 1; }();   // A/B: 256x256x64 kernel for the wide layers
+  static const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 1; }();   // 0: k_mlp_gemm, 2: no interleave   // A/B: 256x256x64 kernel for the wide layers
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
@@ -743,14 +646,11 @@ void dnn_solve(Ctx& x, const char* rho_field) {
                            d.part.p, sP);
       } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
-        if (wide == 3)
-          hipLaunchKernelGGL((k_mlp_gemm_w<true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
-        else if (wide == 2)
-          hipLaunchKernelGGL((k_mlp_gemm_r<true, 5>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+        if (wide == 2)
+          hipLaunchKernelGGL((k_mlp_gemm_w<true, false>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
         else
-          hipLaunchKernelGGL((k_mlp_gemm_r<true, 4>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+          hipLaunchKernelGGL((k_mlp_gemm_w<true, true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
       } else {
         hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,

@@ -1408,6 +1408,7 @@ __global__ void __launch_bounds__(TPB, MINB) k_y_prep_zm(MeshView m, int kz, con
 }
 // planes per workgroup segment: about two workgroups per CU over the whole box, at least 4 planes
 inline int yzm_kz(int nx, int ny, int nz) {
+  if (const char* e = std::getenv("DFMI_ZM_KZ")) return std::max(1, std::atoi(e));   // A/B: planes per segment
   const int tiles = (nx / ZTX) * (ny / ZTY);
   const int nseg = std::max(1, std::min(512 / std::max(1, tiles), nz / 4));
   return (nz + nseg - 1) / nseg;
@@ -1709,6 +1710,153 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
     for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
     dS[ss * Ce + pc] = dg[s];
     rhs[ss * Ce + pc] = sr[s];
+  }
+}
+
+// k_y_assemble_ell on a hex box in blockMesh order, z-marching like k_y_prep_zm: one 16 x 16 column tile
+// per workgroup walks a segment of planes. Per plane the tile's rhoD_s and the plane's face ring are staged
+// in LDS once (the x/y neighbours' rhoD from LDS instead of global gathers); the +z neighbour's rhoD is
+// the thread's own prefetch of the next plane, and the +z face's data (phi, phiUc, the upwind weight, w,
+// deltaCoeffs, |Sf|) and the cell's rhoD stay in registers to serve the next cell's -z face: every cell
+// value and every face value is read from HBM once. Faces, order and products are those of
+// k_y_assemble_ell<S, -1>: bitwise the same rows.
+template <int S>
+__global__ void __launch_bounds__(TPB) k_y_assemble_ell_zm(MeshView m, int kz, const int8_t* __restrict__ tyY, int inert,
+    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
+    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
+    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
+    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
+    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY, const double* __restrict__ wY,
+    const double* __restrict__ bwY) {
+  __shared__ double sR[S][ZNP];
+  const int nx = m.hx, ny = m.hy, nz = m.hz, nxy = nx * ny;
+  const int ntx = nx / ZTX, nty = ny / ZTY;
+  const int bid = xcd_block();
+  const int tx = bid % ntx, tt = bid / ntx, ty = tt % nty, seg = tt / nty;
+  const int k0 = seg * kz, k1 = min(nz, k0 + kz);
+  if (k0 >= nz) return;   // whole workgroup
+  const int t = threadIdx.x, li = t % ZTX, lj = t / ZTX;
+  const int i = tx * ZTX + li, j = ty * ZTY + lj;
+  const int me = (li + 1) + ZPX * (lj + 1);
+  const long C = m.C, B = m.B;
+  const int hxp = i < nx - 1, hyp = j < ny - 1;
+  const int cxy = i + nx * j;
+  int hl = -1, hg = 0;   // the ring cell staged by thread t < 2 (ZTX + ZTY)
+  if (t < 2 * (ZTX + ZTY)) {
+    int a, b;
+    if (t < ZTY) { a = -1; b = t; }
+    else if (t < 2 * ZTY) { a = ZTX; b = t - ZTY; }
+    else if (t < 2 * ZTY + ZTX) { a = t - 2 * ZTY; b = -1; }
+    else { a = t - 2 * ZTY - ZTX; b = ZTY; }
+    const int gi = tx * ZTX + a, gj = ty * ZTY + b;
+    if (gi >= 0 && gi < nx && gj >= 0 && gj < ny) { hl = (a + 1) + ZPX * (b + 1); hg = gi + nx * gj; }
+  }
+  // face data of one face: phi, phiUc, upwind weight, w, deltaCoeffs, |Sf|
+  struct FD { double ph, pu, wu, w, dcf, ms; };
+  auto load_face = [&](long f) {
+    FD d;
+    d.ph = phi[f]; d.pu = phiUc[f];
+    d.wu = wY ? wY[f] : (d.ph >= 0 ? 1.0 : 0.0);
+    d.w = m.w[f]; d.dcf = m.dc[f]; d.ms = m.magSf[f];
+    return d;
+  };
+  double nR[S], pR[S];   // rhoD of the own column: next plane (prefetched), plane below (the -z neighbour)
+  FD zf{};               // the -z face (the +z face of the cell below)
+  {
+    const long c0 = cxy + (long)nxy * k0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) nR[s] = rhoD[s * C + c0];
+    if (k0 > 0) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) pR[s] = rhoD[s * C + c0 - nxy];
+      zf = load_face((long)(hxp + hyp) * C + c0 - nxy);
+    }
+  }
+  for (int kp = k0; kp < k1; ++kp) {
+    const int c = cxy + nxy * kp;
+    const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
+    __syncthreads();   // every thread done with the previous plane's neighbour values
+    double rc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { rc[s] = nR[s]; sR[s][me] = rc[s]; }
+    if (hl >= 0) {
+      const long hc = hg + (long)nxy * kp;
+#pragma unroll
+      for (int s = 0; s < S; ++s) sR[s][hl] = rhoD[s * C + hc];
+    }
+    if (kp + 1 < nz) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) nR[s] = rhoD[s * C + c + nxy];
+    }
+    __syncthreads();
+    double d1 = 0.0, d2 = 0.0;
+    double dL[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) dL[s] = 0.0;
+    int k = 0;
+    auto face = [&](const FD& fd, auto rn, bool own) {
+      const double L1 = -fd.wu * fd.ph, U1 = L1 + fd.ph;
+      const double L2 = -fd.wu * fd.pu, U2 = L2 + fd.pu;
+      if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+      const double Ls = L1 + L2, Us = U1 + U2;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const double r = rn(s);
+        const double UL = fd.dcf * ((own ? interp_f(fd.w, rc[s], r) : interp_f(fd.w, r, rc[s])) * fd.ms);
+        dL[s] -= UL;
+        val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
+      }
+      ++k;
+    };
+    if (kp > 0) face(zf, [&](int s) { return pR[s]; }, false);
+    if (j > 0) face(load_face((long)hxp * C + c - nx), [&](int s) { return sR[s][me - ZPX]; }, false);
+    if (i > 0) face(load_face(c - 1), [&](int s) { return sR[s][me - 1]; }, false);
+    if (hxp) face(load_face(c), [&](int s) { return sR[s][me + 1]; }, true);
+    if (hyp) face(load_face((long)hxp * C + c), [&](int s) { return sR[s][me + ZPX]; }, true);
+    if (kp < nz - 1) {
+      zf = load_face((long)(hxp + hyp) * C + c);
+      face(zf, [&](int s) { return nR[s]; }, true);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) pR[s] = rc[s];
+    const double vol = m.V[c];
+    const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+    const double ro = m.rdt * rho_old[c];
+    double dg[S], sr[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      dg[s] = dd - dL[s];
+      sr[s] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
+    }
+    each_slot(m, tyY, c, [&](int b, int tb) {
+      const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
+      const bool cp = bc_coupled(tb);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const BCoef qc = bcoef_f(tb, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+        const BCoef ql = bcoef_f(tb, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
+        const double gam = cp ? interp_b(m.bw[b], rc[s], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+        const double pG = gam * m.bmagSf[b];
+        const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+        const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+        dg[s] += icv;
+        if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
+        else sr[s] += bcv;
+      }
+      if (cp) ++k;
+    });
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s == inert) continue;
+      const int ss = s < inert ? s : s - 1;
+      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
+      dS[ss * Ce + pc] = dg[s];
+      rhs[ss * Ce + pc] = sr[s];
+    }
   }
 }
 
@@ -2479,9 +2627,10 @@ void y_prep(Ctx& x) {
   const int bmode = eb ? std::atoi(eb) : 1;
   const int brick = (face_hex(x) && !x.trav.n && x.hex[0] % YBX == 0 && x.hex[1] % YBY == 0 && x.hex[2] % YBZ == 0 &&
                      bmode > 0) ? (bmode == 2 ? 2 : 1) : 0;
-  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YPREP_ZM=0: off)
+  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YPREP_ZM=1|2)
   const char* ez = std::getenv("DFMI_YPREP_ZM");
-  const int zmode = ez ? std::atoi(ez) : 1;   // 1: two workgroups per CU (launch bound), 2: the compiler's choice
+  const int zmode = ez ? std::atoi(ez) : 0;   // 1: two workgroups per CU (launch bound), 2: the compiler's choice
+  // (off by default: measured slower than the brick kernel)
   const bool zm = face_hex(x) && !x.trav.n && x.hex[0] % ZTX == 0 && x.hex[1] % ZTY == 0 && zmode > 0;
   const int zkz = zm ? yzm_kz(x.hex[0], x.hex[1], x.hex[2]) : 0;
   const int zgrid = zm ? (x.hex[0] / ZTX) * (x.hex[1] / ZTY) * ((x.hex[2] + zkz - 1) / zkz) : 0;
@@ -2561,9 +2710,26 @@ void y_assemble(Ctx& x) {
 
 void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs) {
   MeshView m = x.view();
-#define CALL(NS) LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), \
-                        x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                    \
-                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
+  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YASM_ZM=1)
+  const char* ez = std::getenv("DFMI_YASM_ZM");
+  // (off by default: measured slower than the cell-parallel kernel)
+  const bool zm = face_hex(x) && !x.trav.n && x.hex[0] % ZTX == 0 && x.hex[1] % ZTY == 0 && ez && std::atoi(ez) != 0;
+  const int zkz = zm ? yzm_kz(x.hex[0], x.hex[1], x.hex[2]) : 0;
+  const int zgrid = zm ? (x.hex[0] / ZTX) * (x.hex[1] / ZTY) * ((x.hex[2] + zkz - 1) / zkz) : 0;
+#define CALL(NS)                                                                                                     \
+  do {                                                                                                               \
+    if (zm) {                                                                                                        \
+      KScope _ks(x, "k_y_assemble_ell");                                                                             \
+      hipLaunchKernelGGL((k_y_assemble_ell_zm<NS>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.inert, \
+                         x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"),      \
+                         x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, \
+                         val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1));                                      \
+      DFMI_HIP(hipGetLastError());                                                                                   \
+    } else                                                                                                           \
+      LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),          \
+                x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                             \
+                x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1)); \
+  } while (0)
 #define GEN(CH) LAUNCH_SWG(k_y_assemble_ell_gen, CH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), \
                        x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),     \
                        x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))

@@ -106,8 +106,13 @@ def _oracle(m, t, st, pt, inert, dt):
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
                                         "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
-                                        "mixed", "mixed-generic", "walls-trav"])
+                                        "mixed", "mixed-generic", "walls-trav", "burke9-zm", "walls-zm"])
 def periodic(request):
+    zm = request.param.endswith("-zm")      # the z-marching YEqn kernels (A/B path, 16 x 16 column tiles)
+    if zm:
+        for k in ("DFMI_YPREP_ZM", "DFMI_YASM_ZM", "DFMI_ZM_KZ"):
+            os.environ[k] = "3" if k == "DFMI_ZM_KZ" else "1"
+            request.addfinalizer(lambda k=k: os.environ.pop(k, None))
     generic = request.param.endswith("-generic")
     if generic:
         os.environ["DFMI_SPECIES_GENERIC"] = "1"
@@ -116,7 +121,7 @@ def periodic(request):
         os.environ["DFMI_FACE_CSR"] = "1"
         request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
     traversal = request.param.endswith("-trav")
-    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "")
+    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "").replace("-zm", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
@@ -147,8 +152,10 @@ def periodic(request):
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
         return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber,
-                     mixed=mixed, traversal=traversal, nx=16 if traversal else 6, ny=12 if traversal else 5,
-                     nz=8 if traversal else 4)
+                     mixed=mixed, traversal=traversal, nx=16 if (traversal or zm) else 6,
+                     ny=16 if zm else 12 if traversal else 5, nz=8 if (traversal or zm) else 4)
+    if zm:   # 16 x 16 x 8 in segments of 3 planes: a short last segment, -z faces across segment starts
+        return _case(mech=param, nx=16, ny=16, nz=8)
     return _case(mech=param, renumber=renumber, nx=16 if renumber else 6, ny=8 if renumber else 5,
                  nz=4 if renumber else 4)
 
