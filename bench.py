@@ -676,7 +676,7 @@ def main():
     fl_path = os.path.join(ROOT, "profiles", PMC_FLOPS_FILE)
     if os.path.exists(fl_path) and n == 128 and world == 1:
         for key, v in json.load(open(fl_path)).items():
-            short = key.split("::")[-1]
+            short = key[len("dfmi::"):] if key.startswith("dfmi::") else key   # (template arguments hold "::" too)
             for fam in ("k_thermo_cells", "k_chem"):
                 if short.startswith(fam + "<") or short.startswith(fam + "_gen<"):
                     if v["flops"] > flops_tab.get(fam, {}).get("flops", -1.0):
@@ -722,7 +722,7 @@ def main():
             roofs[k].update({"bound": "fp64-valu", "unit": "TFLOP/s", "peak": FP64_PEAK_TFS, "achieved": tfs,
                              "frac": tfs / FP64_PEAK_TFS if tfs is not None else None,
                              "flops_per_launch": fl["flops"] if fl else None,
-                             "flops_source": f"profiles/{PMC_FLOPS_FILE} (SQ_INSTS_VALU_FLOPS_FP64 + _TRANS, mean per dispatch)"
+                             "flops_source": f"profiles/{PMC_FLOPS_FILE} (64 x SQ_INSTS_VALU_FLOPS_FP64 per dispatch, mean; = 64 (ADD + MUL + TRANS + 2 FMA) wave-instructions)"
                              if fl else "no PMC FLOP counts for this workload",
                              "hbm_achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS})
     hbm = {k: v for k, v in roofs.items() if v["bound"] == "hbm"}

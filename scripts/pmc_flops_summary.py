@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel FP64 work from scripts/pmc_flops.sh's SQ pass (mean per dispatch):
-  flops      = SQ_INSTS_VALU_FLOPS_FP64 + SQ_INSTS_VALU_FLOPS_FP64_TRANS (the counters' own lane-level FLOP count)
-  flops_inst = 64 (ADD + MUL + TRANS) + 128 FMA instructions (every lane active; a cross-check)
+  flops      = 64 x SQ_INSTS_VALU_FLOPS_FP64: the counter counts wave-instructions weighted by their FLOPs per lane
+               (measured on gfx950: it equals ADD + MUL + TRANS + 2 FMA of the per-instruction counters exactly), so
+               x 64 lanes = FLOPs with every lane active (an upper bound where lanes are masked)
+  flops_inst = 64 (ADD + MUL + TRANS) + 128 FMA instructions (the same sum from the instruction counters)
   python scripts/pmc_flops_summary.py <counter_collection.csv> <out.json>"""
 import collections
 import csv
@@ -20,7 +22,7 @@ def main(path, out):
         n = max(len(v) for v in cs.values())
         g = lambda c: m.get(c, 0.0)
         res[k] = {"dispatches": n, **{c: m[c] for c in sorted(m)},
-                  "flops": g("SQ_INSTS_VALU_FLOPS_FP64") + g("SQ_INSTS_VALU_FLOPS_FP64_TRANS"),
+                  "flops": 64.0 * g("SQ_INSTS_VALU_FLOPS_FP64"),
                   "flops_inst": 64.0 * (g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_MUL_F64") + g("SQ_INSTS_VALU_TRANS_F64"))
                   + 128.0 * g("SQ_INSTS_VALU_FMA_F64")}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)

@@ -24,6 +24,9 @@ out = [n, round(d["ms_per_step"], 3), "ms"]
 for k in os.environ["KERNELS"].split(","):
     r = (d.get("rooflines") or {}).get(k) or {}
     out += [k, round(r.get("avg_us") or 0, 1), "us", "frac", round(r.get("frac") or 0, 3)]
+ch = d.get("chemistry") or {}
+if "k_chem_ms_per_step" in ch:
+    out += ["chem", round(ch["k_chem_ms_per_step"], 3), "ms/step"]
 print(*out)
 EOF
 done
