@@ -27,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
-PMC_FILE = "r03_pmc_traffic.json"
+PMC_FILE = "r04_pmc_traffic.json"
 PMC_FLOPS_FILE = "r04_pmc_flops.json"   # scripts/pmc_flops.sh: FP64 FLOPs per dispatch (SQ_INSTS_VALU_FLOPS_FP64)
 FP64_PEAK_TFS = 78.6                    # MI355X FP64 vector peak
 
@@ -756,7 +756,9 @@ def main():
                          "WRITE_SIZE passes, mean per dispatch, gfx950 read correction)",
                          note=f"achieved = algorithmic bytes of the work done (active systems/iterations; SURVEY 8(d): "
                               f"int32 ids per face counted) / summed HIP-event kernel time over {args.roof_steps} extra "
-                              "steps after the timed region (the headline runs with no events armed); algorithmic_bytes "
+                              "steps after the timed region (the headline runs with no events armed; while they are "
+                              "armed the step's side stream is folded into the main one, so each kernel is timed "
+                              "alone); algorithmic_bytes "
                               "and traffic are per launch; impl_bytes / frac_impl: the bytes this implementation must "
                               "move (gather rows decoded from row classes: 1 B per cell instead of the ids)"),
         "rooflines": {k: {kk: v[kk] for kk in ("bound", "unit", "peak", "achieved", "frac", "traffic", "algorithmic_bytes",

@@ -226,9 +226,11 @@ void do_Y(Ctx& x) {
 // the side stream while the UEqn assembles and solves on the main one: the VALU-bound chemistry beside the
 // memory-bound UEqn. Both are issued before the UEqn's convergence polls block the host. Several ranks keep
 // one stream (every RCCL operation of a rank stays ordered on one communicator). DFMI_STEP_OVERLAP=0: off.
+// While per-kernel timers are armed (dfmi_kernel_timer: the bench's roofline pass) the step runs on one
+// stream, so every timed kernel has the GPU to itself and its HIP-event time is its own.
 bool step_overlap(const Ctx& x) {
   static const bool on = [] { const char* e = std::getenv("DFMI_STEP_OVERLAP"); return !(e && std::atoi(e) == 0); }();
-  return on && x.nranks == 1 && !halo_active(x);
+  return on && x.nranks == 1 && !halo_active(x) && x.ktimer.targets.empty();
 }
 void do_U_Y(Ctx& x) {
   if (!step_overlap(x)) { do_U(x); do_Y(x); return; }
