@@ -614,7 +614,9 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   d.last_reacting = nr;
   if (nr == 0) return;
   const int chunk = std::min(nr, d.chunk);
-  static const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 1; }();   // 0: k_mlp_gemm, 2: no interleave   // A/B: 256x256x64 kernel for the wide layers
+  // DFMI_DNN_WIDE=1|2: the 256x256x64 kernel for the wide layers (1: DMA/reads interleaved, 2: not); measured
+  // 9.77 / 10.07 ms against k_mlp_gemm's 9.57 ms per 65,536-row chunk of the 1600->800 layer, so off
+  const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 0; }();   // A/B: 256x256x64 kernel for the wide layers
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);

@@ -16,12 +16,13 @@ def main(d):
         name = r["Kernel_Name"]
         if "k_mlp_gemm" not in name:
             continue
-        key = ("out" if "ILb1ELb1E" in name else "hidden", int(r["Grid_Size_X"]), int(r["Grid_Size_Z"]))
+        var = "wide" if "k_mlp_gemm_w" in name else "out" if "ILb1ELb1E" in name else "hidden"
+        key = (var, int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X") or 256), int(r["Grid_Size_Z"]))
         groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = []
     for (var, gx, gz), us in sorted(groups.items()):
         us = us[1:] if len(us) > 2 else us   # first dispatch of each shape warms the code object
-        out.append({"variant": var, "grid_x": gx // 256, "nets": gz, "launches": len(us),
+        out.append({"variant": var, "blocks": gx, "nets": gz, "launches": len(us),
                     "avg_us": sum(us) / len(us), "min_us": min(us)})
     print(json.dumps(out, indent=1))
 

@@ -148,11 +148,14 @@ def _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd):
     assert per_species.max() < 4e-3, per_species
 
 
-def test_dnn_53_species_matches_torch_fp32():
+@pytest.mark.parametrize("wide", ["0", "1", "2"])
+def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
     """BASELINE config 4's surrogate shape: 53 species, 52 nets [55, 1600, 800, 400, 1] with
     seeded weights and synthetic normalisation, on a small mesh; the context takes 53 species for the
-    surrogate path (the FV kernels are not instantiated for it)."""
+    surrogate path (the FV kernels are not instantiated for it). wide: the 1600 -> 800 layer through
+    k_mlp_gemm (0, production) or the 256x256x64 A/B kernels (1 interleaved, 2 not)."""
     import torch
+    monkeypatch.setenv("DFMI_DNN_WIDE", wide)
     from dfmi.mesh import hex_box
     from dfmi.lib import Context
     from dfmi import case, dnn_model
