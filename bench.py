@@ -663,7 +663,8 @@ def main():
             ent = [v for key, v in tab.items()
                    if key.split("::")[-1].split("<")[0].rstrip("12") == fam or key.split("::")[-1].startswith(fam + "<")
                    or key.split("::")[-1].split("(")[0] == fam + "_cell"   # k_p_face's cell-walk form
-                   or key.split("::")[-1].startswith(fam + "_brick<")]     # k_y_prep's LDS-staged form
+                   or key.split("::")[-1].startswith(fam + "_brick<")      # k_y_prep's LDS-staged form
+                   or (fam == "k_bcg_eo" and key.split("::")[-1][:7] in ("k_eo_a<", "k_eo_b<", "k_eo_c<", "k_eo_d<"))]
             if not ent:
                 continue
             top = max(v["hbm_bytes_mean"] for v in ent)
