@@ -423,6 +423,179 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+// Ping-pong variant of the wide-layer GEMM (the guide's 256x256 eight-phase schedule, cdna_hip_programming.md
+// section 5): the same 256 x 256 x 64 tile and 8 waves, but each 64-deep K tile runs as four phases, one per
+// C quadrant of the wave's 128 x 64 tile (16 MFMAs: 4 row blocks x 2 column blocks x 2 K halves), and the two
+// wave rows run one barrier apart -- while waves 0-3 issue a phase's MFMAs, waves 4-7 issue their next phase's
+// fragment reads and DMA, so each SIMD always has one wave feeding the MFMA pipe. LDS holds two K tiles as
+// four half-tiles each (A rows of row-half 0 / 1 of both wave rows, W rows of column-half 0 / 1 of all four
+// wave columns: 128 rows x 128 B, swizzled as above), and every half-tile is re-staged (two DMA pieces per
+// wave) one phase after its last read: per tile t, phase 0 reads A0 B0 and stages B0 of t+1, phase 1 reads B1
+// and stages A0 of t+2, phase 2 reads A1 and stages B1 of t+2, phase 3 reads B0 and stages A1 of t+2, then
+// waits vmcnt(6) (the three newest half-tiles stay in flight, tile t+1 has landed). Every phase retires its own
+// reads (lgkmcnt(0)) before its first barrier, which makes the one-phase restage safe with the groups
+// staggered; each read follows the wait that retires its data by at least one barrier of both groups.
+// Past the last tile the stages re-load the last tile's data (in bounds, never read) so that every phase
+// issues the same DMA count; the epilogue drains them first. Accumulation order per output: K tiles in
+// order, K halves in order -- the same MFMA sequence as k_mlp_gemm, so the same results.
+template <bool GELU>
+__global__ void __launch_bounds__(512, 1)
+    k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
+                  long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
+  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512;
+  constexpr int HALF = 128 * BKW;                // halves (fp16 elements) per half-tile: 16 KiB
+  constexpr int STAGE = 4 * HALF;                // [A row-half 0 | A row-half 1 | W col-half 0 | W col-half 1]
+  constexpr int CLD = BNW + 8;
+  constexpr int LDS_H = 2 * STAGE > BMW * CLD ? 2 * STAGE : BMW * CLD;
+  using f32x4 = __attribute__((ext_vector_type(4))) float;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
+  const int z = blockIdx.z;
+  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
+  const int ntn = (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int m0 = (wg / ntn) * BMW, n0 = (wg % ntn) * BNW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // DMA sources: half-tile h, piece q: half-row hr = 16 wave + 8 q + (lane >> 3), 16-B chunk lane & 7 of the
+  // LDS row holding logical chunk (lane & 7) ^ ((hr >> 1) & 7). A half h < 2: tile row (hr / 64) 128 + 64 h +
+  // hr % 64 (rows of both wave rows); W half h = 2 + jh: tile row (hr / 32) 64 + 32 jh + hr % 32 (all columns)
+  const _Float16* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int hr = 16 * wave + 8 * q + (lane >> 3), ch = (lane & 7) ^ ((hr >> 1) & 7);
+      if (h < 2) {
+        const int row = (hr >> 6) * 128 + h * 64 + (hr & 63);
+        src[h][q] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
+      } else {
+        const int row = (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31);
+        src[h][q] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
+      }
+    }
+  auto stage_half = [&](int buf, int h, int k0) {
+    _Float16* d = lds + buf * STAGE + h * HALF + 16 * wave * BKW;
+    glds16(src[h][0] + k0, d);
+    glds16(src[h][1] + k0, d + 8 * BKW);
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int r = lane & 15, g = lane >> 4;
+  const int fo[2] = {r * BKW + ((g) ^ (r >> 1)) * 8, r * BKW + ((4 + g) ^ (r >> 1)) * 8};
+  half8 af[4][2], bf[2][2];   // the quadrant's fragments: 4 row blocks / 2 column blocks x 2 K halves
+  auto read_a = [&](int buf, int ih) {
+    const _Float16* s0 = lds + buf * STAGE + ih * HALF + (wr * 64) * BKW;
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) af[ib][kh] = *reinterpret_cast<const half8*>(s0 + ib * 16 * BKW + fo[kh]);
+  };
+  auto read_b = [&](int buf, int jh) {
+    const _Float16* s0 = lds + buf * STAGE + (2 + jh) * HALF + (wc * 32) * BKW;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) bf[jb][kh] = *reinterpret_cast<const half8*>(s0 + jb * 16 * BKW + fo[kh]);
+  };
+  const int nk = K / BKW;
+  auto kloop = [&](auto jl_c) {
+    constexpr int JL = decltype(jl_c)::value;
+    auto quad = [&](int ih, int jh) {   // 16 MFMAs, K half outer so that dependent MFMAs are 8 apart
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          if (2 * jh + jb < JL)
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib)
+              acc[4 * ih + ib][2 * jh + jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ib][kh], bf[jb][kh],
+                                                                                   acc[4 * ih + ib][2 * jh + jb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // one phase: fragment reads and one half-tile's DMA, own reads retired, barrier, MFMAs, barrier
+    auto sync_mfma = [&](int ih, int jh) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this phase's reads retired before its first barrier
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      quad(ih, jh);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // no scalar load outstanding into the loop
+    // prologue: tile 0 complete, tile 1's A0 B1 A1 in flight (the steady-state issue order)
+    const int k1 = min(1, nk - 1) * BKW;
+    stage_half(0, 0, 0); stage_half(0, 3, 0); stage_half(0, 1, 0); stage_half(0, 2, 0);
+    stage_half(1, 0, k1); stage_half(1, 3, k1); stage_half(1, 1, k1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();   // the stagger: waves 4-7 run one barrier behind
+    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < nk; ++t) {
+      const int b = t & 1;
+      const int kn = min(t + 1, nk - 1) * BKW, k2 = min(t + 2, nk - 1) * BKW;
+      read_b(b, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(b, 0);
+      stage_half(b ^ 1, 2, kn);          // W col-half 0 of tile t+1 (its slot's last read: tile t-1, phase 3)
+      sync_mfma(0, 0);
+      read_b(b, 1);
+      stage_half(b, 0, k2);              // A row-half 0 of tile t+2 (last read: phase 0)
+      sync_mfma(0, 1);
+      read_a(b, 1);
+      stage_half(b, 3, k2);              // W col-half 1 of tile t+2 (last read: phase 1)
+      sync_mfma(1, 1);
+      read_b(b, 0);
+      stage_half(b, 1, k2);              // A row-half 1 of tile t+2 (last read: phase 2)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t+1 landed (t+2's first three halves in flight)
+      sync_mfma(1, 0);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();   // both groups end on the same barrier count
+    __builtin_amdgcn_s_waitcnt(0);              // the re-staging DMAs past the last tile drained
+  };
+  const int wm = wr * 128, wn = wc * 64;
+  switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
+    case 4: kloop(std::integral_constant<int, 4>{}); break;
+    case 3: kloop(std::integral_constant<int, 3>{}); break;
+    case 2: kloop(std::integral_constant<int, 2>{}); break;
+    case 1: kloop(std::integral_constant<int, 1>{}); break;
+    default: kloop(std::integral_constant<int, 0>{}); break;
+  }
+  // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
+  __syncthreads();
+  _Float16* cs = lds;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
+    const bool live = col < N;
+    const float bv = live ? bias[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int rl = wm + 16 * i + 4 * g + e;
+        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
+        if (GELU) v = gelu_fast2(v);
+        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
+        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
+      }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
+    const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
+    const int row = m0 + rl, col = n0 + ch * 8;
+    if (row < M && col < ldc)
+      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+  }
+}
+
 // reacting-cell compaction (deterministic): per-block counts, one-block scan, scatter
 constexpr int CB = 1024;
 __global__ void k_react_count(int C, const double* __restrict__ T, double Tr, int* __restrict__ bc) {
@@ -614,9 +787,10 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   d.last_reacting = nr;
   if (nr == 0) return;
   const int chunk = std::min(nr, d.chunk);
-  // DFMI_DNN_WIDE=1|2: the 256x256x64 kernel for the wide layers (1: DMA/reads interleaved, 2: not); measured
-  // 9.77 / 10.07 ms against k_mlp_gemm's 9.57 ms per 65,536-row chunk of the 1600->800 layer, so off
-  const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 0; }();   // A/B: 256x256x64 kernel for the wide layers
+  // the wide layers (K % 64 == 0, N >= 512: the 1600 -> 800 layer) through the 256x256x64 ping-pong kernel
+  // (DFMI_DNN_WIDE=3, default): 8.72 ms per 65,536-row chunk against k_mlp_gemm's 9.66 (DFMI_DNN_WIDE=0);
+  // 1 / 2: the single-group variants, 9.77 / 10.07 ms
+  const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 3; }();   // A/B: 256x256x64 kernel for the wide layers
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
@@ -648,7 +822,10 @@ void dnn_solve(Ctx& x, const char* rho_field) {
                            d.part.p, sP);
       } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
-        if (wide == 2)
+        if (wide == 3)
+          hipLaunchKernelGGL((k_mlp_gemm_pp<true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
+        else if (wide == 2)
           hipLaunchKernelGGL((k_mlp_gemm_w<true, false>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
         else

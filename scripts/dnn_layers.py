@@ -39,7 +39,7 @@ def main():
     bsf, bmag, bdc, bw, bfc = m.boundary_arrays()
     ctx.init_constant_fields_boundary(bsf, bmag, bdc, bw, bfc, pt["calculated"], pt["extrapolated"])
     ctx.set_inert_index(S - 1)
-    dims = [S + 2, 1600, 800, 400, 1]
+    dims = [int(v) for v in os.environ["DIMS"].split(",")] if os.environ.get("DIMS") else [S + 2, 1600, 800, 400, 1]
     ctx.dnn_set_model(dims, dnn_model.seeded_weights(n_modules=S - 1, dims=dims), np.zeros(S + 2), np.ones(S + 2),
                       np.zeros(S - 1), np.full(S - 1, 0.01))
     ctx.chem_set_options(2)

@@ -16,7 +16,8 @@ def main(d):
         name = r["Kernel_Name"]
         if "k_mlp_gemm" not in name:
             continue
-        var = "wide" if "k_mlp_gemm_w" in name else "out" if "ILb1ELb1E" in name else "hidden"
+        var = ("pingpong" if "k_mlp_gemm_pp" in name else "wide" if "k_mlp_gemm_w" in name
+               else "out" if "ILb1ELb1E" in name else "hidden")
         key = (var, int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X") or 256), int(r["Grid_Size_Z"]))
         groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = []

@@ -148,12 +148,12 @@ def _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd):
     assert per_species.max() < 4e-3, per_species
 
 
-@pytest.mark.parametrize("wide", ["0", "1", "2"])
+@pytest.mark.parametrize("wide", ["0", "1", "2", "3"])
 def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
     """BASELINE config 4's surrogate shape: 53 species, 52 nets [55, 1600, 800, 400, 1] with
     seeded weights and synthetic normalisation, on a small mesh; the context takes 53 species for the
     surrogate path (the FV kernels are not instantiated for it). wide: the 1600 -> 800 layer through
-    k_mlp_gemm (0, production) or the 256x256x64 A/B kernels (1 interleaved, 2 not)."""
+    k_mlp_gemm (0, production) or the 256x256x64 A/B kernels (1 interleaved, 2 not, 3 ping-pong)."""
     import torch
     monkeypatch.setenv("DFMI_DNN_WIDE", wide)
     from dfmi.mesh import hex_box
@@ -214,3 +214,48 @@ def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
     assert np.median(err) < 2e-3, np.median(err)
     assert err.max() < 2e-2, err.max()
     _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd)
+
+
+def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
+    """The 256x256x64 wide-layer kernels (DFMI_DNN_WIDE=1 interleaved, 3 ping-pong: staggered wave groups,
+    one-phase half-tile restaging) issue the same MFMA sequence per output as k_mlp_gemm, so the source
+    terms of 32,768 reacting cells x 52 nets agree bitwise -- a race in a pipeline's LDS reuse would show here
+    (128 row tiles x 4 column tiles x 52 nets per launch, every CU busy)."""
+    from dfmi.mesh import hex_box
+    from dfmi.lib import Context
+    from dfmi import case, dnn_model
+    S = 53
+    m = hex_box(32, 32, 32)
+    C = m.n_cells
+    dims = [S + 2, 1600, 800, 400, 1]
+    mods = dnn_model.seeded_weights(n_modules=S - 1, dims=dims, seed=3)
+    rng = np.random.default_rng(5)
+    Y = rng.gamma(0.3, 1.0, (S, C)) + 1e-8
+    Y /= Y.sum(axis=0)
+    T = 800.0 + 1500.0 * rng.random(C)
+    p = np.full(C, 101325.0)
+    rho = p / (300.0 * T)
+    out = {}
+    for wide in ("0", "1", "3"):
+        monkeypatch.setenv("DFMI_DNN_WIDE", wide)
+        ctx = Context(0)
+        pt = case.default_patch_types(m)
+        rows, cols = m.proc_rows_cols()
+        ctx.set_constant_values(C, C, m.n_faces, m.n_boundary_slots, m.n_patches, int(rows.size), m.patch_sizes, S, 1e6)
+        ctx.set_cyclic_info(m.cyclic_neighbour())
+        ctx.set_constant_indexes(m.owner, m.neighbour, rows, cols, 0)
+        ctx.init_constant_fields_internal(m.sf, m.mag_sf, m.weight, m.delta_coeffs, m.volume, m.mesh_distance)
+        bsf, bmag, bdc, bw, bfc = m.boundary_arrays()
+        ctx.init_constant_fields_boundary(bsf, bmag, bdc, bw, bfc, pt["calculated"], pt["extrapolated"])
+        ctx.set_inert_index(S - 1)
+        xmu, xstd = np.zeros(S + 2), np.ones(S + 2)
+        xmu[0], xstd[0], xmu[1], xstd[1] = 1300.0, 400.0, 101325.0, 1.0
+        ctx.dnn_set_model(dims, mods, xmu, xstd, np.zeros(S - 1), np.full(S - 1, 0.01))
+        for n, v in (("T", T), ("p", p), ("rho", rho), ("Y", Y)):
+            ctx.set_field(n, v)
+        assert ctx.dnn_infer() == C
+        out[wide] = ctx.get_field("RR", (S, C))
+        ctx.close()
+    assert np.isfinite(out["0"]).all()
+    for wide in ("1", "3"):
+        assert np.array_equal(out[wide], out["0"]), (wide, np.abs(out[wide] - out["0"]).max())
