@@ -20,7 +20,7 @@ for v in "${VS[@]}"; do
 import json, os, sys
 n = sys.argv[1]
 d = json.loads(open(f"gpurun_out/ab_{n}.log").read().strip().splitlines()[-1])
-out = [n, round(d["ms_per_step"], 3), "ms"]
+out = [n, round(d["ms_per_step"], 3), "ms", "iters", d.get("solver_iters")]
 for k in os.environ["KERNELS"].split(","):
     r = (d.get("rooflines") or {}).get(k) or {}
     out += [k, round(r.get("avg_us") or 0, 1), "us", "frac", round(r.get("frac") or 0, 3)]
