@@ -232,30 +232,56 @@ bool step_overlap(const Ctx& x) {
   static const bool on = [] { const char* e = std::getenv("DFMI_STEP_OVERLAP"); return !(e && std::atoi(e) == 0); }();
   return on && x.nranks == 1 && !halo_active(x) && x.ktimer.targets.empty();
 }
-void do_U_Y(Ctx& x) {
-  if (!step_overlap(x)) { do_U(x); do_Y(x); return; }
+// the side stream forks from the main one and runs the YEqn front; ev_join marks its end
+void do_U_Y_fork(Ctx& x) {
   if (!x.stream2) {
     DFMI_HIP(hipStreamCreateWithFlags(&x.stream2, hipStreamNonBlocking));
-    DFMI_HIP(hipEventCreateWithFlags(&x.ev_fork, hipEventDisableTiming));
-    DFMI_HIP(hipEventCreateWithFlags(&x.ev_join, hipEventDisableTiming));
+    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e})
+      DFMI_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
   DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_fork, 0));
-  {
-    OnStream _os(x, x.stream2);
-    do_Y_front(x);
-    DFMI_HIP(hipEventRecord(x.ev_join, x.stream2));
-  }
+  OnStream _os(x, x.stream2);
+  do_Y_front(x);
+  DFMI_HIP(hipEventRecord(x.ev_join, x.stream2));
+}
+void do_U_Y(Ctx& x) {
+  if (!step_overlap(x)) { do_U(x); do_Y(x); return; }
+  do_U_Y_fork(x);
   do_U(x);
   DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_join, 0));
   do_Y_back(x);
 }
-void do_E(Ctx& x) {
-  e_assemble(x);
+void do_E_back(Ctx& x) {
   Matrix& A = x.mE;
   solve_bicgstab(x, "E", 1, nullptr, A.lower, 0, A.upper, 0, A.diag, 0, A.source, 0, A.ic, A.bc, 0, "he", x.f("he"), 0,
                  x.solver["E"]);
   e_post_solve(x);
+}
+void do_E(Ctx& x) {
+  e_assemble(x);
+  do_E_back(x);
+}
+// UEqn, YEqn, EEqn with the overlap above and one more: the EEqn scheme terms (K's limited weights from the
+// UEqn's K, the cubic correction of hDiffCorrFlux from the YEqn preparation) read nothing the Y solve writes,
+// so they run on the side stream after both while the main stream solves the species; the rest of the
+// assembly needs the solved Y (the thermo's boundary energy gradient) and follows the Y solve
+void do_U_Y_E(Ctx& x) {
+  if (!step_overlap(x)) { do_U_Y(x); do_E(x); return; }
+  do_U_Y_fork(x);
+  do_U(x);
+  DFMI_HIP(hipEventRecord(x.ev_u, x.stream));
+  {
+    OnStream _os(x, x.stream2);
+    DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_u, 0));
+    e_assemble_front(x);
+    DFMI_HIP(hipEventRecord(x.ev_e, x.stream2));
+  }
+  DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_join, 0));
+  do_Y_back(x);
+  DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_e, 0));
+  e_assemble_back(x);
+  do_E_back(x);
 }
 void do_p(Ctx& x) {
   p_assemble(x);
@@ -628,8 +654,8 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     copy_old(x);                    // preTimeStep
     if (x.chem.mode == 2) dnn_prepare(x);   // reacting cells of this step's T (read after the UEqn polls)
     rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
-    do_U_Y(x);                      // UEqn, YEqn (one rank: the chemistry and YEqn assembly beside the UEqn)
-    do_E(x);                        // EEqn
+    do_U_Y_E(x);                    // UEqn, YEqn, EEqn (one rank: the chemistry and YEqn assembly beside the
+                                    // UEqn, the EEqn assembly beside the Y solve)
     thermo_correct(x, false);       // correctThermo
     for (int i = 0; i < n_corr; ++i) {   // pEqn_GPU.H
       thermo_rho_from_psi(x);

@@ -294,7 +294,7 @@ struct Ctx {
   SolverWs& sws() { return ws_is_y ? ws_y : ws; }
   // side stream of the time step (dfmi_time_step: chemistry + YEqn preparation beside the UEqn) and its events
   hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr;
   // final solver state of the last solve of each equation, copied asynchronously at the end of the
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
@@ -408,6 +408,8 @@ void y_assemble(Ctx& x);
 void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs);
 void y_post_solve(Ctx& x);
 void e_assemble(Ctx& x);
+void e_assemble_front(Ctx& x);   // the scheme terms (independent of the Y solve)
+void e_assemble_back(Ctx& x);    // boundary energy gradient, he's boundary values, the matrix
 void e_post_solve(Ctx& x);
 void conv_weights(Ctx& x);   // div(phi,Yi_h) weights (start of YEqn; EEqn reuses them)
 void copy_old(Ctx& x);

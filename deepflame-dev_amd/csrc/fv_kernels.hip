@@ -2748,18 +2748,25 @@ void y_post_solve(Ctx& x) {
   halo_fields(x, {"Y"});
 }
 
-void e_assemble(Ctx& x) {
+// EEqn assembly in two parts: the scheme terms (K's limited weights from the UEqn's K, hDiffCorrFlux's cubic
+// correction from the YEqn preparation) read nothing of the Y solve; the boundary energy gradient (the
+// thermo at the solved boundary Y), he's boundary values and the matrix come after it
+void e_assemble_front(Ctx& x) { e_scheme_terms(x); }
+void e_assemble_back(Ctx& x) {
   Matrix& A = x.mE;
   MeshView m = x.view();
   thermo_energy_gradient(x);   // eeqn_calculate_energy_gradient (dfEEqn.cu:148, :266-287)
   k_bc_correct(x, "he", x.f("he"), x.f("boundary_he"), 1);
-  e_scheme_terms(x);
   const double* eg = x.f("boundary_heGradient");
   LAUNCH_W(k_e_assemble, x.C, m, x.st("he"), x.st("K"), x.f("he"), x.f("boundary_he"), x.f("rho"), x.f("rho_old"),
          x.f("K"), x.f("K_old"), x.f("boundary_K"), x.f("phi"), x.f("boundary_phi"), x.f("alpha"),
          x.f("boundary_alpha"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("dpdt"), x.f("diffAlphaD"),
          eg, A.lower.p, A.upper.p, A.diag.p, A.source.p, A.ic.p, A.bc.p, x.sch_w(0), x.sch_w(1), x.sch_w(2),
          x.sch_w(3), x.sch_w(4), x.sch_w(5));
+}
+void e_assemble(Ctx& x) {
+  e_assemble_front(x);
+  e_assemble_back(x);
 }
 
 void e_post_solve(Ctx& x) {

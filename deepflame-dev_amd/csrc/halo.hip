@@ -150,6 +150,8 @@ Ctx::~Ctx() {
   if (stream2) { (void)hipStreamSynchronize(stream2); (void)hipStreamDestroy(stream2); }
   if (ev_fork) (void)hipEventDestroy(ev_fork);
   if (ev_join) (void)hipEventDestroy(ev_join);
+  if (ev_u) (void)hipEventDestroy(ev_u);
+  if (ev_e) (void)hipEventDestroy(ev_e);
 }
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }
