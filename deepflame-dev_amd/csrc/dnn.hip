@@ -438,10 +438,15 @@ __global__ void __launch_bounds__(512, 1)
 // Past the last tile the stages re-load the last tile's data (in bounds, never read) so that every phase
 // issues the same DMA count; the epilogue drains them first. Accumulation order per output: K tiles in
 // order, K halves in order -- the same MFMA sequence as k_mlp_gemm, so the same results.
-template <bool GELU>
+// OUT (the last hidden layer, K zero-padded to a multiple of 64): the 1-wide output layer fused into the
+// epilogue as in k_mlp_gemm -- per row, the products with wo over each wave's 64 columns, summed over the
+// lane's four 16-column blocks and a 16-lane xor tree, written as partial P[z][4 tile_n + wave_n][M]: the
+// same 64-column groups in the same order as k_mlp_gemm's two 64-column partials per 128-wide tile.
+template <bool GELU, bool OUT = false>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
-                  long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
+                  long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
+                  const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0) {
   constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512;
   constexpr int HALF = 128 * BKW;                // halves (fp16 elements) per half-tile: 16 KiB
   constexpr int STAGE = 4 * HALF;                // [A row-half 0 | A row-half 1 | W col-half 0 | W col-half 1]
@@ -451,6 +456,7 @@ __global__ void __launch_bounds__(512, 1)
   __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
+  if constexpr (OUT) { wo += z * swo; P += z * sP; }
   const int ntn = (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
@@ -566,6 +572,40 @@ __global__ void __launch_bounds__(512, 1)
     case 2: kloop(std::integral_constant<int, 2>{}); break;
     case 1: kloop(std::integral_constant<int, 1>{}); break;
     default: kloop(std::integral_constant<int, 0>{}); break;
+  }
+  if constexpr (OUT) {   // the fused output layer (no LDS use: the drained stages are not touched)
+    float bv[4], wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      bv[j] = col < N ? bias[col] : 0.0f;
+      wv[j] = col < N ? (float)wo[col] : 0.0f;   // dead columns contribute 0
+    }
+    float* Pw = P + (long)(4 * (wg % ntn) + wc) * M;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        f32x2 sacc = {0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j]);   // the Linear's fp16 output
+          if (GELU) v = gelu_fast2(v);
+          const f32x2 hq = {(float)(_Float16)v.x, (float)(_Float16)v.y};   // the fp16 activation
+          sacc = __builtin_elementwise_fma(hq, f32x2(wv[j]), sacc);
+        }
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) {
+          sacc.x += __shfl_xor(sacc.x, off);
+          sacc.y += __shfl_xor(sacc.y, off);
+        }
+        const int row = m0 + wm + 16 * i + 4 * g + e;
+        if ((lane & 15) == 0) {
+          if (row < M) Pw[row] = sacc.x;
+          if (row + 1 < M) Pw[row + 1] = sacc.y;
+        }
+      }
+    return;
   }
   // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
   __syncthreads();
@@ -721,7 +761,9 @@ void dnn_upload(Ctx& x, int nmod, int nlayers, const int* dims, const float* par
   for (int l = 0; l < nlayers; ++l) {
     // K of every layer padded to the GEMM K tile; activations are stored with that row stride (the
     // padding columns are written as 0, the padded weight columns are 0)
-    d.Kp[l] = (dims[l] + KPAD - 1) / KPAD * KPAD;
+    // (widths >= 512 to 64: the ping-pong kernel's K tile; the extra zero columns add exact zeros)
+    const int kp = dims[l] >= 512 ? 64 : KPAD;
+    d.Kp[l] = (dims[l] + kp - 1) / kp * kp;
     if (l == nlayers - 1) DFMI_CHECK(dims[l] % 8 == 0, "DNN: last hidden width must be a multiple of 8");
   }
   // repack weights: per layer [module][out][Kp] fp16 (K zero-padded), biases fp16-rounded, kept as fp32 [module][out]
@@ -806,7 +848,10 @@ void dnn_solve(Ctx& x, const char* rho_field) {
     long sIn = 0;
     _Float16* bufs[2] = {d.h0.p, d.h1.p};
     int lda = d.Kp[0];
-    const int nq = 2 * blocks_for(d.dims[L - 1], BN);   // partial sums per row of the fused output layer
+    // the last hidden layer by the ping-pong kernel where its K allows (four 64-column partials per 256-wide
+    // tile) or by k_mlp_gemm (two per 128-wide tile): partial sums per row of the fused output layer
+    const bool pp_out = wide == 3 && d.Kp[L - 2] % 64 == 0 && d.Kp[L - 2] >= 512;
+    const int nq = pp_out ? 4 * blocks_for(d.dims[L - 1], 256) : 2 * blocks_for(d.dims[L - 1], BN);
     const long sP = (long)nq * n;
     if (d.part.n < (size_t)d.nmod * sP) d.part.alloc((size_t)d.nmod * sP);
     for (int l = 0; l + 1 < L; ++l) {
@@ -817,9 +862,14 @@ void dnn_solve(Ctx& x, const char* rho_field) {
       KScope _ks(x, "k_mlp_gemm");
       if (l + 2 == L) {   // last hidden layer: the output layer fused into the epilogue
         d.gemm_flops += 2.0 * n * N * d.nmod;
-        hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                           (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
-                           d.part.p, sP);
+        if (pp_out)
+          hipLaunchKernelGGL((k_mlp_gemm_pp<true, true>), dim3(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod),
+                             dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
+                             ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1], d.part.p, sP);
+        else
+          hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
+                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
+                             d.part.p, sP);
       } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
         if (wide == 3)
