@@ -28,6 +28,18 @@ namespace {
 constexpr int TPB = 256;
 constexpr int NW = TPB / 64;
 constexpr int MAX_BLOCKS = 2048;
+// blocks of the even-odd half-row passes (DFMI_EO_BLOCKS): measured 256 / 512 / 768 / 1024 / 2048 / 3072 / 4096
+// -> 42.8 / 34.7 / 36.7 / 32.8 / 35.1 / 47.7 / 45.0 us per Schur application (the partial sums every consumer
+// block re-sums grow with the grid; fewer blocks leave too few waves)
+inline int eo_max_blocks() {
+  static const int v = [] { const char* e = std::getenv("DFMI_EO_BLOCKS"); return e ? std::max(64, std::atoi(e)) : 1024; }();
+  return v;
+}
+// blocks of the PCG kernels (DFMI_CG_BLOCKS, A/B)
+inline int cg_max_blocks() {
+  static const int v = [] { const char* e = std::getenv("DFMI_CG_BLOCKS"); return e ? std::max(64, std::min(MAX_BLOCKS, std::atoi(e))) : MAX_BLOCKS; }();
+  return v;
+}
 constexpr int PAD = INT_MIN;
 constexpr int NSCAL = 16;
 
@@ -1491,7 +1503,8 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs) {
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
   const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
-  const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C + (size_t)nsys * nblk * 12 + 64;
+  const size_t need = (size_t)BCG_VECS * nsys * Ce + (size_t)nsys * W * C +
+                      (size_t)nsys * std::max(nblk, eo_max_blocks()) * 12 + 64;
   if (x.sws().buf.n < need) { x.sws().buf.alloc(need); x.sws().buf.zero(x.stream); }   // no stale NaN under a 0 coefficient
   const long N = nsys * Ce;
   *dS = x.sws().buf.p;
@@ -1623,7 +1636,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   DFMI_HIP(hipGetLastError());
   if (x.ell.eo) {   // the reduced system (build_ell decided; several ranks: split-vector halos, gathered sums)
     const int ne = x.ell.ne, no = (int)C - ne;
-    const int hb = std::min(blocks_for(std::max(ne, no), TPB), MAX_BLOCKS);
+    const int hb = std::min(blocks_for(std::max(ne, no), TPB), eo_max_blocks());
     const dim3 gh(hb, nsys);
     const ColView ec = x.ell.eo_cols();
     double* pI = val + (size_t)nsys * W * C;       // (||b - A x0||^2 colour 0)
@@ -1754,7 +1767,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   CommTag _ct(x, std::string("pcg ") + eqn);
   const long C = x.C, Ce = (long)x.C + x.H;
   const int W = x.ell.W;
-  const int nblk = std::min(blocks_for(C, TPB), MAX_BLOCKS);
+  const int nblk = std::min(blocks_for(C, TPB), cg_max_blocks());
   auto& WS = x.sws();
   const size_t need = 8 * Ce + (size_t)W * C + (size_t)nblk * 6 + 64;
   if (WS.buf.n < need) WS.buf.alloc(need);
