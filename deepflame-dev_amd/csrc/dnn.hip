@@ -35,28 +35,121 @@ constexpr int TILE_W = BN * BK;           // halves per staged W tile (8 KiB)
 // the exact-erf form; the library erff branches per lane on |x| < 1). Packed fp32 arithmetic (v_pk_mul_f32 / v_pk_fma_f32, two values per instruction: no MFMA competes for the
 // issue slots in the epilogue), hardware reciprocal and exp2 (<= 1 ulp each; __frcp_rn expands to the
 // correctly-rounded division sequence, which dominated the epilogue), explicit fmas (-ffp-contract=off).
+// The form 0.5 v (1 + sign(v) erf(|v|/sqrt2)) = 0.5 fma(|v|, erf(|v|/sqrt2), v), with 1/sqrt2 folded into the
+// constants: no copysign, one abs per value, 12% faster at full occupancy than evaluating u = v/sqrt2 first
+// (scripts/probes/gelu_probe.hip); the epilogue is VALU-bound on it (a 64-deep K leaves it nothing to hide behind).
 using f32x2 = __attribute__((ext_vector_type(2))) float;
+using half2v = __attribute__((ext_vector_type(2))) _Float16;
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 v) {
-  const f32x2 u = v * 0.70710678118654752440f;
-  const f32x2 a = __builtin_elementwise_abs(u);
-  const f32x2 d = __builtin_elementwise_fma(a, f32x2(0.3275911f), f32x2(1.0f));
+  const f32x2 a = __builtin_elementwise_abs(v);
+  const f32x2 d = __builtin_elementwise_fma(a, f32x2(0.23164202848f), f32x2(1.0f));   // 1 + 0.3275911 |v| / sqrt2
   const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
   f32x2 q = __builtin_elementwise_fma(t, f32x2(1.061405429f), f32x2(-1.453152027f));
   q = __builtin_elementwise_fma(t, q, f32x2(1.421413741f));
   q = __builtin_elementwise_fma(t, q, f32x2(-0.284496736f));
   q = __builtin_elementwise_fma(t, q, f32x2(0.254829592f));
-  const f32x2 poly = t * q;
-  const f32x2 w = (a * a) * -1.44269504088896340736f;
+  const f32x2 w = v * (v * -0.72134752044448170368f);                                 // -(v^2 / 2) log2(e)
   const f32x2 ex = {__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
-  const f32x2 e = __builtin_elementwise_fma(-poly, ex, f32x2(1.0f));
-  const f32x2 hv = v * 0.5f;
-  const f32x2 se = {copysignf(e.x, u.x), copysignf(e.y, u.y)};
-  return __builtin_elementwise_fma(hv, se, hv);
+  const f32x2 e = __builtin_elementwise_fma(-(t * q), ex, f32x2(1.0f));                // erf(|v| / sqrt2)
+  return __builtin_elementwise_fma(a, e, v) * 0.5f;
 }
 
 // fp16 rounding kept in fp32 registers: torch's fp16 Linear writes its output (x W^T + b, fp32
 // accumulation) as fp16 before the GELU reads it, and the GELU's own output is rounded again
-__device__ __forceinline__ f32x2 round16(f32x2 v) { return {(float)(_Float16)v.x, (float)(_Float16)v.y}; }
+// (v_cvt_pk_f16_f32: one conversion per pair)
+__device__ __forceinline__ half2v to16(f32x2 v) { return __builtin_convertvector(v, half2v); }
+__device__ __forceinline__ f32x2 round16(f32x2 v) { return __builtin_convertvector(to16(v), f32x2); }
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// GEMM epilogue shared by the kernels below, for one wave's 16 NI x 64 accumulator tile (NI x 4 blocks of 16 x 16,
+// C/D map col = lane & 15, row = 4 (lane >> 4) + e) at tile-local rows wm.., columns wn.. of the N tile at n0:
+// bias + GELU, rounded to fp16, into the LDS output tile cs (row stride CLD). 16-column blocks wholly past N (the
+// padded tail of the last N tile: 224 of the 1,024 columns of an 800-wide layer) are written as zeros without
+// evaluating the GELU -- a wave-uniform test; the GELU is the epilogue's whole cost.
+template <bool GELU, int CLD, int NI = 8>
+__device__ __forceinline__ void stage_out_tile(const f32x4 (&acc)[NI][4], _Float16* cs, int wm, int wn, int n0, int N,
+                                               const float* __restrict__ bias, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
+    if (n0 + wn + 16 * j >= N) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[(wm + 16 * i + 4 * g + e) * CLD + cl] = (_Float16)0.0f;
+      continue;
+    }
+    const bool live = col < N;
+    const float bv = live ? bias[col] : 0.0f;
+    auto block = [&](auto full_c) {   // full: all 16 columns live (no per-lane select)
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int rl = wm + 16 * i + 4 * g + e;
+          f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
+          if (GELU) v = gelu_fast2(v);
+          half2v h = to16(v);
+          if (!decltype(full_c)::value && !live) h = half2v{(_Float16)0.0f, (_Float16)0.0f};
+          cs[rl * CLD + cl] = h.x;
+          cs[(rl + 1) * CLD + cl] = h.y;
+        }
+    };
+    if (n0 + wn + 16 * j + 16 <= N) block(std::true_type{});
+    else block(std::false_type{});
+  }
+}
+
+// OUT epilogue (the last hidden layer): the net's 1-wide output layer fused in instead of storing the tile --
+// each fp16-rounded activation times its output weight wo[col], summed per row (fp32, fixed order: over the
+// lane's four 16-column blocks, then a 16-lane xor tree) into the wave's partial Pw[row]. Blocks wholly past N
+// are skipped (their products are zeros).
+template <bool GELU>
+__device__ __forceinline__ void out_layer_partials(const f32x4 (&acc)[8][4], float* __restrict__ Pw, int M, int m0, int wm,
+                                                   int wn, int n0, int N, const float* __restrict__ bias,
+                                                   const _Float16* __restrict__ wo, int lane) {
+  float bv[4], wv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn + 16 * j + (lane & 15);
+    bv[j] = col < N ? bias[col] : 0.0f;
+    wv[j] = col < N ? (float)wo[col] : 0.0f;   // dead columns contribute 0
+  }
+  f32x2 sacc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sacc[i][0] = sacc[i][1] = f32x2{0.0f, 0.0f};
+  // column blocks outermost (one wave-uniform test each; the per-row sums still run over j in order)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (n0 + wn + 16 * j >= N) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j]);   // the Linear's fp16 output
+        if (GELU) v = gelu_fast2(v);
+        sacc[i][e / 2] = __builtin_elementwise_fma(round16(v), f32x2(wv[j]), sacc[i][e / 2]);   // the fp16 activation
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      f32x2 sa = sacc[i][e / 2];
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1) {
+        sa.x += __shfl_xor(sa.x, off);
+        sa.y += __shfl_xor(sa.y, off);
+      }
+      const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
+      if ((lane & 15) == 0) {
+        if (row < M) Pw[row] = sa.x;
+        if (row + 1 < M) Pw[row + 1] = sa.y;
+      }
+    }
+}
 
 // 16-byte global -> LDS DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_wave + 16 l
 __device__ __forceinline__ void glds16(const _Float16* g, _Float16* lds_wave) {
@@ -93,7 +186,6 @@ __global__ void __launch_bounds__(256, 2)
                const _Float16* __restrict__ wo, long swo, float* __restrict__ P, long sP) {
   constexpr int BMW = 256, GTW = 256;
   constexpr int TILE_A = BMW * BK, STAGE = TILE_A + TILE_W;
-  using f32x4 = __attribute__((ext_vector_type(4))) float;
   __shared__ __attribute__((aligned(16))) _Float16 lds[NBUF * STAGE];   // [buf][A (256 x 32) | W (128 x 32)]
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC; wo += z * swo; P += z * sP;
@@ -174,39 +266,8 @@ __global__ void __launch_bounds__(256, 2)
       cur = cur == NBUF - 1 ? 0 : cur + 1;
     }
   }
-  // epilogue: bias + GELU in registers (C/D map col = lane & 15, row = 4 (lane >> 4) + e)
   if constexpr (OUT) {
-    float bv[4], wv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-      bv[j] = col < N ? bias[col] : 0.0f;
-      wv[j] = col < N ? (float)wo[col] : 0.0f;   // dead columns contribute 0
-    }
-    float* Pw = P + (long)(2 * (wg % ntn) + (wave & 1)) * M;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        f32x2 sacc = {0.0f, 0.0f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j]);   // the Linear's fp16 output
-          if (GELU) v = gelu_fast2(v);
-          const f32x2 hq = {(float)(_Float16)v.x, (float)(_Float16)v.y};   // the fp16 activation
-          sacc = __builtin_elementwise_fma(hq, f32x2(wv[j]), sacc);
-        }
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          sacc.x += __shfl_xor(sacc.x, off);
-          sacc.y += __shfl_xor(sacc.y, off);
-        }
-        const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + e;
-        if ((lane & 15) == 0) {
-          if (row < M) Pw[row] = sacc.x;
-          if (row + 1 < M) Pw[row + 1] = sacc.y;
-        }
-      }
+    out_layer_partials<GELU>(acc, P + (long)(2 * (wg % ntn) + (wave & 1)) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
     return;
   }
   // the fp16 tile staged through LDS, written back as 16-B row chunks
@@ -214,22 +275,7 @@ __global__ void __launch_bounds__(256, 2)
   constexpr int CLD = BN + 8;
   static_assert(BMW * CLD <= NBUF * STAGE, "output tile must fit the staging ring");
   _Float16* cs = lds;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
-    const bool live = col < N;
-    const float bv = live ? bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rl = wm + 16 * i + 4 * (lane >> 4) + e;
-        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
-        if (GELU) v = gelu_fast2(v);
-        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
-        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
-      }
-  }
+  stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < BMW * BN / 8 / GTW; ++it) {
@@ -237,6 +283,83 @@ __global__ void __launch_bounds__(256, 2)
     const int row = m0 + rl, col = n0 + ch * 8;
     if (row < M && col < ldc)
       *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+  }
+}
+
+// Input-layer variant (K <= 64: the 55 -> 1600 first layer, K padded to 64): with one K tile there is nothing for
+// a DMA ring to overlap, and the layer's time is its epilogue -- 5.45 G GELUs per 65,536-row chunk of the 52 nets,
+// VALU-bound, plus 10.9 GB of fp16 activations written. So the tile is small enough for four workgroups (16
+// waves) per CU to hide the GELU's dependent transcendental latencies behind one another: 128 x 128 x 64, 4 waves
+// (2 x 2) of 64 x 64 (4 x 4 MFMA blocks), the whole K staged by DMA at once (A and W 128 rows x 128 B each,
+// rows swizzled as in k_mlp_gemm_w), then the output tile staged through the same LDS (35 KiB) and written as
+// 16-B row chunks. Same MFMA order per output as k_mlp_gemm (K halves in order), so the same results.
+template <bool GELU>
+__global__ void __launch_bounds__(256, 4)
+    k_mlp_gemm_in(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
+                  long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
+  constexpr int BMI = 128, BNI = 128, BKI = 64, NT = 256;
+  constexpr int CLD = BNI + 8;
+  constexpr int TILE = 128 * BKI;                               // halves per operand tile (16 KiB)
+  constexpr int LDS_H = 2 * TILE > BMI * CLD ? 2 * TILE : BMI * CLD;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];   // [A (128 x 64) | W (128 x 64)], then C
+  const int z = blockIdx.z;
+  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
+  const int ntn = (N + BNI - 1) / BNI, ntm = (M + BMI - 1) / BMI, nwg = ntn * ntm;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int m0 = (wg / ntn) * BMI, n0 = (wg % ntn) * BNI;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int r = lane & 15, g = lane >> 4;
+  const int fo[2] = {r * BKI + ((g) ^ (r >> 1)) * 8, r * BKI + ((4 + g) ^ (r >> 1)) * 8};
+  // staging: wave w fills A and W rows [32 w, 32 w + 32), 8 rows (1 KiB) per DMA piece
+  const _Float16* pa[4];
+  const _Float16* pw[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 32 + i * 8 + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
+    pa[i] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
+    pw[i] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int jl = min(4, max(0, (N - (n0 + wn) + 15) / 16));   // live 16-column blocks of this wave
+  for (int k0 = 0; k0 < K; k0 += BKI) {
+    const int kh_n = min(2, (K - k0) / 32);                    // K halves in this tile (K % 32 == 0)
+    if (k0 > 0) __syncthreads();                               // the previous tile's reads done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(pa[i] + k0, lds + (wave * 32 + i * 8) * BKI);
+      glds16(pw[i] + k0, lds + TILE + (wave * 32 + i * 8) * BKI);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int kh = 0; kh < kh_n; ++kh) {
+      half8 af[4], bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(lds + TILE + (wn + 16 * j) * BKI + fo[kh]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const half8*>(lds + (wm + 16 * i) * BKI + fo[kh]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < jl)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  stage_out_tile<GELU, CLD, 4>(acc, lds, wm, wn, n0, N, bias, lane);
+  __syncthreads();
+#pragma unroll 4
+  for (int it = 0; it < BMI * BNI / 8 / NT; ++it) {
+    const int idx = tid + it * NT, rl = idx / (BNI / 8), ch = idx % (BNI / 8);
+    const int row = m0 + rl, col = n0 + ch * 8;
+    if (row < M && col < ldc)
+      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(lds + rl * CLD + ch * 8);
   }
 }
 
@@ -260,7 +383,6 @@ __global__ void __launch_bounds__(512, 1)
   constexpr int TILE_A = BMW * BKW, STAGE = TILE_A + BNW * BKW;   // halves: 2 x 32 KiB per stage
   constexpr int CLD = BNW + 8;
   constexpr int LDS_H = 2 * STAGE > BMW * CLD ? 2 * STAGE : BMW * CLD;
-  using f32x4 = __attribute__((ext_vector_type(4))) float;
   __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
@@ -397,22 +519,7 @@ __global__ void __launch_bounds__(512, 1)
   // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
   __syncthreads();
   _Float16* cs = lds;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
-    const bool live = col < N;
-    const float bv = live ? bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rl = wm + 16 * i + 4 * g + e;
-        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
-        if (GELU) v = gelu_fast2(v);
-        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
-        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
-      }
-  }
+  stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
   __syncthreads();
 #pragma unroll 4
   for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
@@ -452,7 +559,6 @@ __global__ void __launch_bounds__(512, 1)
   constexpr int STAGE = 4 * HALF;                // [A row-half 0 | A row-half 1 | W col-half 0 | W col-half 1]
   constexpr int CLD = BNW + 8;
   constexpr int LDS_H = 2 * STAGE > BMW * CLD ? 2 * STAGE : BMW * CLD;
-  using f32x4 = __attribute__((ext_vector_type(4))) float;
   __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
@@ -574,58 +680,13 @@ __global__ void __launch_bounds__(512, 1)
     default: kloop(std::integral_constant<int, 0>{}); break;
   }
   if constexpr (OUT) {   // the fused output layer (no LDS use: the drained stages are not touched)
-    float bv[4], wv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-      bv[j] = col < N ? bias[col] : 0.0f;
-      wv[j] = col < N ? (float)wo[col] : 0.0f;   // dead columns contribute 0
-    }
-    float* Pw = P + (long)(4 * (wg % ntn) + wc) * M;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        f32x2 sacc = {0.0f, 0.0f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv[j]);   // the Linear's fp16 output
-          if (GELU) v = gelu_fast2(v);
-          const f32x2 hq = {(float)(_Float16)v.x, (float)(_Float16)v.y};   // the fp16 activation
-          sacc = __builtin_elementwise_fma(hq, f32x2(wv[j]), sacc);
-        }
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          sacc.x += __shfl_xor(sacc.x, off);
-          sacc.y += __shfl_xor(sacc.y, off);
-        }
-        const int row = m0 + wm + 16 * i + 4 * g + e;
-        if ((lane & 15) == 0) {
-          if (row < M) Pw[row] = sacc.x;
-          if (row + 1 < M) Pw[row + 1] = sacc.y;
-        }
-      }
+    out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
     return;
   }
   // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
   __syncthreads();
   _Float16* cs = lds;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
-    const bool live = col < N;
-    const float bv = live ? bias[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rl = wm + 16 * i + 4 * g + e;
-        f32x2 v = round16(f32x2{acc[i][j][e], acc[i][j][e + 1]} + bv);
-        if (GELU) v = gelu_fast2(v);
-        cs[rl * CLD + cl] = live ? (_Float16)v.x : (_Float16)0.0f;
-        cs[(rl + 1) * CLD + cl] = live ? (_Float16)v.y : (_Float16)0.0f;
-      }
-  }
+  stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
   __syncthreads();
 #pragma unroll 4
   for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
@@ -833,6 +894,8 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   // (DFMI_DNN_WIDE=3, default): 8.72 ms per 65,536-row chunk against k_mlp_gemm's 9.66 (DFMI_DNN_WIDE=0);
   // 1 / 2: the single-group variants, 9.77 / 10.07 ms
   const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 3; }();   // A/B: 256x256x64 kernel for the wide layers
+  // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
+  const bool in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) != 0 : true; }();
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
@@ -881,6 +944,10 @@ void dnn_solve(Ctx& x, const char* rho_field) {
         else
           hipLaunchKernelGGL((k_mlp_gemm_w<true, true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
+      } else if (in_tile && K == 64) {   // the 55 -> 1600 input layer of the 53-species nets
+        hipLaunchKernelGGL((k_mlp_gemm_in<true>), dim3(blocks_for(N, 128) * blocks_for(n, 128), 1, d.nmod), dim3(256), 0,
+                           x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
+                           (long)n * ldc);
       } else {
         hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                            (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);

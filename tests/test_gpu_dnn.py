@@ -218,7 +218,8 @@ def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
 
 def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     """The 256x256x64 wide-layer kernels (DFMI_DNN_WIDE=1 interleaved, 3 ping-pong: staggered wave groups,
-    one-phase half-tile restaging) issue the same MFMA sequence per output as k_mlp_gemm, so the source
+    one-phase half-tile restaging) and the 128x128 input-layer kernel (DFMI_DNN_IN=1, four workgroups per CU)
+    issue the same MFMA sequence per output as k_mlp_gemm, so the source
     terms of 32,768 reacting cells x 52 nets agree bitwise -- a race in a pipeline's LDS reuse would show here
     (128 row tiles x 4 column tiles x 52 nets per launch, every CU busy)."""
     from dfmi.mesh import hex_box
@@ -236,8 +237,11 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     p = np.full(C, 101325.0)
     rho = p / (300.0 * T)
     out = {}
-    for wide in ("0", "1", "3"):
-        monkeypatch.setenv("DFMI_DNN_WIDE", wide)
+    # (DFMI_DNN_WIDE, DFMI_DNN_IN): "0" = k_mlp_gemm for every layer
+    variants = {"0": ("0", "0"), "1": ("1", "1"), "3": ("3", "1")}
+    for wide, (w, i) in variants.items():
+        monkeypatch.setenv("DFMI_DNN_WIDE", w)
+        monkeypatch.setenv("DFMI_DNN_IN", i)
         ctx = Context(0)
         pt = case.default_patch_types(m)
         rows, cols = m.proc_rows_cols()
