@@ -1973,8 +1973,15 @@ __device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, i
   }
 }
 
+// One launch covers the species [s_lo, s_hi) of one pass (pass 2 needs the finished sumYDiffError). The
+// cross-species sums are carried between launches in their output arrays (sumE / dAD, hD, and the boundary
+// fields as before), in species order, so any split is bitwise the single launch. The split is for locality:
+// a thread walking all S species keeps every species' Y / alpha*hai / rhoD of the cells in flight live in L2
+// (2 waves per SIMD: 16k cells per XCD x 53 species x 3 arrays = 20 MB against its 4 MB), so each neighbour
+// value is fetched again by each of the cells that read it; a range of species per launch shrinks that set.
 template <int CH, int WT>
-__global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int8_t* __restrict__ tyY,
+__global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int s_lo, int s_hi, int pass,
+    const int8_t* __restrict__ tyY,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ hai, const double* __restrict__ bhai,
     const double* __restrict__ alpha, const double* __restrict__ balpha, double* __restrict__ sumE,
@@ -1983,10 +1990,17 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
   if (c >= m.C) return;
   const long C = m.C, B = m.B;
+  const int S = s_hi;   // species bound of this launch
   const double ac = alpha[c], vol = m.V[c];
   double se[3] = {0.0, 0.0, 0.0}, dad = 0.0;
+  if (pass == 1) {
+  if (s_lo > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) se[k] = sumE[k * C + c];
+    dad = dAD[c];
+  }
   // pass 1: gradients + laplacians -> sumYDiffError, diffAlphaD; boundary sumYDiffError summed in place
-  for (int s0 = 0; s0 < S; s0 += CH) {
+  for (int s0 = s_lo; s0 < s_hi; s0 += CH) {
     double g[CH][3], lap[CH], yc[CH];
     y_chunk_grad<CH, true, WT>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
     if (gout) {
@@ -2021,11 +2035,19 @@ __global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int S, const int
 #pragma unroll
   for (int k = 0; k < 3; ++k) sumE[k * C + c] = se[k];
   dAD[c] = dad;
+  return;
+  }
   // pass 2: hDiffCorrFlux = sum_i hai_i (rhoD_i grad Y_i - Y_i sumYDiffError) (and on the slots)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) se[k] = sumE[k * C + c];
   double hd[3] = {0.0, 0.0, 0.0};
-  for (int s0 = 0; s0 < S; s0 += CH) {
+  if (s_lo > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hd[k] = hD[k * C + c];
+  }
+  for (int s0 = s_lo; s0 < s_hi; s0 += CH) {
     double g[CH][3], lap[CH], yc[CH];
-    y_chunk_grad<CH, false, WT>(m, tyY, S, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
+    y_chunk_grad<CH, false, WT>(m, tyY, s_hi, s0, c, Y, bY, hai, bhai, alpha, balpha, ac, g, lap, yc);
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -2120,8 +2142,10 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_gen(MeshView m, int S, const
 }
 
 // YEqn in the solver's ELL rows, chunked over species (production path for S > 16)
+// One launch covers the species [s_lo, s_hi) (the species are independent here; split for L2 locality of the
+// neighbour rhoD gathers, as k_y_prep_gen)
 template <int CH, int WT>
-__global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, const int8_t* __restrict__ tyY, int inert,
+__global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int s_lo, int S, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
@@ -2133,7 +2157,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell_gen(MeshView m, int S, c
   const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
   const long C = m.C, B = m.B;
   const double vol = m.V[c];
-  for (int s0 = 0; s0 < S; s0 += CH) {
+  for (int s0 = s_lo; s0 < S; s0 += CH) {
     double d1 = 0.0, d2 = 0.0;
     double dL[CH], rc[CH];
 #pragma unroll
@@ -2348,8 +2372,15 @@ bool gen_rows(const Ctx& x) {
   const char* e = std::getenv("DFMI_GEN_ROWS");
   return face_rows(x) && e && std::atoi(e) != 0;
 }
+// the chunked kernels walk the CSR face lists on hex boxes too: 2M cells x 53 species, y_assemble_ell 4.43
+// against 5.84 ms per step by the computed hex walk (its 179 VGPRs: two waves per SIMD), y_prep 8.61 against
+// 8.71 (scripts/c4_ab.sh); DFMI_GEN_HEX=1 for the hex walk
+bool gen_hex(const Ctx& x) {
+  const char* e = std::getenv("DFMI_GEN_HEX");
+  return face_hex(x) && e && std::atoi(e) != 0;
+}
 #define LAUNCH_SWG(kern, NS, n, ...) \
-  do { if (face_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (gen_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
+  do { if (gen_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (gen_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
        else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
 #define LAUNCH_SW(kern, NS, n, ...) \
   do { if (face_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
@@ -2675,10 +2706,20 @@ void y_prep(Ctx& x) {
              x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
              gout);                                                                                                  \
   } while (0)
-#define GEN(CH) LAUNCH_SWG(k_y_prep_gen, CH, x.C, m, x.S, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),     \
-                       x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
-                       x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                  \
-                       x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout)
+  // the chunked kernel in species ranges of DFMI_YPREP_LCH species per launch (default 8; 0: all in one), pass 1
+  // over every range, then pass 2 (it reads the finished sumYDiffError)
+  const char* elch = std::getenv("DFMI_YPREP_LCH");
+  const int lch_req = elch ? std::atoi(elch) : 8;
+#define GEN(CH)                                                                                                      \
+  do {                                                                                                               \
+    const int lch = lch_req > 0 ? std::max(CH, lch_req / CH * CH) : x.S;                                            \
+    for (int pass = 1; pass <= 2; ++pass)                                                                            \
+      for (int s_lo = 0; s_lo < x.S; s_lo += lch)                                                                    \
+        LAUNCH_SWG(k_y_prep_gen, CH, x.C, m, s_lo, std::min(x.S, s_lo + lch), pass, x.st("Y"), x.f("Y"),             \
+                   x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), \
+                   x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),  \
+                   x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), pass == 1 ? gout : nullptr);                   \
+  } while (0)
   // DFMI_YPREP_CH=2|3|4|8: species per chunk of the chunked kernel (default 4 for S > 16; set, it also
   // replaces the full-S kernels of S <= 16, an A/B knob)
   const char* ech = std::getenv("DFMI_YPREP_CH");
@@ -2730,9 +2771,18 @@ void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs
                 x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                             \
                 x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1)); \
   } while (0)
-#define GEN(CH) LAUNCH_SWG(k_y_assemble_ell_gen, CH, x.C, m, x.S, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), \
-                       x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),     \
-                       x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
+  // species ranges of DFMI_YASM_LCH species per launch (default 8; 0: all in one launch)
+  const char* elch = std::getenv("DFMI_YASM_LCH");
+  const int lch_req = elch ? std::atoi(elch) : 8;
+#define GEN(CH)                                                                                                      \
+  do {                                                                                                               \
+    const int lch = lch_req > 0 ? std::max(CH, lch_req / CH * CH) : x.S;                                            \
+    for (int s_lo = 0; s_lo < x.S; s_lo += lch)                                                                      \
+      LAUNCH_SWG(k_y_assemble_ell_gen, CH, x.C, m, s_lo, std::min(x.S, s_lo + lch), x.st("Y"), x.inert, x.f("Y"),    \
+                 x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), \
+                 x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"),       \
+                 x.sch_w(0), x.sch_w(1));                                                                            \
+  } while (0)
   const char* ech = std::getenv("DFMI_YASM_CH");   // species per chunk, A/B knob (default 8)
   const int ch = ech ? std::atoi(ech) : 8;
   DFMI_SWITCH_S(x.S, CALL, if (ch == 4) GEN(4); else GEN(8))

@@ -106,7 +106,7 @@ def _oracle(m, t, st, pt, inert, dt):
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
                                         "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
-                                        "mixed", "mixed-generic", "walls-trav", "burke9-zm", "walls-zm"])
+                                        "mixed", "mixed-generic", "walls-trav", "burke9-zm", "walls-zm", "gri53-walls-split"])
 def periodic(request):
     zm = request.param.endswith("-zm")      # the z-marching YEqn kernels (A/B path, 16 x 16 column tiles)
     if zm:
@@ -120,8 +120,12 @@ def periodic(request):
     if request.param.endswith("-csr"):     # face loops by the CSR walk instead of the gather rows
         os.environ["DFMI_FACE_CSR"] = "1"
         request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
+    if request.param.endswith("-split"):   # other species ranges per launch of the chunked YEqn kernels
+        for k, v in (("DFMI_YPREP_LCH", "4"), ("DFMI_YASM_LCH", "16")):
+            os.environ[k] = v
+            request.addfinalizer(lambda k=k: os.environ.pop(k, None))
     traversal = request.param.endswith("-trav")
-    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "").replace("-zm", "")
+    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "").replace("-zm", "").replace("-split", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
