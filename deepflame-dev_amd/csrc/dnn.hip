@@ -62,17 +62,17 @@ __device__ __forceinline__ f32x2 round16(f32x2 v) { return __builtin_convertvect
 
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
-// GEMM epilogue shared by the kernels below, for one wave's 16 NI x 64 accumulator tile (NI x 4 blocks of 16 x 16,
+// GEMM epilogue shared by the kernels below, for one wave's 16 NI x 16 NJ accumulator tile (NI x NJ blocks of 16 x 16,
 // C/D map col = lane & 15, row = 4 (lane >> 4) + e) at tile-local rows wm.., columns wn.. of the N tile at n0:
 // bias + GELU, rounded to fp16, into the LDS output tile cs (row stride CLD). 16-column blocks wholly past N (the
 // padded tail of the last N tile: 224 of the 1,024 columns of an 800-wide layer) are written as zeros without
 // evaluating the GELU -- a wave-uniform test; the GELU is the epilogue's whole cost.
-template <bool GELU, int CLD, int NI = 8>
-__device__ __forceinline__ void stage_out_tile(const f32x4 (&acc)[NI][4], _Float16* cs, int wm, int wn, int n0, int N,
+template <bool GELU, int CLD, int NI = 8, int NJ = 4>
+__device__ __forceinline__ void stage_out_tile(const f32x4 (&acc)[NI][NJ], _Float16* cs, int wm, int wn, int n0, int N,
                                                const float* __restrict__ bias, int lane) {
   const int g = lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int cl = wn + 16 * j + (lane & 15), col = n0 + cl;
     if (n0 + wn + 16 * j >= N) {
 #pragma unroll
@@ -549,21 +549,31 @@ __global__ void __launch_bounds__(512, 1)
 // epilogue as in k_mlp_gemm -- per row, the products with wo over each wave's 64 columns, summed over the
 // lane's four 16-column blocks and a 16-lane xor tree, written as partial P[z][4 tile_n + wave_n][M]: the
 // same 64-column groups in the same order as k_mlp_gemm's two 64-column partials per 128-wide tile.
-template <bool GELU, bool OUT = false>
+//
+// TAIL (N = 256 q + t, 0 < t <= 32: the 800-wide layer): q column tiles instead of q + 1, the last one also
+// computing the t tail columns as a 256 x 32 strip -- wave (wr, wc) owns its rows 32 wc.. of the strip (2 x 2
+// MFMA blocks, 8 MFMAs per K tile). Its A fragments are the ones the wave already holds for that half of its rows
+// (phase 0 for wc < 2, phase 2 otherwise); its W rows (32 x 64 per K tile) are staged by waves 0-3 (one DMA
+// piece each, with A row-half 1 at phase 3: the strip's reads end in phase 2) into a 4 KiB slot per stage.
+// A 32-column tile of its own streams all of A for 1/8 of a tile's MFMAs (63 % of a full tile's time).
+template <bool GELU, bool OUT = false, bool TAIL = false>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                   long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
                   const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0) {
-  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512;
+  static_assert(!(OUT && TAIL), "the fused output layer has no tail strip");
+  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512, TW = 32;
   constexpr int HALF = 128 * BKW;                // halves (fp16 elements) per half-tile: 16 KiB
   constexpr int STAGE = 4 * HALF;                // [A row-half 0 | A row-half 1 | W col-half 0 | W col-half 1]
-  constexpr int CLD = BNW + 8;
-  constexpr int LDS_H = 2 * STAGE > BMW * CLD ? 2 * STAGE : BMW * CLD;
+  constexpr int TSLOT = TW * BKW;                // tail W rows per stage (4 KiB), after the two stages
+  constexpr int CLD = BNW + (TAIL ? TW : 0) + 8;
+  constexpr int LDS_IN = 2 * STAGE + (TAIL ? 2 * TSLOT : 0);
+  constexpr int LDS_H = LDS_IN > BMW * CLD ? LDS_IN : BMW * CLD;
   __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
   if constexpr (OUT) { wo += z * swo; P += z * sP; }
-  const int ntn = (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
+  const int ntn = TAIL ? N / BNW : (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
   const int orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
@@ -592,6 +602,14 @@ __global__ void __launch_bounds__(512, 1)
     glds16(src[h][0] + k0, d);
     glds16(src[h][1] + k0, d + 8 * BKW);
   };
+  // tail strip W rows: wave w < 4 stages rows 8 w .. 8 w + 7 (clamped to N - 1: dead columns masked on store)
+  const int nt0 = ntn * BNW;
+  const _Float16* tsrc;
+  {
+    const int trow = 8 * (wave & 3) + (lane >> 3), ch = (lane & 7) ^ ((trow >> 1) & 7);
+    tsrc = W + (long)min(nt0 + trow, N - 1) * K + ch * 8;
+  }
+  auto stage_tail = [&](int buf, int k0) { glds16(tsrc + k0, lds + 2 * STAGE + buf * TSLOT + 8 * (wave & 3) * BKW); };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -614,9 +632,35 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) bf[jb][kh] = *reinterpret_cast<const half8*>(s0 + jb * 16 * BKW + fo[kh]);
   };
+  f32x4 acct[2][2];   // the tail strip: rows 32 wc + 16 ib of the wave's 128, columns 16 jb of the strip
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acct[i][0] = acct[i][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  half8 bt[2][2];
+  auto read_bt = [&](int buf) {
+    const _Float16* s0 = lds + 2 * STAGE + buf * TSLOT;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) bt[jb][kh] = *reinterpret_cast<const half8*>(s0 + jb * 16 * BKW + fo[kh]);
+  };
   const int nk = K / BKW;
-  auto kloop = [&](auto jl_c) {
+  auto kloop = [&](auto jl_c, auto tail_c) {
     constexpr int JL = decltype(jl_c)::value;
+    constexpr bool TT = decltype(tail_c)::value;   // this tile computes the tail strip
+    auto tail_from = [&](auto o_c) {   // rows of the strip in af[O + ib], O = 2 (wc & 1); K half outer
+      constexpr int O = decltype(o_c)::value;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int ib = 0; ib < 2; ++ib)
+            acct[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[O + ib][kh], bt[jb][kh], acct[ib][jb], 0, 0, 0);
+    };
+    auto tail_mfmas = [&]() {
+      if (wc & 1) tail_from(std::integral_constant<int, 2>{});
+      else tail_from(std::integral_constant<int, 0>{});
+    };
     auto quad = [&](int ih, int jh) {   // 16 MFMAs, K half outer so that dependent MFMAs are 8 apart
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -631,21 +675,35 @@ __global__ void __launch_bounds__(512, 1)
       __builtin_amdgcn_s_setprio(0);
     };
     // one phase: fragment reads and one half-tile's DMA, own reads retired, barrier, MFMAs, barrier
-    auto sync_mfma = [&](int ih, int jh) {
+    // tail strip of the half ih: the waves whose strip rows lie in it (wc < 2: half 0, else half 1)
+    auto sync_mfma = [&](int ih, int jh, bool tail) {
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this phase's reads retired before its first barrier
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       quad(ih, jh);
+      if constexpr (TT) {
+        if (tail) {
+          __builtin_amdgcn_s_setprio(1);
+          tail_mfmas();
+          __builtin_amdgcn_s_setprio(0);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
+    const bool tw0 = TT && wc < 2, tw1 = TT && wc >= 2, tstage = TT && wr == 0;
     __builtin_amdgcn_s_waitcnt(0xC07F);   // no scalar load outstanding into the loop
-    // prologue: tile 0 complete, tile 1's A0 B1 A1 in flight (the steady-state issue order)
+    // prologue: tile 0 complete, tile 1's A0 B1 A1 in flight (the steady-state issue order); the tail strip's
+    // W rows of tile 0 with tile 0, of tile 1 after tile 1's A0 (as in the loop: one more piece in flight)
     const int k1 = min(1, nk - 1) * BKW;
     stage_half(0, 0, 0); stage_half(0, 3, 0); stage_half(0, 1, 0); stage_half(0, 2, 0);
-    stage_half(1, 0, k1); stage_half(1, 3, k1); stage_half(1, 1, k1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (tstage) stage_tail(0, 0);
+    stage_half(1, 0, k1);
+    if (tstage) stage_tail(1, k1);
+    stage_half(1, 3, k1); stage_half(1, 1, k1);
+    if (tstage) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();   // the stagger: waves 4-7 run one barrier behind
     __builtin_amdgcn_sched_barrier(0);
@@ -655,29 +713,42 @@ __global__ void __launch_bounds__(512, 1)
       read_b(b, 0);
       __builtin_amdgcn_sched_barrier(0);
       read_a(b, 0);
+      if (tw0) read_bt(b);
       stage_half(b ^ 1, 2, kn);          // W col-half 0 of tile t+1 (its slot's last read: tile t-1, phase 3)
-      sync_mfma(0, 0);
+      sync_mfma(0, 0, tw0);
       read_b(b, 1);
       stage_half(b, 0, k2);              // A row-half 0 of tile t+2 (last read: phase 0)
-      sync_mfma(0, 1);
+      sync_mfma(0, 1, false);
       read_a(b, 1);
+      if (tw1) read_bt(b);
       stage_half(b, 3, k2);              // W col-half 1 of tile t+2 (last read: phase 1)
-      sync_mfma(1, 1);
+      sync_mfma(1, 1, tw1);
       read_b(b, 0);
       stage_half(b, 1, k2);              // A row-half 1 of tile t+2 (last read: phase 2)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t+1 landed (t+2's first three halves in flight)
-      sync_mfma(1, 0);
+      if (tstage) {
+        stage_tail(b, k2);               // the strip's W rows of tile t+2 (last read: phase 2)
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t+1 landed (t+2's first three halves in flight)
+      }
+      sync_mfma(1, 0, false);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();   // both groups end on the same barrier count
     __builtin_amdgcn_s_waitcnt(0);              // the re-staging DMAs past the last tile drained
   };
   const int wm = wr * 128, wn = wc * 64;
-  switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
-    case 4: kloop(std::integral_constant<int, 4>{}); break;
-    case 3: kloop(std::integral_constant<int, 3>{}); break;
-    case 2: kloop(std::integral_constant<int, 2>{}); break;
-    case 1: kloop(std::integral_constant<int, 1>{}); break;
-    default: kloop(std::integral_constant<int, 0>{}); break;
+  const bool tail_tile = TAIL && wg % ntn == ntn - 1;
+  if constexpr (TAIL) {   // every main tile is full
+    if (tail_tile) kloop(std::integral_constant<int, 4>{}, std::true_type{});
+    else kloop(std::integral_constant<int, 4>{}, std::false_type{});
+  } else {
+    switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
+      case 4: kloop(std::integral_constant<int, 4>{}, std::false_type{}); break;
+      case 3: kloop(std::integral_constant<int, 3>{}, std::false_type{}); break;
+      case 2: kloop(std::integral_constant<int, 2>{}, std::false_type{}); break;
+      case 1: kloop(std::integral_constant<int, 1>{}, std::false_type{}); break;
+      default: kloop(std::integral_constant<int, 0>{}, std::false_type{}); break;
+    }
   }
   if constexpr (OUT) {   // the fused output layer (no LDS use: the drained stages are not touched)
     out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
@@ -687,13 +758,27 @@ __global__ void __launch_bounds__(512, 1)
   __syncthreads();
   _Float16* cs = lds;
   stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
+  if (tail_tile) stage_out_tile<GELU, CLD, 2, 2>(acct, cs, wm + 32 * wc, BNW, n0, N, bias, lane);
   __syncthreads();
+  if (!tail_tile) {
 #pragma unroll 4
-  for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
-    const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
-    const int row = m0 + rl, col = n0 + ch * 8;
-    if (row < M && col < ldc)
-      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+    for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
+      const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
+      const int row = m0 + rl, col = n0 + ch * 8;
+      if (row < M && col < ldc)
+        *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+    }
+  } else {   // the tile, the strip, and zeros for the padding columns up to ldc (at most 64 past the strip)
+    constexpr int NCH = (BNW + TW + 32) / 8;
+    for (int idx = tid; idx < BMW * NCH; idx += NT) {
+      const int rl = idx / NCH, ch = idx % NCH;
+      const int row = m0 + rl, col = n0 + ch * 8;
+      if (row < M && col < ldc) {
+        half8 v = {};
+        if (ch * 8 < BNW + TW) v = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+        *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = v;
+      }
+    }
   }
 }
 
@@ -894,6 +979,7 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   // (DFMI_DNN_WIDE=3, default): 8.72 ms per 65,536-row chunk against k_mlp_gemm's 9.66 (DFMI_DNN_WIDE=0);
   // 1 / 2: the single-group variants, 9.77 / 10.07 ms
   const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 3; }();   // A/B: 256x256x64 kernel for the wide layers
+  const bool tail_strip = [] { const char* e = std::getenv("DFMI_DNN_TAIL"); return e ? std::atoi(e) != 0 : true; }();
   // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
   const bool in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) != 0 : true; }();
   // activation buffers for one chunk: ping-pong [module][chunk][width]
@@ -935,7 +1021,14 @@ void dnn_solve(Ctx& x, const char* rho_field) {
                              d.part.p, sP);
       } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
-        if (wide == 3)
+        // N = 256 q + t, 0 < t <= 32 (the 800-wide layer): q tiles, the last with the t-column strip
+        // (DFMI_DNN_TAIL=1, default; 0: a (q+1)-th tile)
+        const bool tail = tail_strip && N % 256 != 0 && N % 256 <= 32 && ldc <= N / 256 * 256 + 64;
+        if (wide == 3 && tail)
+          hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, true>), dim3(N / 256 * blocks_for(n, 256), 1, d.nmod), dim3(512),
+                             0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
+                             (long)n * ldc, nullptr, 0L, nullptr, 0L);
+        else if (wide == 3)
           hipLaunchKernelGGL((k_mlp_gemm_pp<true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
         else if (wide == 2)
