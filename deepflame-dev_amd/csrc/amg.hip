@@ -746,20 +746,25 @@ void global_setup(Ctx& x, const std::vector<int>& col0, const std::vector<std::v
     }
   }
   // external couplings of each local coarsest row: (peer, peer's coarsest id) -> level-0 ELL sources k C + c
+  // (a rank-local inconsistency is agreed on in the next all-gather, so every rank throws together instead of
+  // the others blocking in a collective the failed rank never joins)
   std::vector<std::map<std::pair<int, int>, std::vector<int>>> ext(nloc);
+  bool bad = false;
   for (int c = 0; c < C; ++c)
     for (int k = 0; k < W0; ++k) {
       const int j = col0[(size_t)k * C + c];
       if (j < C) continue;
       const int h = j - C;
-      DFMI_CHECK(hpeer[h] >= 0 && ids[j] >= 0, "AMG: processor face without a peer aggregate");
+      if (!(hpeer[h] >= 0 && ids[j] >= 0)) { bad = true; continue; }
       ext[cid[c]][{hpeer[h], (int)ids[j]}].push_back(k * C + c);
     }
   int wext = 0;
   for (auto& e : ext) wext = std::max(wext, (int)e.size());
   {
-    const std::vector<double> all = gather({(double)wext});
-    for (int r = 0; r < R; ++r) we = std::max(we, (int)all[r]);
+    const std::vector<double> all = gather({(double)wext, bad ? 1.0 : 0.0});
+    bool any_bad = false;
+    for (int r = 0; r < R; ++r) { we = std::max(we, (int)all[2 * r]); any_bad = any_bad || all[2 * r + 1] != 0.0; }
+    DFMI_CHECK(!any_bad, "AMG: processor face without a peer aggregate (on some rank)");
   }
   const int ng = R * nmax, wg = wc + we;
   if (ng > COARSEST || (size_t)ng * wg > LDS_ENT) return;   // the same decision on every rank
