@@ -861,29 +861,43 @@ __global__ void k_dnn_input(int n, int C, int S, int Kp, const int* __restrict__
 }
 
 // output layer (K -> 1) of every net + calculate_y_new + calculate_RR
-__global__ void k_dnn_output(int n, int C, int S, int nq, int nmod, const int* __restrict__ idx,
+// one workgroup per 64 reacting cells, 8 waves: wave g evaluates species g, g + 8, ... of the 64 cells (coalesced
+// partial-sum reads across the cells), the renormalising sum runs over the species in order by wave 0 (the
+// sequential sum of the one-thread-per-cell form, bitwise; that form ran one wave per SIMD -- 1,024 waves for a
+// 65,536-row chunk -- and kept yn[] in scratch: 270 us per chunk)
+constexpr int OG = 8;
+__global__ void __launch_bounds__(64 * OG) k_dnn_output(int n, int C, int S, int nq, int nmod, const int* __restrict__ idx,
                              const float* __restrict__ P, long sP, const float* __restrict__ b,
                              const double* __restrict__ Ymu, const double* __restrict__ Ystd,
                              const double* __restrict__ Y, const double* __restrict__ rho,
                              const double* __restrict__ p, double dt, double* __restrict__ RR) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int c = idx[i];
-  double yn[63];
-  double sum = 0.0;
-  for (int m = 0; m < nmod; ++m) {
-    float a = 0.0f;
-    for (int q = 0; q < nq; ++q) a += P[m * sP + (long)q * n + i];   // the GEMM's partial dot products, in order
-    const double out = (double)(_Float16)(a + b[m]);   // the net's fp16 output, as .to(kDouble)
-    const double ybct = (pow(Y[(long)m * C + c], 0.1) - 1.0) * 10.0;
-    const double v = out * Ystd[m] + Ymu[m] + ybct;
-    yn[m] = pow(v * 0.1 + 1.0, 10.0);
-    sum += yn[m];
+  __shared__ double syn[64][64], ssum[64];   // [species][cell]; nmod <= 63
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cl;
+  const bool live = i < n;
+  const int c = live ? idx[i] : 0;
+  if (live)
+    for (int m = g; m < nmod; m += OG) {
+      float a = 0.0f;
+      for (int q = 0; q < nq; ++q) a += P[m * sP + (long)q * n + i];   // the GEMM's partial dot products, in order
+      const double out = (double)(_Float16)(a + b[m]);   // the net's fp16 output, as .to(kDouble)
+      const double ybct = (pow(Y[(long)m * C + c], 0.1) - 1.0) * 10.0;
+      const double v = out * Ystd[m] + Ymu[m] + ybct;
+      syn[m][cl] = pow(v * 0.1 + 1.0, 10.0);
+    }
+  __syncthreads();
+  if (g == 0 && live) {
+    double sum = 0.0;
+    for (int m = 0; m < nmod; ++m) sum += syn[m][cl];
+    ssum[cl] = sum + Y[(long)(S - 1) * C + c];
   }
-  sum += Y[(long)(S - 1) * C + c];
-  for (int m = 0; m < nmod; ++m) {
-    const double y = yn[m] / sum;
-    RR[(long)m * C + c] = (y - Y[(long)m * C + c]) * rho[c] * (p[c] / 101325.0) / dt;
+  __syncthreads();
+  if (live) {
+    const double rc = rho[c], pc = p[c] / 101325.0, sum = ssum[cl];
+    for (int m = g; m < nmod; m += OG) {
+      const double y = syn[m][cl] / sum;
+      RR[(long)m * C + c] = (y - Y[(long)m * C + c]) * rc * pc / dt;
+    }
   }
 }
 
@@ -1051,7 +1065,7 @@ void dnn_solve(Ctx& x, const char* rho_field) {
       lda = ldc;
     }
     KScope _ks(x, "k_dnn_output");
-    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 256)), dim3(256), 0, x.stream, n, C, S, nq, d.nmod, idx,
+    hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 64)), dim3(64 * OG), 0, x.stream, n, C, S, nq, d.nmod, idx,
                        d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f(rho_field), x.f("p"), d.dt, RR);
     DFMI_HIP(hipGetLastError());
   }
