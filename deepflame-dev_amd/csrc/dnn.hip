@@ -550,22 +550,23 @@ __global__ void __launch_bounds__(512, 1)
 // lane's four 16-column blocks and a 16-lane xor tree, written as partial P[z][4 tile_n + wave_n][M]: the
 // same 64-column groups in the same order as k_mlp_gemm's two 64-column partials per 128-wide tile.
 //
-// TAIL (N = 256 q + t, 0 < t <= 32: the 800-wide layer): q column tiles instead of q + 1, the last one also
-// computing the t tail columns as a 256 x 32 strip -- wave (wr, wc) owns its rows 32 wc.. of the strip (2 x 2
-// MFMA blocks, 8 MFMAs per K tile). Its A fragments are the ones the wave already holds for that half of its rows
-// (phase 0 for wc < 2, phase 2 otherwise); its W rows (32 x 64 per K tile) are staged by waves 0-3 (one DMA
-// piece each, with A row-half 1 at phase 3: the strip's reads end in phase 2) into a 4 KiB slot per stage.
+// TS > 0 (N = 256 q + t, 0 < t <= 32: the 800-wide layer): q column tiles instead of q + 1, the last 32 / TS of
+// them also computing TS of the tail columns as a 256 x TS strip -- wave (wr, wc) owns its rows 32 wc.. of the
+// strip (2 x TS/16 MFMA blocks). Its A fragments are the ones the wave already holds for that half of its rows
+// (phase 0 for wc < 2, phase 2 otherwise); its W rows (TS x 64 per K tile) are staged by waves 0 .. TS/8 - 1 (one
+// DMA piece each, with A row-half 1 at phase 3: the strip's reads end in phase 2) into a slot per stage.
 // A 32-column tile of its own streams all of A for 1/8 of a tile's MFMAs (63 % of a full tile's time).
-template <bool GELU, bool OUT = false, bool TAIL = false>
+template <bool GELU, bool OUT = false, int TS = 0>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                   long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
                   const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0) {
-  static_assert(!(OUT && TAIL), "the fused output layer has no tail strip");
-  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512, TW = 32;
+  constexpr bool TAIL = TS > 0;
+  static_assert(!(OUT && TAIL) && (TS == 0 || TS == 16 || TS == 32), "tail strips: 16 or 32 columns, no OUT");
+  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512, TW = TS, NJT = TS / 16, NSTRIP = TAIL ? 32 / TS : 0;
   constexpr int HALF = 128 * BKW;                // halves (fp16 elements) per half-tile: 16 KiB
   constexpr int STAGE = 4 * HALF;                // [A row-half 0 | A row-half 1 | W col-half 0 | W col-half 1]
-  constexpr int TSLOT = TW * BKW;                // tail W rows per stage (4 KiB), after the two stages
+  constexpr int TSLOT = TW * BKW;                // tail W rows per stage (TS x 128 B), after the two stages
   constexpr int CLD = BNW + (TAIL ? TW : 0) + 8;
   constexpr int LDS_IN = 2 * STAGE + (TAIL ? 2 * TSLOT : 0);
   constexpr int LDS_H = LDS_IN > BMW * CLD ? LDS_IN : BMW * CLD;
@@ -602,12 +603,13 @@ __global__ void __launch_bounds__(512, 1)
     glds16(src[h][0] + k0, d);
     glds16(src[h][1] + k0, d + 8 * BKW);
   };
-  // tail strip W rows: wave w < 4 stages rows 8 w .. 8 w + 7 (clamped to N - 1: dead columns masked on store)
-  const int nt0 = ntn * BNW;
+  // this tile's strip (the last NSTRIP tiles: strip si at columns nt0 + TS si); its W rows: wave w < TS / 8
+  // stages rows 8 w .. 8 w + 7 (clamped to N - 1: dead columns masked on store)
+  const int nt0 = ntn * BNW, si = TAIL ? wg % ntn - (ntn - NSTRIP) : -1, so = nt0 + TS * si;
   const _Float16* tsrc;
   {
     const int trow = 8 * (wave & 3) + (lane >> 3), ch = (lane & 7) ^ ((trow >> 1) & 7);
-    tsrc = W + (long)min(nt0 + trow, N - 1) * K + ch * 8;
+    tsrc = W + (long)min(max(so, 0) + trow, N - 1) * K + ch * 8;
   }
   auto stage_tail = [&](int buf, int k0) { glds16(tsrc + k0, lds + 2 * STAGE + buf * TSLOT + 8 * (wave & 3) * BKW); };
   f32x4 acc[8][4];
@@ -632,14 +634,17 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) bf[jb][kh] = *reinterpret_cast<const half8*>(s0 + jb * 16 * BKW + fo[kh]);
   };
-  f32x4 acct[2][2];   // the tail strip: rows 32 wc + 16 ib of the wave's 128, columns 16 jb of the strip
+  constexpr int NJ1 = NJT > 0 ? NJT : 1;
+  f32x4 acct[2][NJ1];   // the tail strip: rows 32 wc + 16 ib of the wave's 128, columns 16 jb of the strip
 #pragma unroll
-  for (int i = 0; i < 2; ++i) acct[i][0] = acct[i][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  half8 bt[2][2];
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ1; ++j) acct[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  half8 bt[NJ1][2];
   auto read_bt = [&](int buf) {
     const _Float16* s0 = lds + 2 * STAGE + buf * TSLOT;
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
+    for (int jb = 0; jb < NJT; ++jb)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) bt[jb][kh] = *reinterpret_cast<const half8*>(s0 + jb * 16 * BKW + fo[kh]);
   };
@@ -652,7 +657,7 @@ __global__ void __launch_bounds__(512, 1)
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < NJT; ++jb)
 #pragma unroll
           for (int ib = 0; ib < 2; ++ib)
             acct[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[O + ib][kh], bt[jb][kh], acct[ib][jb], 0, 0, 0);
@@ -692,7 +697,7 @@ __global__ void __launch_bounds__(512, 1)
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
-    const bool tw0 = TT && wc < 2, tw1 = TT && wc >= 2, tstage = TT && wr == 0;
+    const bool tw0 = TT && wc < 2, tw1 = TT && wc >= 2, tstage = TT && wave < TS / 8;
     __builtin_amdgcn_s_waitcnt(0xC07F);   // no scalar load outstanding into the loop
     // prologue: tile 0 complete, tile 1's A0 B1 A1 in flight (the steady-state issue order); the tail strip's
     // W rows of tile 0 with tile 0, of tile 1 after tile 1's A0 (as in the loop: one more piece in flight)
@@ -737,7 +742,7 @@ __global__ void __launch_bounds__(512, 1)
     __builtin_amdgcn_s_waitcnt(0);              // the re-staging DMAs past the last tile drained
   };
   const int wm = wr * 128, wn = wc * 64;
-  const bool tail_tile = TAIL && wg % ntn == ntn - 1;
+  const bool tail_tile = TAIL && si >= 0;
   if constexpr (TAIL) {   // every main tile is full
     if (tail_tile) kloop(std::integral_constant<int, 4>{}, std::true_type{});
     else kloop(std::integral_constant<int, 4>{}, std::false_type{});
@@ -758,24 +763,26 @@ __global__ void __launch_bounds__(512, 1)
   __syncthreads();
   _Float16* cs = lds;
   stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
-  if (tail_tile) stage_out_tile<GELU, CLD, 2, 2>(acct, cs, wm + 32 * wc, BNW, n0, N, bias, lane);
+  if constexpr (TAIL)
+    if (tail_tile) stage_out_tile<GELU, CLD, 2, NJT>(acct, cs, wm + 32 * wc, BNW, so - BNW, N, bias, lane);
   __syncthreads();
-  if (!tail_tile) {
 #pragma unroll 4
-    for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
-      const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
-      const int row = m0 + rl, col = n0 + ch * 8;
-      if (row < M && col < ldc)
-        *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
-    }
-  } else {   // the tile, the strip, and zeros for the padding columns up to ldc (at most 64 past the strip)
-    constexpr int NCH = (BNW + TW + 32) / 8;
+  for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
+    const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
+    const int row = m0 + rl, col = n0 + ch * 8;
+    if (row < M && col < ldc)
+      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+  }
+  if (tail_tile) {   // the strip, and (last tile) zeros for the padding columns nt0 + 32 .. ldc (at most 32)
+    constexpr int NSC = TS / 8, NCH = NSC + 4;
+    const bool last = si == NSTRIP - 1;
     for (int idx = tid; idx < BMW * NCH; idx += NT) {
       const int rl = idx / NCH, ch = idx % NCH;
-      const int row = m0 + rl, col = n0 + ch * 8;
+      if (ch >= NSC && !last) continue;
+      const int row = m0 + rl, col = ch < NSC ? so + ch * 8 : nt0 + 32 + (ch - NSC) * 8;
       if (row < M && col < ldc) {
         half8 v = {};
-        if (ch * 8 < BNW + TW) v = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
+        if (ch < NSC) v = *reinterpret_cast<const half8*>(cs + rl * CLD + BNW + ch * 8);
         *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = v;
       }
     }
@@ -993,7 +1000,13 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   // (DFMI_DNN_WIDE=3, default): 8.72 ms per 65,536-row chunk against k_mlp_gemm's 9.66 (DFMI_DNN_WIDE=0);
   // 1 / 2: the single-group variants, 9.77 / 10.07 ms
   const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 3; }();   // A/B: 256x256x64 kernel for the wide layers
-  const bool tail_strip = [] { const char* e = std::getenv("DFMI_DNN_TAIL"); return e ? std::atoi(e) != 0 : true; }();
+  // tail strips of N = 256 q + t (t <= 32) layers: DFMI_DNN_TAIL=16 (default: two 16-column strips in the last two
+  // tiles), 32 (one strip in the last tile; 1 means 32), 0 (a (q+1)-th tile)
+  const int tail_strip = [] {
+    const char* e = std::getenv("DFMI_DNN_TAIL");
+    const int v = e ? std::atoi(e) : 16;
+    return v == 1 ? 32 : (v == 16 || v == 32 ? v : 0);
+  }();
   // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
   const bool in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) != 0 : true; }();
   // activation buffers for one chunk: ping-pong [module][chunk][width]
@@ -1035,13 +1048,16 @@ void dnn_solve(Ctx& x, const char* rho_field) {
                              d.part.p, sP);
       } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
-        // N = 256 q + t, 0 < t <= 32 (the 800-wide layer): q tiles, the last with the t-column strip
-        // (DFMI_DNN_TAIL=1, default; 0: a (q+1)-th tile)
-        const bool tail = tail_strip && N % 256 != 0 && N % 256 <= 32 && ldc <= N / 256 * 256 + 64;
-        if (wide == 3 && tail)
-          hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, true>), dim3(N / 256 * blocks_for(n, 256), 1, d.nmod), dim3(512),
-                             0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
-                             (long)n * ldc, nullptr, 0L, nullptr, 0L);
+        // N = 256 q + t, 0 < t <= 32 (the 800-wide layer): q tiles, the last one or two with the tail strips
+        const bool tail = tail_strip > 0 && N % 256 != 0 && N % 256 <= 32 && ldc <= N / 256 * 256 + 64 &&
+                          N / 256 >= 32 / tail_strip;
+        const dim3 gt(N / 256 * blocks_for(n, 256), 1, d.nmod);
+        if (wide == 3 && tail && tail_strip == 16)
+          hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, 16>), gt, dim3(512), 0, x.stream, n, N, K, in, lda, sIn,
+                             d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
+        else if (wide == 3 && tail)
+          hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, 32>), gt, dim3(512), 0, x.stream, n, N, K, in, lda, sIn,
+                             d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
         else if (wide == 3)
           hipLaunchKernelGGL((k_mlp_gemm_pp<true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
