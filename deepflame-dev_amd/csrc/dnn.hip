@@ -293,15 +293,16 @@ __global__ void __launch_bounds__(256, 2)
 // (2 x 2) of 64 x 64 (4 x 4 MFMA blocks), the whole K staged by DMA at once (A and W 128 rows x 128 B each,
 // rows swizzled as in k_mlp_gemm_w), then the output tile staged through the same LDS (35 KiB) and written as
 // 16-B row chunks. Same MFMA order per output as k_mlp_gemm (K halves in order), so the same results.
-template <bool GELU>
-__global__ void __launch_bounds__(256, 4)
+template <bool GELU, int BMI>
+__global__ void __launch_bounds__(256, BMI == 64 ? 6 : 4)
     k_mlp_gemm_in(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                   long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
-  constexpr int BMI = 128, BNI = 128, BKI = 64, NT = 256;
+  // BMI = 128: 4 waves (2 x 2) of 64 x 64; BMI = 64: 4 waves (1 x 4) of 64 x 32 (six workgroups per CU)
+  constexpr int BNI = 128, BKI = 64, NT = 256, NWN = BMI == 128 ? 2 : 4, NJ = BNI / NWN / 16, PA = BMI / 32;
   constexpr int CLD = BNI + 8;
-  constexpr int TILE = 128 * BKI;                               // halves per operand tile (16 KiB)
-  constexpr int LDS_H = 2 * TILE > BMI * CLD ? 2 * TILE : BMI * CLD;
-  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];   // [A (128 x 64) | W (128 x 64)], then C
+  constexpr int TILE_A = BMI * BKI, TILE_W = BNI * BKI;
+  constexpr int LDS_H = TILE_A + TILE_W > BMI * CLD ? TILE_A + TILE_W : BMI * CLD;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];   // [A (BMI x 64) | W (128 x 64)], then C
   const int z = blockIdx.z;
   A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
   const int ntn = (N + BNI - 1) / BNI, ntm = (M + BMI - 1) / BMI, nwg = ntn * ntm;
@@ -310,49 +311,52 @@ __global__ void __launch_bounds__(256, 4)
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int m0 = (wg / ntn) * BMI, n0 = (wg % ntn) * BNI;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave / NWN) * 64, wn = (wave % NWN) * (16 * NJ);
   const int r = lane & 15, g = lane >> 4;
   const int fo[2] = {r * BKI + ((g) ^ (r >> 1)) * 8, r * BKI + ((4 + g) ^ (r >> 1)) * 8};
-  // staging: wave w fills A and W rows [32 w, 32 w + 32), 8 rows (1 KiB) per DMA piece
-  const _Float16* pa[4];
+  // staging: wave w fills A rows [BMI/4 w, ..) and W rows [32 w, 32 w + 32), 8 rows (1 KiB) per DMA piece
+  const _Float16* pa[PA];
   const _Float16* pw[4];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int row = wave * (BMI / 4) + i * 8 + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
+    pa[i] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = wave * 32 + i * 8 + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
-    pa[i] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
     pw[i] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
   }
-  f32x4 acc[4][4];
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  const int jl = min(4, max(0, (N - (n0 + wn) + 15) / 16));   // live 16-column blocks of this wave
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int jl = min(NJ, max(0, (N - (n0 + wn) + 15) / 16));   // live 16-column blocks of this wave
   for (int k0 = 0; k0 < K; k0 += BKI) {
     const int kh_n = min(2, (K - k0) / 32);                    // K halves in this tile (K % 32 == 0)
     if (k0 > 0) __syncthreads();                               // the previous tile's reads done
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(pa[i] + k0, lds + (wave * 32 + i * 8) * BKI);
-      glds16(pw[i] + k0, lds + TILE + (wave * 32 + i * 8) * BKI);
-    }
+    for (int i = 0; i < PA; ++i) glds16(pa[i] + k0, lds + (wave * (BMI / 4) + i * 8) * BKI);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(pw[i] + k0, lds + TILE_A + (wave * 32 + i * 8) * BKI);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     for (int kh = 0; kh < kh_n; ++kh) {
-      half8 af[4], bf[4];
+      half8 af[4], bf[NJ];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(lds + TILE + (wn + 16 * j) * BKI + fo[kh]);
+      for (int j = 0; j < NJ; ++j) bf[j] = *reinterpret_cast<const half8*>(lds + TILE_A + (wn + 16 * j) * BKI + fo[kh]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const half8*>(lds + (wm + 16 * i) * BKI + fo[kh]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
         if (j < jl)
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();
-  stage_out_tile<GELU, CLD, 4>(acc, lds, wm, wn, n0, N, bias, lane);
+  stage_out_tile<GELU, CLD, 4, NJ>(acc, lds, wm, wn, n0, N, bias, lane);
   __syncthreads();
 #pragma unroll 4
   for (int it = 0; it < BMI * BNI / 8 / NT; ++it) {
@@ -1008,7 +1012,8 @@ void dnn_solve(Ctx& x, const char* rho_field) {
     return v == 1 ? 32 : (v == 16 || v == 32 ? v : 0);
   }();
   // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
-  const bool in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) != 0 : true; }();
+  // (2: a 64 x 128 tile, six workgroups per CU)
+  const int in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) : 1; }();
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
@@ -1068,9 +1073,14 @@ void dnn_solve(Ctx& x, const char* rho_field) {
           hipLaunchKernelGGL((k_mlp_gemm_w<true, true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
       } else if (in_tile && K == 64) {   // the 55 -> 1600 input layer of the 53-species nets
-        hipLaunchKernelGGL((k_mlp_gemm_in<true>), dim3(blocks_for(N, 128) * blocks_for(n, 128), 1, d.nmod), dim3(256), 0,
-                           x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
-                           (long)n * ldc);
+        if (in_tile == 2)
+          hipLaunchKernelGGL((k_mlp_gemm_in<true, 64>), dim3(blocks_for(N, 128) * blocks_for(n, 64), 1, d.nmod), dim3(256),
+                             0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
+                             (long)n * ldc);
+        else
+          hipLaunchKernelGGL((k_mlp_gemm_in<true, 128>), dim3(blocks_for(N, 128) * blocks_for(n, 128), 1, d.nmod),
+                             dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
+                             ldc, (long)n * ldc);
       } else {
         hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                            (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);

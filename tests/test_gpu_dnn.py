@@ -241,7 +241,7 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     # the 800-wide layer's tail columns as two 16-column strips in its second and third tiles, "3w" as one
     # 32-column strip in the third, "3n" in a fourth tile
     variants = {"0": ("0", "0", "0"), "1": ("1", "1", "0"), "3": ("3", "1", "16"), "3w": ("3", "1", "32"),
-                "3n": ("3", "1", "0")}
+                "3n": ("3", "1", "0"), "3i": ("3", "2", "16")}   # "3i": the 64-row input-layer tile
     for wide, (w, i, t) in variants.items():
         monkeypatch.setenv("DFMI_DNN_WIDE", w)
         monkeypatch.setenv("DFMI_DNN_IN", i)
@@ -265,5 +265,5 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
         out[wide] = ctx.get_field("RR", (S, C))
         ctx.close()
     assert np.isfinite(out["0"]).all()
-    for wide in ("1", "3", "3w", "3n"):
+    for wide in ("1", "3", "3w", "3n", "3i"):
         assert np.array_equal(out[wide], out["0"]), (wide, np.abs(out[wide] - out["0"]).max())
