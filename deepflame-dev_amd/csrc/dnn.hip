@@ -564,7 +564,8 @@ template <bool GELU, bool OUT = false, int TS = 0>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                   long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
-                  const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0) {
+                  const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0,
+                  int ilv_ok = 1) {
   constexpr bool TAIL = TS > 0;
   static_assert(!(OUT && TAIL) && (TS == 0 || TS == 16 || TS == 32), "tail strips: 16 or 32 columns, no OUT");
   constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512, TW = TS, NJT = TS / 16, NSTRIP = TAIL ? 32 / TS : 0;
@@ -588,6 +589,12 @@ __global__ void __launch_bounds__(512, 1)
   // DMA sources: half-tile h, piece q: half-row hr = 16 wave + 8 q + (lane >> 3), 16-B chunk lane & 7 of the
   // LDS row holding logical chunk (lane & 7) ^ ((hr >> 1) & 7). A half h < 2: tile row (hr / 64) 128 + 64 h +
   // hr % 64 (rows of both wave rows); W half h = 2 + jh: tile row (hr / 32) 64 + 32 jh + hr % 32 (all columns)
+  // OUT, last tile partially live (N = 400: 144 of 256 columns): its live column blocks interleaved over the four
+  // wave columns (block 4 b + wc in the wave's local block b: 3 / 2 / 2 / 2 live blocks instead of 4 / 4 / 1 / 0),
+  // so that the SIMDs share its MFMAs (waves 4 r + c run on SIMD c); the partial sums stay per 64 consecutive
+  // columns (the activations go through LDS), bitwise the contiguous form
+  const bool ilv = OUT && ilv_ok && n0 + BNW > N;
+  const int nblk = (N - n0 + 15) / 16;   // live 16-column blocks of this tile (> 4 w.r.t. a wave: clamped below)
   const _Float16* src[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
@@ -598,7 +605,9 @@ __global__ void __launch_bounds__(512, 1)
         const int row = (hr >> 6) * 128 + h * 64 + (hr & 63);
         src[h][q] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
       } else {
-        const int row = (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31);
+        const int lc = (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31);   // the wave-column-major LDS position
+        // interleaved last OUT tile: wave column w's local block b holds tile column block 4 b + w
+        const int row = ilv ? 16 * (4 * ((lc >> 4) & 3) + (lc >> 6)) + (lc & 15) : lc;
         src[h][q] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
       }
     }
@@ -751,7 +760,7 @@ __global__ void __launch_bounds__(512, 1)
     if (tail_tile) kloop(std::integral_constant<int, 4>{}, std::true_type{});
     else kloop(std::integral_constant<int, 4>{}, std::false_type{});
   } else {
-    switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
+    switch (ilv ? min(4, max(0, (nblk - wc + 3) / 4)) : min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
       case 4: kloop(std::integral_constant<int, 4>{}, std::false_type{}); break;
       case 3: kloop(std::integral_constant<int, 3>{}, std::false_type{}); break;
       case 2: kloop(std::integral_constant<int, 2>{}, std::false_type{}); break;
@@ -760,7 +769,66 @@ __global__ void __launch_bounds__(512, 1)
     }
   }
   if constexpr (OUT) {   // the fused output layer (no LDS use: the drained stages are not touched)
-    out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
+    if (!ilv) {
+      out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
+      return;
+    }
+    // interleaved tile: the fp16 activations of the wave's blocks into LDS, then each wave's partials over its
+    // natural 64 columns from there (the same values and operation order as out_layer_partials)
+    __syncthreads();
+    _Float16* cs = lds;
+    const int g4 = 4 * (lane >> 4);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int cb = 4 * b + wc;   // tile column block
+      if (cb >= nblk) continue;
+      const int cl = 16 * cb + (lane & 15), col = n0 + cl;
+      const bool live = col < N;
+      const float bv = live ? bias[col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int rl = wm + 16 * i + g4 + e;
+          f32x2 v = round16(f32x2{acc[i][b][e], acc[i][b][e + 1]} + bv);
+          if (GELU) v = gelu_fast2(v);
+          const half2v h = to16(v);
+          cs[rl * CLD + cl] = h.x;
+          cs[(rl + 1) * CLD + cl] = h.y;
+        }
+    }
+    __syncthreads();
+    float wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      wv[j] = col < N ? (float)wo[col] : 0.0f;
+    }
+    float* Pw = P + (long)(4 * (wg % ntn) + wc) * M;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int rl = wm + 16 * i + g4 + e;
+        f32x2 sa = {0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (n0 + wn + 16 * j >= N) break;
+          const int cl = wn + 16 * j + (lane & 15);
+          const f32x2 hq = {(float)cs[rl * CLD + cl], (float)cs[(rl + 1) * CLD + cl]};
+          sa = __builtin_elementwise_fma(hq, f32x2(wv[j]), sa);
+        }
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) {
+          sa.x += __shfl_xor(sa.x, off);
+          sa.y += __shfl_xor(sa.y, off);
+        }
+        const int row = m0 + rl;
+        if ((lane & 15) == 0) {
+          if (row < M) Pw[row] = sa.x;
+          if (row + 1 < M) Pw[row + 1] = sa.y;
+        }
+      }
     return;
   }
   // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
@@ -1011,6 +1079,9 @@ void dnn_solve(Ctx& x, const char* rho_field) {
     const int v = e ? std::atoi(e) : 16;
     return v == 1 ? 32 : (v == 16 || v == 32 ? v : 0);
   }();
+  // the fused-output layer's partially live last tile with its column blocks interleaved over the wave columns
+  // (DFMI_DNN_OUT_ILV=1; default 0: contiguous)
+  const int out_ilv = [] { const char* e = std::getenv("DFMI_DNN_OUT_ILV"); return e ? std::atoi(e) : 0; }();
   // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
   // (2: a 64 x 128 tile, six workgroups per CU)
   const int in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) : 1; }();
@@ -1046,7 +1117,7 @@ void dnn_solve(Ctx& x, const char* rho_field) {
         if (pp_out)
           hipLaunchKernelGGL((k_mlp_gemm_pp<true, true>), dim3(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod),
                              dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
-                             ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1], d.part.p, sP);
+                             ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1], d.part.p, sP, out_ilv);
         else
           hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],

@@ -240,12 +240,14 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     # (DFMI_DNN_WIDE, DFMI_DNN_IN, DFMI_DNN_TAIL): "0" = k_mlp_gemm for every layer; "3" the ping-pong kernel with
     # the 800-wide layer's tail columns as two 16-column strips in its second and third tiles, "3w" as one
     # 32-column strip in the third, "3n" in a fourth tile
-    variants = {"0": ("0", "0", "0"), "1": ("1", "1", "0"), "3": ("3", "1", "16"), "3w": ("3", "1", "32"),
-                "3n": ("3", "1", "0"), "3i": ("3", "2", "16")}   # "3i": the 64-row input-layer tile
-    for wide, (w, i, t) in variants.items():
+    # "3i": the 64-row input-layer tile
+    variants = {"0": ("0", "0", "0", "0"), "1": ("1", "1", "0", "0"), "3": ("3", "1", "16", "0"),
+                "3w": ("3", "1", "32", "0"), "3n": ("3", "1", "0", "0"), "3i": ("3", "2", "16", "0")}
+    for wide, (w, i, t, o) in variants.items():
         monkeypatch.setenv("DFMI_DNN_WIDE", w)
         monkeypatch.setenv("DFMI_DNN_IN", i)
         monkeypatch.setenv("DFMI_DNN_TAIL", t)
+        monkeypatch.setenv("DFMI_DNN_OUT_ILV", o)
         ctx = Context(0)
         pt = case.default_patch_types(m)
         rows, cols = m.proc_rows_cols()
