@@ -240,9 +240,11 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     # (DFMI_DNN_WIDE, DFMI_DNN_IN, DFMI_DNN_TAIL): "0" = k_mlp_gemm for every layer; "3" the ping-pong kernel with
     # the 800-wide layer's tail columns as two 16-column strips in its second and third tiles, "3w" as one
     # 32-column strip in the third, "3n" in a fourth tile
-    # "3i": the 64-row input-layer tile
+    # "3i": the 64-row input-layer tile; "3v": the fused-output layer's last tile with its column blocks
+    # interleaved over the wave columns (DFMI_DNN_OUT_ILV=1)
     variants = {"0": ("0", "0", "0", "0"), "1": ("1", "1", "0", "0"), "3": ("3", "1", "16", "0"),
-                "3w": ("3", "1", "32", "0"), "3n": ("3", "1", "0", "0"), "3i": ("3", "2", "16", "0")}
+                "3w": ("3", "1", "32", "0"), "3n": ("3", "1", "0", "0"), "3i": ("3", "2", "16", "0"),
+                "3v": ("3", "1", "16", "1")}
     for wide, (w, i, t, o) in variants.items():
         monkeypatch.setenv("DFMI_DNN_WIDE", w)
         monkeypatch.setenv("DFMI_DNN_IN", i)
@@ -267,5 +269,5 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
         out[wide] = ctx.get_field("RR", (S, C))
         ctx.close()
     assert np.isfinite(out["0"]).all()
-    for wide in ("1", "3", "3w", "3n", "3i"):
+    for wide in ("1", "3", "3w", "3n", "3i", "3v"):
         assert np.array_equal(out[wide], out["0"]), (wide, np.abs(out[wide] - out["0"]).max())
