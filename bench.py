@@ -113,7 +113,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
+    ap.add_argument("--n", "--cells-per-dir", dest="n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
     ap.add_argument("--mech", default="burke9", choices=sorted(MECHS))
     ap.add_argument("--ncorr", type=int, default=2)
     ap.add_argument("--init", default="reference", choices=["reference", "tgv"],
@@ -142,7 +142,29 @@ def parse():
                          "limitedLinear01 / limitedLinear / cubic, what the reference CPU solver runs) or the "
                          "reference GPU path's hard-wired upwind / linear / linear; the other set is timed beside")
     ap.add_argument("--alt-steps", type=int, default=5, help="timed steps with the other scheme set (0: skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks and their mesh blocks, print the line's layout fields, touch no GPU "
+                         "(tests of the launcher and the decomposition on CPU)")
     return ap.parse_args()
+
+
+def spawn_ranks(n_gpus: int) -> int:
+    """--gpus N > 1 started as a plain `python bench.py --gpus N` (no torchrun environment): launch the N ranks
+    here, one process per GPU, exactly as the driver's torchrun command would (the reference binds one GPU per
+    rank inside its own init, src_gpu/dfNcclBase.cu:23-65). This process never touches the GPU: it only waits
+    for the children and returns their status; rank 0's JSON line goes straight to our stdout."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:   # a free rendezvous port on the loopback
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    # torchrun's own parser takes an abbreviation of its options even among the script's arguments ("--n" is
+    # ambiguous with --nnodes / --nproc-per-node): hand the children the long spelling
+    own = ["--cells-per-dir" + a[3:] if a == "--n" or a.startswith("--n=") else a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + own
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
 
 
 def case_schemes():
@@ -497,14 +519,64 @@ def chem_step_stats(ctx, C):
             "wave_eff_sorted": float(cost.mean() / srt) if srt else None}
 
 
+def decomposition(world: int):
+    """decomposePar blocks of the weak-scaling box: 2x1x1 / 2x2x1 / 2x2x2 (N = 8 is BASELINE config 5)"""
+    return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}.get(world, (world, 1, 1))
+
+
+def rank_block(n: int, decomp, rank: int):
+    """this rank's n^3 block of the (n d0) x (n d1) x (n d2) periodic 2 pi mm-per-block box"""
+    from dfmi.mesh import hex_box
+    L = 6.283185307179586e-3
+    return hex_box(n * decomp[0], n * decomp[1], n * decomp[2], lengths=(L * decomp[0], L * decomp[1], L * decomp[2]),
+                   decomp=decomp, rank=rank)
+
+
+def dry_run(args, world: int, rank: int):
+    """the launcher and layout without a GPU: every rank builds its block and its processor patches, rank 0
+    prints the fields of the line that describe them"""
+    import torch.distributed as dist
+    decomp = decomposition(world)
+    m = rank_block(args.n, decomp, rank)
+    mine = {"rank": rank, "cells": m.n_cells, "proc_faces": int(m.proc_rows_cols()[0].size),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
+    every = [mine]
+    if world > 1:
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+    if rank == 0:
+        print(json.dumps({"metric": "cell-updates/s (dfLowMachFoam outer iter)", "dry_run": True, "n_gpus": world,
+                          "scaling": "weak",
+                          "config": {"cells_per_gpu": m.n_cells, "cells_total": sum(e["cells"] for e in every),
+                                     "parallelism": parallelism(decomp, world)},
+                          "ranks": every}), flush=True)
+
+
+def parallelism(decomp, world: int) -> str:
+    return (f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1 else "single")
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU: the parent only waits
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; the world size decides",
+              file=sys.stderr)
     import numpy as np
     import torch                                   # loads the HIP runtime first: one runtime per process
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        dry_run(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1 and os.environ.get("DFMI_RCCL_SPLIT_HOSTS"):
         # rehearsal of the multi-GPU path on a box with fewer GPUs than ranks: each rank poses as its own
         # host (RCCL then connects the ranks through sockets instead of refusing two ranks per device);
@@ -528,12 +600,8 @@ def main():
     inert = ym["species"].index("N2")
 
     n = args.n
-    decomp = {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}.get(world)
-    if decomp is None:
-        decomp = (world, 1, 1)
-    L = 6.283185307179586e-3
-    m = hex_box(n * decomp[0], n * decomp[1], n * decomp[2], lengths=(L * decomp[0], L * decomp[1], L * decomp[2]),
-                decomp=decomp, rank=rank)
+    decomp = decomposition(world)
+    m = rank_block(n, decomp, rank)
     if args.renumber != "none":   # renumberMesh's role: cells in Morton bricks, faces re-sorted
         from dfmi.renumber import renumber_mesh
         m, _ = renumber_mesh(m, args.renumber)
@@ -579,7 +647,8 @@ def main():
     ctx.sync()
     if world > 1:
         dist.barrier()
-    # ---- headline: K steps, nothing armed (no timing events inside the timed region)
+    # ---- headline: K steps; only an event on the context stream after every step (dfmi_step_timer, no sync)
+    ctx.step_timer(True)
     torch.cuda.synchronize(local)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -590,10 +659,13 @@ def main():
     if world > 1:
         dist.barrier()
     el = t1 - t0
+    step_ms = ctx.step_times(args.steps)
+    ctx.step_timer(False)
+    med = float(np.median(step_ms)) if step_ms.size else float("nan")
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64)
+        tt = torch.tensor([el, med], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+        el, med = float(tt[0].item()), float(tt[1].item())
     stats = {e: ctx.solver_stats(e) for e in ("U", "Y", "E", "p")}
 
     # ---- roofline pass: the same step, HIP events around every launch of the measured kernels and the
@@ -736,6 +808,12 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
+        "ms_per_step_median": med,
+        "ms_per_step_events": {"min": float(step_ms.min()) if step_ms.size else None,
+                               "max": float(step_ms.max()) if step_ms.size else None,
+                               "mean": float(step_ms.mean()) if step_ms.size else None,
+                               "note": "HIP events on the context stream after every timed step (rank 0's; the "
+                                       "median is the max over ranks); ms_per_step is the bracketed wall time / K"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -751,8 +829,7 @@ def main():
                                                           if args.schemes == "case" else
                                                           "the reference GPU path's hard-wired upwind/linear"),
                    "traversal": args.traversal,
-                   "parallelism": f"domain decomposition {decomp[0]}x{decomp[1]}x{decomp[2]}, RCCL halo" if world > 1
-                   else "single"},
+                   "parallelism": parallelism(decomp, world)},
         "roofline": None if primary is None else dict(roofs[primary], traffic_source=f"profiles/{PMC_FILE} (rocprofv3 --pmc FETCH_SIZE / "
                          "WRITE_SIZE passes, mean per dispatch, gfx950 read correction)",
                          note=f"achieved = algorithmic bytes of the work done (active systems/iterations; SURVEY 8(d): "

@@ -650,6 +650,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
   return guard([&] {
     Ctx& x = ctx->x;
     require_ready(x);
+    if (x.steptimer.on && x.steptimer.used == 0) x.steptimer.mark(x.stream);
     x.dnn.prepared = false;         // never reuse a compaction of an earlier (failed) step
     copy_old(x);                    // preTimeStep
     if (x.chem.mode == 2) dnn_prepare(x);   // reacting cells of this step's T (read after the UEqn polls)
@@ -667,6 +668,31 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     }
     thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
     if (x.chem.mode == 1) chem_check(x);   // the p solves' polls have already passed the chemistry
+    if (x.steptimer.on) x.steptimer.mark(x.stream);
+  });
+}
+
+int dfmi_step_timer(dfmi_ctx* ctx, int on) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    x.steptimer.on = on != 0;
+    x.steptimer.used = 0;
+  });
+}
+
+int dfmi_step_times(dfmi_ctx* ctx, double* ms, int n, int* got) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+    const StepTimer& t = x.steptimer;
+    const int have = t.used > 1 ? (int)t.used - 1 : 0;
+    for (int i = 0; i < have && i < n; ++i) {
+      float v = 0;
+      DFMI_HIP(hipEventElapsedTime(&v, t.ev[i], t.ev[i + 1]));
+      ms[i] = v;
+    }
+    if (got) *got = have;
   });
 }
 

@@ -175,6 +175,24 @@ struct KernelTimer {
   }
 };
 
+// Per-step timing (dfmi_step_timer / dfmi_step_times): while armed, dfmi_time_step records an event on the
+// context stream before its first step and after every step (no synchronisation), so the bench reads each
+// step's duration -- end of step i to end of step i-1 -- and reports their median beside the bracketed mean.
+struct StepTimer {
+  bool on = false;
+  std::vector<hipEvent_t> ev;         // ev[0]: before the first armed step; ev[i]: after step i
+  size_t used = 0;
+  ~StepTimer() { for (auto e : ev) (void)hipEventDestroy(e); }
+  void mark(hipStream_t s) {
+    if (used == ev.size()) {
+      hipEvent_t e;
+      DFMI_HIP(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+    DFMI_HIP(hipEventRecord(ev[used++], s));
+  }
+};
+
 // Communication accounting per exchange point (dfmi_comm_timer / dfmi_comm_report): every transport call
 // of a halo exchange (ncclSend/ncclRecv group) or an all-gather, HIP events around it on the stream it is
 // issued on (the compute stream, or the halo's comm stream for overlapped exchanges), with the bytes this
@@ -301,6 +319,7 @@ struct Ctx {
   std::map<std::string, StatSnap> stat_snap;
   DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
+  StepTimer steptimer;
   CommStats comm;
   DevBuf<int> trav;   // dfmi_set_traversal: the order threads visit cells in the gather kernels (empty: natural)
   int hex[3] = {0, 0, 0};   // MeshView::hx/hy/hz (build_ell)

@@ -59,6 +59,7 @@ SIGNATURES = {
     "dfmi_thermo_update_rho": [_P], "dfmi_thermo_psip0": [_P], "dfmi_thermo_correct_psip_rho": [_P],
     "dfmi_U_get_HbyA": [_P], "dfmi_p_process": [_P], "dfmi_post_time_step": [_P],
     "dfmi_time_step": [_P, C.c_int], "dfmi_sync": [_P],
+    "dfmi_step_timer": [_P, C.c_int], "dfmi_step_times": [_P, _DP, C.c_int, _IP],
     "dfmi_hbm_copy_peak": [_P, C.c_double, C.c_int, _DP],
     "dfmi_assemble": [_P, C.c_char_p],
     "dfmi_get_matrix": [_P, C.c_char_p, C.c_char_p, _DP, C.c_long],
@@ -405,6 +406,17 @@ class Context:
         v = C.c_double()
         self._call("dfmi_hbm_copy_peak", self.h, float(gib), int(reps), C.byref(v))
         return v.value
+
+    def step_timer(self, on: bool = True):
+        """arm per-step HIP events on the context stream (dfmi_time_step marks the end of every step)"""
+        self._call("dfmi_step_timer", self.h, int(on))
+
+    def step_times(self, n: int) -> np.ndarray:
+        """durations (ms) of the steps run since step_timer(True): end of step i minus end of step i-1"""
+        out = np.zeros(max(n, 1))
+        got = C.c_int(0)
+        self._call("dfmi_step_times", self.h, _dp(out), int(n), C.byref(got))
+        return out[:min(got.value, n)]
 
     def sync(self):
         self._call("dfmi_sync", self.h)

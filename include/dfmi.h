@@ -164,6 +164,10 @@ int dfmi_post_time_step(dfmi_ctx* ctx);         /* dfMatrixDataBase::postTimeSte
 /* the whole loop body above with n_corr pressure correctors */
 int dfmi_time_step(dfmi_ctx* ctx, int n_corr);   /* non-zero also when chemistry hit its step limit */
 int dfmi_sync(dfmi_ctx* ctx);
+/* per-step HIP events on the context stream (bench: median step time); no reference counterpart (its
+ * TIME_GPU host ticks, dfLowMachFoam.C:249-531). dfmi_step_times returns got = steps timed since arming */
+int dfmi_step_timer(dfmi_ctx* ctx, int on);
+int dfmi_step_times(dfmi_ctx* ctx, double* ms, int n, int* got);
 /* diagnostic: measured device-memory copy bandwidth (read + write GB/s) of a gib-GiB buffer copied reps
  * times by a 16-B-vector streaming kernel -- the measured peak beside the datasheet's 8 TB/s */
 int dfmi_hbm_copy_peak(dfmi_ctx* ctx, double gib, int reps, double* gbs);

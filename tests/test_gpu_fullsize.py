@@ -92,9 +92,10 @@ def test_config4_full_size_deterministic_and_closed():
     source of 52 nets [55,1600,800,400,1] on MFMA fp16): the large-mechanism kernels (species-chunked Y
     assembly, cooperative thermo, batched 52-system BiCGStab, compacted DNN inference) give bitwise
     identical fields when the same state is stepped twice, species close to 1 in every cell, T stays
-    physical and every solve meets its tolerance."""
+    physical and every solve meets its tolerance. Run with the case's convection schemes, as the bench's
+    config-4 line (bench.py config4_line) runs it."""
     sys.path.insert(0, ROOT)
-    from bench import MECHS, reference_fields
+    from bench import MECHS, reference_fields, case_schemes
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi.lib import Context
@@ -106,7 +107,7 @@ def test_config4_full_size_deterministic_and_closed():
     sp = gri53_species(os.path.join(GOLDEN, "gri30.yaml"))
     t = read_thermo_table(os.path.join(GOLDEN, "thermo_gri53_synthetic.txt"), sp)
     ctx = Context(0)
-    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6)
+    case.setup_context(ctx, m, t, sp.index("N2"), 1e-6, schemes=case_schemes())
     gri53_dnn(ctx)
     ctx.chem_set_options(2)
     T0 = f["T"]
