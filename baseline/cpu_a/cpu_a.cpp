@@ -32,7 +32,7 @@
 #include <vector>
 
 #define DFMI_HD   // the generated kinetics run on the host here
-#define DFMI_OPAQUE(v, q)   // scheduling barrier of the device build only
+#define DFMI_SCHED_FENCE()   // scheduling barrier of the device build only
 #pragma GCC diagnostic push
 #pragma GCC diagnostic ignored "-Wunused-variable"
 #include "../../deepflame-dev_amd/csrc/chem_gen_burke9.inc"
@@ -585,7 +585,7 @@ int chem_cells(Ctx& x, double dt, const double* rho_rr) {
     const double iys = 1.0 / ys;
     for (int i = 0; i < S; ++i) sw += std::fmax(Y0[i], 0.0) * iys / G::W[i];
     const double rho = pf[c] / (sw * RU * T);
-    for (int i = 0; i < S; ++i) { y[i] = rho * (std::fmax(Y0[i], 0.0) * iys) / G::W[i]; sc[i] = atol * rho / G::W[i]; }
+    for (int i = 0; i < S; ++i) { y[i] = rho * (std::fmax(Y0[i], 0.0) * iys) / G::W[i]; sc[i] = atol * rho * G::RW[i]; }
     int steps = 0, rejects = 0;
     double hnext = 0.0;
     if (T >= Tmin) {
@@ -598,9 +598,8 @@ int chem_cells(Ctx& x, double dt, const double* rho_rr) {
         if (t + h > dt) h = dt - t;
         const double hg = h * g, rh = 1.0 / h;
         double f0[SA], A[SA * SA];
-        G::wdot(T, k, y, f0);
         for (int e = 0; e < SA * SA; ++e) A[e] = 0.0;
-        G::jac(T, k, y, A);
+        G::wdot_jac(T, k, y, f0, A);
         for (int e = 0; e < SA * SA; ++e) A[e] = (e % (SA + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
         bool ok = G::factor(A);
         double err = 0.0, yn[SA];
@@ -1051,6 +1050,9 @@ int dfmi_thermo_psip0(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x);
 int dfmi_thermo_correct_psip_rho(dfmi_ctx* ctx) { return guard([&] { require_ready(ctx->x); correct_psip_rho(ctx->x); }); }
 int dfmi_time_step(dfmi_ctx* ctx, int n_corr) { return guard([&] { require_ready(ctx->x); time_step(ctx->x, n_corr); }); }
 int dfmi_sync(dfmi_ctx*) { return 0; }
+// no device events on the CPU: the bench times CPU-A with host clocks
+int dfmi_step_timer(dfmi_ctx*, int) { return 0; }
+int dfmi_step_times(dfmi_ctx*, double*, int, int* got) { if (got) *got = 0; return 0; }
 int dfmi_hbm_copy_peak(dfmi_ctx*, double, int, double*) { return guard([&] { throw Error("dfmi (CPU-A): no device memory"); }); }
 
 int dfmi_correct_boundary(dfmi_ctx* ctx, const char* field) {

@@ -100,12 +100,24 @@ template <class T> struct AmgView {
 AmgView<float> amg_view_f32(Ctx& x, const int* col0);
 AmgView<double> amg_view_f64(Ctx& x, const double* val0, const double* D0, const int* col0);
 
+// The PCG stop test (linsolve.hip k_cg_spmv: ||r|| <= tol ||r0|| or <= abs_tol) evaluated by the V-cycle's
+// first launch after the fused update, from the same partials in the same order, so a converged solve skips
+// its last V-cycle; k_cg_spmv of iteration `it` then finds the flag set and returns. The recorded residual and
+// iteration count are the ones k_cg_spmv would record.
+struct CgStop {
+  Red rr;               // the update's r.r partials
+  double* scal;         // PCG scalars (4 res0, 5 res, 6 active, 7 iters); nullptr: no test
+  int it;               // the PCG iteration the test belongs to
+  double tol, abs_tol;
+};
+
 void amg_setup(Ctx& x);
 void amg_galerkin(Ctx& x, const double* val0, const double* D0);
 // z = M^-1 r with block partials of r.z written to partial[0 .. nblk) (grid of `nblk` blocks); every
 // kernel returns at once when *active == 0 (a converged solve; nullptr: always run)
 void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
-               double* partial, int nblk, const double* active = nullptr, bool l0_done = false);
+               double* partial, int nblk, const double* active = nullptr, bool l0_done = false,
+               const CgStop& stop = CgStop{});
 // the level-0 first sweep (x0, residual) can be written by the PCG update kernel instead (linsolve.hip:
 // k_cg_x_smooth): fp32 V-cycle, launch-per-level path, one pre-sweep, at least two levels
 bool amg_l0_fusable(const Ctx& x);

@@ -282,10 +282,26 @@ __global__ void __launch_bounds__(TPB) k_post_smooth_h(int n, int W_, ColView co
 }
 
 template <class T>
-__global__ void k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
-                           const T* __restrict__ r, T* __restrict__ bc, const double* act) {
+__global__ void __launch_bounds__(TPB) k_restrict(int nc, const int* __restrict__ mstart, const int* __restrict__ members,
+                                                  const T* __restrict__ r, T* __restrict__ bc, const double* act,
+                                                  CgStop st = CgStop{}) {
+  if (st.scal) {   // every block repeats the PCG stop test (CgStop); block 0 records it
+    __shared__ double sa;
+    if (threadIdx.x == 0) sa = *act;   // one read per block: block 0 may set the flag meanwhile
+    __syncthreads();
+    if (sa == 0.0) return;
+    double b[1];
+    red_sum<1>(st.rr, 0, b);
+    const double res = sqrt(b[0]);
+    if (res <= st.tol * st.scal[4] || res <= st.abs_tol) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) { st.scal[5] = res; st.scal[7] = st.it; st.scal[6] = 0.0; }
+      return;
+    }
+  } else if (act && *act == 0.0) {
+    return;
+  }
   const int I = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I >= nc || (act && *act == 0.0)) return;
+  if (I >= nc) return;
   T a = 0;
   for (int e = mstart[I]; e < mstart[I + 1]; ++e) a += r[members[e]];
   bc[I] = a;
@@ -994,7 +1010,7 @@ void launch_w(int W, dim3 g, hipStream_t st, K0 k0, K6 k6, A... a) {
 // z = M^-1 r in precision T; block partials of r.z (one per block of the level-0 grid) into `partial`
 template <class T>
 void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
-             double* partial, int nblk, const double* act, bool l0_done) {
+             double* partial, int nblk, const double* act, bool l0_done, const CgStop& stop) {
   constexpr bool F = std::is_same<T, float>::value;
   Amg& a = x.amg;
   const int L = (int)a.lv.size();
@@ -1103,7 +1119,8 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
     {
       KScope _ks(x, "k_restrict");
       hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[l + 1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[l + 1].n,
-                         f.mstart.p, f.members.p, (const T*)rcur, BV(l + 1), act);
+                         f.mstart.p, f.members.p, (const T*)rcur, BV(l + 1), act,
+                         l == 0 && l0_done ? stop : CgStop{});
     }
   }
   // coarsest: the agglomerated level (every rank's coarsest right-hand sides gathered, the global level
@@ -1231,15 +1248,15 @@ bool amg_l0_fusable(const Ctx& x) {
 }
 
 void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
-               double* partial, int nblk, const double* active, bool l0_done) {
+               double* partial, int nblk, const double* active, bool l0_done, const CgStop& stop) {
   Amg& a = x.amg;
   DFMI_CHECK(!l0_done || amg_l0_fusable(x), "AMG: level-0 sweep fused on an unsupported configuration");
   CommTag _ct(x, x.comm.tag + " amg");
   auto direct = [&] {
-    if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
-    else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done);
+    if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
+    else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
   };
-  if (!a.use_graph || !x.ktimer.targets.empty()) { direct(); return; }
+  if (!a.use_graph || !x.ktimer.targets.empty() || stop.scal) { direct(); return; }
   const std::array<uintptr_t, 8> key{(uintptr_t)val0, (uintptr_t)D0, (uintptr_t)col0.col, (uintptr_t)r, (uintptr_t)z,
                                      (uintptr_t)partial, (uintptr_t)nblk * 2 + (l0_done ? 1 : 0), (uintptr_t)active};
   auto it = a.graphs.find(key);

@@ -535,19 +535,29 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wunused-variable"
 #define DFMI_HD __device__   // the generated kinetics are plain C++; here they run on the device
-// value v passes through an empty asm that also reads q: the same value, but not available before q
-#define DFMI_OPAQUE(v, q) asm volatile("" : "+v"(v) : "v"(q))
+// between the reactions of the fused rates + Jacobian pass: nothing is scheduled across, so one reaction's
+// temporaries die before the next one's loads are issued (the register peak is J plus one reaction)
+#define DFMI_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #include "chem_gen_burke9.inc"
 #include "chem_gen_es80.inc"
 #pragma clang diagnostic pop
 
 // The integrated state is the mechanism's active species (G::SA; a third-body-only species such as N2 keeps its
 // concentration and rides along in y) -- bitwise the full-state integration: the dropped rows and columns
-// only ever multiply or add exact zeros (chem_codegen.py). RK: the rate constants are computed inline, next to
-// their reaction, in every rates / rates_jac call (two per step) instead of once per cell and held across the
-// step loop (48 doubles for Burke 9); the same values and sums, bitwise.
-template <class G, bool RK, int WV>
-__global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __restrict__ perm,
+// only ever multiply or add exact zeros (chem_codegen.py).
+// Registers: the dense iteration matrix (SA^2 doubles, 128 VGPRs for Burke 9), the state and the stage vectors
+// fill the wave's registers, so the NK rate constants -- computed once per cell (T is frozen), read by every
+// rate and Jacobian evaluation of the step loop -- live in LDS as [constant][lane] (conflict-free ds_read_b64,
+// 24.6 KiB per 64-lane workgroup for Burke 9) instead of 96 more VGPRs that spilled to scratch (round 4:
+// 256 VGPR + 256 AGPR + 84 B/lane of scratch at one wave per SIMD).
+struct KLds {
+  double* base;   // the workgroup's constants, [constant][lane]
+  int lane;       // constant i of this lane at base[i * LANES + lane]
+  __device__ __forceinline__ double& operator[](int i) const { return base[i * LANES + lane]; }
+};
+
+template <class G>
+__global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __restrict__ perm,
     const double* __restrict__ Tf, const double* __restrict__ pf, const double* __restrict__ rhof,
     const double* __restrict__ Yf, double dt, double rtol, double atol, double Tmin, int max_steps,
     double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail) {
@@ -557,6 +567,8 @@ __global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __res
                    c32 = 0.92076794298330791242156818474003e1;
   constexpr double m2 = 0.61697947043828245592553615689730e1, m3 = -0.42772256543218573326238373806514;
   constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
+  __shared__ double kl[G::NK * LANES];
+  KLds kh{kl, (int)threadIdx.x};
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
   if (t >= n) return;
   const long c = perm ? perm[t] : t;
@@ -572,24 +584,23 @@ __global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __res
   int steps = 0, rejects = 0;
   double hnext = 0.0;   // the step the integration would take next
   if (T >= Tmin) {
-    double kh[G::NK];   // held across the loop unless RK (then unused)
-    if constexpr (!RK) G::consts(T, kh);
+    G::consts(T, kh);
     // first step: the size the previous solve of this cell ended with (OpenFOAM's per-cell deltaTChem)
     const double hp = stats[2 * n + c];
     double t = 0.0, h = hp > 0.0 ? fmin(dt, hp) : dt;
     while (t < dt) {
+      // the lane offset passes through an empty asm each iteration: the constants' LDS reads cannot be hoisted
+      // out of the loop (held in registers across it, which is what this layout exists to avoid)
+      asm volatile("" : "+v"(kh.lane));
+      double arho = atol * rho;   // tolerance scale atol rho / W_i, formed per use (not 8 values held across the loop)
+      asm volatile("" : "+v"(arho));
       if (steps + rejects >= max_steps) { steps = -1; break; }
       if (t + h > dt) h = dt - t;
       const double hg = h * g, rh = 1.0 / h;
       double f0[SA], A[SA * SA];
 #pragma unroll
       for (int e = 0; e < SA * SA; ++e) A[e] = 0.0;
-      if constexpr (RK) {
-        G::rates_jac(T, y, f0, A);
-      } else {
-        G::wdot(T, kh, y, f0);
-        G::jac(T, kh, y, A);
-      }
+      G::wdot_jac(T, kh, y, f0, A);
 #pragma unroll
       for (int e = 0; e < SA * SA; ++e) A[e] = (e % (SA + 1) == 0 ? 1.0 : 0.0) - hg * A[e];
       bool ok = G::factor(A);
@@ -603,11 +614,7 @@ __global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __res
         for (int i = 0; i < S; ++i) y2[i] = y[i];
 #pragma unroll
         for (int a = 0; a < SA; ++a) y2[G::ACT[a]] = y[G::ACT[a]] + k1[a];
-        if constexpr (RK) {
-          G::rates(T, y2, f2);
-        } else {
-          G::wdot(T, kh, y2, f2);
-        }
+        G::wdot(T, kh, y2, f2);
 #pragma unroll
         for (int a = 0; a < SA; ++a) k2[a] = hg * (f2[a] + c21 * rh * k1[a]);
         G::solve(A, k2);
@@ -618,7 +625,7 @@ __global__ void __launch_bounds__(LANES, WV) k_chem_gen(long n, const int* __res
         for (int a = 0; a < SA; ++a) {
           const int i = G::ACT[a];
           yn[a] = y[i] + k1[a] + m2 * k2[a] + m3 * k3[a];
-          const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) / (atol * rho / G::W[i] + rtol * fmax(fabs(y[i]), fabs(yn[a])));
+          const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) / (arho * G::RW[i] + rtol * fmax(fabs(y[i]), fabs(yn[a])));
           err += e * e;   // weighted RMS error norm (KPP / CVODE) over all S species (inactive terms are 0)
         }
         err = sqrt(err / S);
@@ -721,18 +728,9 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   }
   if (h.generated) {
     KScope _ks(x, "k_chem");
-    // DFMI_CHEM_RECOMP=0: rate constants held across the step loop (k_chem_gen<G, false, 1>); DFMI_CHEM_WAVES=2:
-    // the inline-constant form compiled for two waves per SIMD (A/B)
-    static const bool rk = [] { const char* e = std::getenv("DFMI_CHEM_RECOMP"); return e && std::atoi(e) != 0; }();
-    static const int wv = [] { const char* e = std::getenv("DFMI_CHEM_WAVES"); return e ? std::atoi(e) : 1; }();
-#define GEN(G, RK, WV) hipLaunchKernelGGL((k_chem_gen<G, RK, WV>), g, dim3(LANES), 0, x.stream, (long)x.C, perm,  \
-                                          x.f("T"), x.f("p"), rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin,          \
-                                          h.max_steps, x.f("RR"), stats, h.fail.p)
-    if (h.generated == 1) {
-      if (!rk) GEN(ChemGen_burke9, false, 1); else if (wv == 2) GEN(ChemGen_burke9, true, 2); else GEN(ChemGen_burke9, true, 1);
-    } else {
-      if (!rk) GEN(ChemGen_es80, false, 1); else if (wv == 2) GEN(ChemGen_es80, true, 2); else GEN(ChemGen_es80, true, 1);
-    }
+#define GEN(G) hipLaunchKernelGGL((k_chem_gen<G>), g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"), x.f("p"),  \
+                                  rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats, h.fail.p)
+    if (h.generated == 1) GEN(ChemGen_burke9); else GEN(ChemGen_es80);
 #undef GEN
     DFMI_HIP(hipGetLastError());
     chem_fail_snapshot(x);

@@ -158,4 +158,40 @@ template <class T, class FN> __device__ __forceinline__ void face_row(const Face
   }
 }
 
+// ---- fixed-order reductions of per-block partials (solvers: linsolve.hip; the PCG stop test the AMG's
+// first V-cycle kernel repeats, amg.hip). Blocks of RED_TPB threads.
+constexpr int RED_TPB = 256, RED_NW = RED_TPB / 64;
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+// value(s, i, k) = p[i * si + s * ss + k], i < np: the per-block partials (single rank) or the
+// all-gathered per-rank sums (multi-rank)
+struct Red { const double* p; int np; long si, ss; };
+
+// fixed-order block-wide sum, result in every thread
+template <int NV> __device__ __forceinline__ void red_sum(const Red& r, int s, double (&out)[NV]) {
+  __shared__ double sh[RED_NW][NV];
+  double v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.0;
+  for (int i = threadIdx.x; i < r.np; i += RED_TPB)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += r.p[(long)i * r.si + (long)s * r.ss + k];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) { const double t = wave_sum(v[k]); if (lane == 0) sh[wid][k] = t; }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double a = 0.0;
+#pragma unroll
+    for (int w = 0; w < RED_NW; ++w) a += sh[w][k];
+    out[k] = a;
+  }
+  __syncthreads();
+}
+
 }  // namespace dfmi

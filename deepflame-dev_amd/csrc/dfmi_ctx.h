@@ -317,6 +317,7 @@ struct Ctx {
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
   std::map<std::string, StatSnap> stat_snap;
+  std::map<std::string, int> solve_expect;   // iterations of the last solve per equation (linsolve.hip Poller)
   DevBuf<double> work;           // per equation (U, Y, E, p): system-iterations, summed on the device
   KernelTimer ktimer;
   StepTimer steptimer;

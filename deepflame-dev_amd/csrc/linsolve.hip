@@ -43,38 +43,7 @@ inline int cg_max_blocks() {
 constexpr int PAD = INT_MIN;
 constexpr int NSCAL = 16;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  return v;
-}
-
-// value(s, i, k) = p[i * si + s * ss + k], i < np: the per-block partials (single rank) or the
-// all-gathered per-rank sums (multi-rank)
-struct Red { const double* p; int np; long si, ss; };
-
-// fixed-order block-wide sum, result in every thread
-template <int NV> __device__ __forceinline__ void red_sum(const Red& r, int s, double (&out)[NV]) {
-  __shared__ double sh[NW][NV];
-  double v[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = 0.0;
-  for (int i = threadIdx.x; i < r.np; i += TPB)
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] += r.p[(long)i * r.si + (long)s * r.ss + k];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) { const double t = wave_sum(v[k]); if (lane == 0) sh[wid][k] = t; }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    double a = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) a += sh[w][k];
-    out[k] = a;
-  }
-  __syncthreads();
-}
+static_assert(TPB == RED_TPB, "the fixed-order reductions (dfmi_common.h red_sum) assume 256-thread blocks");
 
 // block partial of NV values -> partial[(s * nblk + blockIdx.x) * NV + k]
 // Row sets of the halo-overlapped SpMVs (multi-rank, DFMI_HALO_OVERLAP=1): part 1 = the rows without a
@@ -1133,22 +1102,36 @@ bool small_solve(const Ctx& x) {
   return !(e && std::atoi(e) == 0);
 }
 
-// Convergence polling without draining the stream: every `check` iterations the solver state is
-// copied into pinned host memory behind an event, and the host reads the snapshot of the PREVIOUS
-// check -- the GPU is already running the next batch by then (systems that converged turn every
-// kernel into an early return), so the queue never empties inside a solve. The decision is a pure
-// function of the globally reduced scalars, identical on every rank.
+// Convergence polling without draining the stream: after an iteration the solver state is copied into
+// pinned host memory behind an event, and the host reads the snapshot of an EARLIER check -- the GPU is
+// already running the next iteration(s) by then (systems that stopped turn every kernel into an early
+// return), so the queue never empties inside a solve. The decision is a pure function of the globally
+// reduced scalars, identical on every rank.
+// Cadence (round 5): the iterations the previous solve of the same equation needed (`expect`, 0 = none yet)
+// place the checks. Before expect - 1 a snapshot every 4 iterations (a solve that converges early costs a
+// few early-return launches more); from there a snapshot after EVERY iteration, each check reading the one
+// an iteration back, so a converged solve is stopped one iteration after the one that set its flag. The
+// round-4 cadence (a snapshot every 2 iterations, read 2 later) ran 3-4 iterations of early-return launches
+// after every solve (~4.7 us each: 0.3 ms per p-solve, ~1.2 ms per step, profiles/r05_timeline.json).
 struct Poller {
   Ctx& x;
   const double* scal;
   int nsys, slot = 0, pending = -1;
-  Poller(Ctx& c, const double* s, int n) : x(c), scal(s), nsys(n) {
+  int expect;
+  std::string key;
+  Poller(Ctx& c, const double* s, int n, const std::string& k) : x(c), scal(s), nsys(n), key(k) {
     x.sws().poll.ensure((size_t)2 * n * NSCAL);
     for (auto& e : x.sws().ev)
       if (!e) DFMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    auto f = x.solve_expect.find(key);
+    expect = f == x.solve_expect.end() ? 0 : f->second;
   }
-  // snapshot now; true when the previous snapshot shows every system stopped
-  bool snapshot_and_test() {
+  // after iteration `it` (0-based) has been enqueued: snapshot when the cadence says so; true when an
+  // earlier snapshot shows every system stopped (its iteration count becomes the next solve's `expect`)
+  bool after(int it) {
+    const int n = it + 1;
+    const bool snap = expect > 0 ? (n >= expect - 1 || n % 4 == 0) : (n % 2 == 0);
+    if (!snap) return false;
     double* dst = x.sws().poll.p + (size_t)slot * nsys * NSCAL;
     DFMI_HIP(hipMemcpyAsync(dst, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
     DFMI_HIP(hipEventRecord(x.sws().ev[slot], x.stream));
@@ -1157,7 +1140,12 @@ struct Poller {
       DFMI_HIP(hipEventSynchronize(x.sws().ev[pending]));
       const double* h = x.sws().poll.p + (size_t)pending * nsys * NSCAL;
       done = true;
-      for (int s = 0; s < nsys; ++s) done = done && h[s * NSCAL + 6] == 0.0;
+      int iters = 0;
+      for (int s = 0; s < nsys; ++s) {
+        done = done && h[s * NSCAL + 6] == 0.0;
+        iters = std::max(iters, (int)h[s * NSCAL + 7]);
+      }
+      if (done) x.solve_expect[key] = iters;
     }
     pending = slot;
     slot ^= 1;
@@ -1662,7 +1650,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     });
     DFMI_HIP(hipGetLastError());
     Red red = L.after(pR3, 3, 0, hb);
-    Poller poll(x, WS.scal.p, nsys);
+    Poller poll(x, WS.scal.p, nsys, std::string(eqn) + (x.ws_is_y ? "/y" : ""));
     for (int it = 0;; ++it) {
       hx({b.p});
       dispatch_W(W, [&](auto wt) {
@@ -1695,7 +1683,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
       { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_eo_xp, gh, bl, 0, x.stream, Ce, ne, no, rT, WS.scal.p, b, pR); }
       DFMI_HIP(hipGetLastError());
       red = L.after(pR, 2, 0, hb);
-      if ((it + 1) % 2 == 0 && poll.snapshot_and_test()) break;
+      if (poll.after(it)) break;
     }
     hx({b.xw});
     dispatch_W(W, [&](auto wt) {
@@ -1726,8 +1714,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
   });
   DFMI_HIP(hipGetLastError());
   Red red = L.after(pR, 2);
-  Poller poll(x, WS.scal.p, nsys);
-  const int check = 2;
+  Poller poll(x, WS.scal.p, nsys, std::string(eqn) + (x.ws_is_y ? "/y" : ""));
   for (int it = 0;; ++it) {
     const int np1 = spmv_with_halo(x, {b.p}, nsys, Ce, nblk, [&](RowSet rs) {
       dispatch_W(W, [&](auto wt) {
@@ -1752,7 +1739,7 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_bcg_xp, g, bl, 0, x.stream, C, Ce, red_t, q, smap, WS.scal.p, b, pR); }
     DFMI_HIP(hipGetLastError());
     red = L.after(pR, 2, 0);
-    if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
+    if (poll.after(it)) break;
   }
   DFMI_HIP(hipGetLastError());
   record_stats(x, eqn, WS.scal.p, nsys);
@@ -1861,8 +1848,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   };
   Red red_rz, red_rr;
   reds(red_rz, red_rr, nullptr);
-  Poller poll(x, WS.scal.p, 1);
-  const int check = amg ? 2 : 8;
+  Poller poll(x, WS.scal.p, 1, std::string(eqn) + (amg ? "/amg" : "/jacobi"));
   double* pold = v.pa;
   double* pnew = v.pb;
   // one rank: the update kernel also does the V-cycle's level-0 first sweep (DFMI_CG_FUSE=0: separate)
@@ -1901,10 +1887,12 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
       std::swap(v.r, v.z);   // z was dead (k_cg_spmv has read it); the V-cycle writes the new z over the old r
       Red r2 = L.after(q2, 2, 0);
       red_rr = r2; red_rr.p += 1;
-      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, WS.scal.p + 6, true);
+      // the next iteration's stop test runs in the V-cycle's first launch (CgStop): no V-cycle after convergence
+      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, WS.scal.p + 6, true,
+                CgStop{red_rr, WS.scal.p, it + 1, cfg.tol, cfg.abs_tol});
       red_rz = L.after(q3, 1, 1);
       std::swap(pold, pnew);
-      if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
+      if (poll.after(it)) break;
       continue;
     }
     {
@@ -1915,7 +1903,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     DFMI_HIP(hipGetLastError());
     reds(red_rz, red_rr, WS.scal.p + 6);
     std::swap(pold, pnew);
-    if ((it + 1) % check == 0 && poll.snapshot_and_test()) break;
+    if (poll.after(it)) break;
   }
   DFMI_HIP(hipGetLastError());
   record_stats(x, eqn, WS.scal.p, 1);

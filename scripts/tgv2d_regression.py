@@ -23,16 +23,27 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--schemes", default="case", choices=["case", "default"])
     ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--thermo", default="reference", choices=["reference", "fit"],
+                    help="transport table: the reference's thermo_ES80_H2-7-16.txt, or fits regenerated from the YAML "
+                         "by dfmi.transport_fit (what the reference CPU path's Cantera builds at run time)")
     a = ap.parse_args()
     from dfmi import regression as R
     from dfmi.schemes import DEFAULT
     golden = os.path.join(ROOT, "tests", "golden")
     lib = os.path.join(ROOT, "baseline", "cpu_a", "libdfmi_cpu_a.so") if a.lib == "cpu_a" else None
     kw = {} if a.schemes == "case" else {"schemes": dict(DEFAULT)}
+    if a.thermo == "fit":
+        import tempfile
+        from dfmi.mech import read_yaml_mechanism, write_thermo_table
+        from dfmi.transport_fit import fit_mechanism
+        tab = os.path.join(tempfile.mkdtemp(), "thermo_ES80_fit.txt")
+        write_thermo_table(tab, fit_mechanism(read_yaml_mechanism(os.path.join(golden, "ES80_H2-7-16.yaml"))))
+        kw["thermo_table"] = tab
     t0 = time.time()
     out = R.run_tgv2d(os.path.join(golden, "tgv2d"), golden, steps=a.steps, lib_path=lib,
                       log=lambda s: print(f"[{time.time() - t0:6.1f}s] {s}", flush=True), **kw)
     res = {"case": "test/dfLowMachFoam/twoD_reactingTGV/H2/cvodeSolver", "lib": a.lib, "schemes": a.schemes,
+           "thermo": a.thermo,
            "wall_s": time.time() - t0, "steps": {str(k): v for k, v in out.items()},
            "max_rel_dev": max(abs(v["value"] - v["expected"]) / v["expected"] for v in out.values())}
     print(json.dumps(res))
