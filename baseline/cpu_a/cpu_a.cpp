@@ -1052,6 +1052,13 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) { return guard([&] { require_ready
 int dfmi_sync(dfmi_ctx*) { return 0; }
 // no device events on the CPU: the bench times CPU-A with host clocks
 int dfmi_step_timer(dfmi_ctx*, int) { return 0; }
+// CPU-A runs one fixed configuration (the GPU path's defaults: AMG omega 0.9, over-correction 1.35, ...)
+int dfmi_set_option(dfmi_ctx*, const char* key, double) {
+  return guard([&] { throw Error(std::string("dfmi (CPU-A): option '") + key + "' is not configurable here"); });
+}
+int dfmi_get_option(dfmi_ctx*, const char* key, double*) {
+  return guard([&] { throw Error(std::string("dfmi (CPU-A): option '") + key + "' is not configurable here"); });
+}
 int dfmi_step_times(dfmi_ctx*, double*, int, int* got) { if (got) *got = 0; return 0; }
 int dfmi_hbm_copy_peak(dfmi_ctx*, double, int, double*) { return guard([&] { throw Error("dfmi (CPU-A): no device memory"); }); }
 

@@ -720,7 +720,9 @@ def main():
 
     ncls = ctx.row_classes()
     hexd = ctx.hex_dims()
-    hexw = hexd[0] > 0 and os.environ.get("DFMI_FACE_HEX", "1") != "0"
+    opt_face_hex = ctx.get_option("fv.hex_walk") != 0 and ctx.get_option("fv.csr_walk") == 0
+    opt_face_form = ctx.get_option("pcg.face_form") != 0
+    hexw = hexd[0] > 0 and opt_face_hex
     cells_total = m.n_cells * world
     value = cells_total * args.steps / el
     # HBM bytes per launch from the PMC passes committed under profiles/ (scripts/pmc_traffic.sh +
@@ -775,7 +777,7 @@ def main():
         per_unit = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc)
         per_impl = algorithmic_bytes(k, m.n_cells, m.n_faces, m.n_boundary_slots, table.S, Bc, classes=ncls > 0,
                                      hex_walk=hexw, face_form=hexw and world == 1
-                                     and os.environ.get("DFMI_P_FACEFORM", "1") != "0")
+                                     and opt_face_form)
         total_bytes = per_unit * units[k]
         total_impl = per_impl * units[k]
         if k in ("k_bcg_spmv", "k_bcg_eo"):   # U's three components share one operator: its bytes count once per three systems

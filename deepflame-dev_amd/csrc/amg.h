@@ -21,10 +21,10 @@ struct AmgLevel {
   DevBuf<float> fr2;
 };
 
-// Precision of the V-cycle. fp32 (default) keeps every level's operator and work vectors in single
+// Precision of the V-cycle (amg.precision). fp32 (default) keeps every level's operator and work vectors in single
 // precision (AmgX's mixed mode: preconditioner in float, Krylov iteration in double); the outer PCG
 // residuals, dot products and solution stay fp64, so the attainable accuracy is unchanged and only
-// the preconditioner's HBM traffic halves. DFMI_AMG_PREC=f64 keeps the whole hierarchy in double.
+// the preconditioner's HBM traffic halves. amg.precision = 64 keeps the whole hierarchy in double.
 struct Amg {
   bool ready = false;
   bool fp32 = true;
@@ -34,10 +34,9 @@ struct Amg {
   int l0_sweeps = 1;       // weighted-Jacobi sweeps before and after the coarse correction on level 0
   bool padded = false;     // levels 1 .. L-2 in aligned groups of 8 per aggregate (pad_levels)
   bool tail = false;       // levels L-2 and L-1 of the fp32 V-cycle in one workgroup (k_vtail)
-  int fused_coarse = 0;   // smoothing + residual + restriction in one kernel: 1 levels >= 1, 2 all, 0 none
   int coarsest = 4096;
   std::vector<AmgLevel> lv;
-  // Agglomerated coarsest level (several ranks; DFMI_AMG_GLOBAL=1, off by default: measured no fewer
+  // Agglomerated coarsest level (several ranks; amg.global_coarse = 1, off by default: measured no fewer
   // p-iterations). The rank-local hierarchies stop at
   // coarsest / nranks cells; every rank's coarsest cells are gathered into ONE global level of ng = nranks x
   // nmax cells (rank r's cell I at r nmax + I, padding rows with a unit diagonal) whose operator includes the
@@ -45,7 +44,7 @@ struct Amg {
   // Per solve the ranks all-gather their packed rows; per V-cycle their coarsest right-hand sides, and every
   // rank smooths the identical global level redundantly (k_coarsest) -- the role of AmgX's consolidated
   // coarse levels (src_gpu/AmgXSolver.cu:184-266) in place of block-Jacobi across ranks.
-  // level 0 with its processor couplings (several ranks; DFMI_AMG_HALO_L0=0: off): the first sweep's residual and
+  // level 0 with its processor couplings (several ranks; amg.halo_l0 = 0: off): the first sweep's residual and
   // the post-sweep include the halo columns (the PCG residual and diagonal exchanged, the prolongated
   // correction exchanged before the post-sweep) instead of dropping them (block-Jacobi)
   bool halo_l0 = false;
@@ -65,16 +64,6 @@ struct Amg {
   DevBuf<double> g_bs, g_bg;              // coarsest right-hand side: own nmax, all ng
   DevBuf<double> g_val, g_D, g_x;         // global operator / solution in the V-cycle precision (f64 ...)
   DevBuf<float> g_fval, g_fD, g_fx;       // (... or f32)
-  // the V-cycle's launches captured once per (operands, precision) and replayed as one graph launch
-  // (DFMI_AMG_GRAPH=0: direct launches); not used while kernel timers are armed
-  bool use_graph = false;
-  int coop_blocks = 0;   // > 0: levels >= 1 of the V-cycle run as one cooperative launch of this many blocks
-  std::map<std::array<uintptr_t, 8>, hipGraphExec_t> graphs;
-  void clear_graphs() {
-    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
-    graphs.clear();
-  }
-  ~Amg() { clear_graphs(); }
 };
 
 // The hierarchy as plain pointers (one workgroup runs the whole V-cycle of a small system in

@@ -21,7 +21,6 @@
 #include "dfmi_ctx.h"
 #include "amg.h"
 #include "amg_graph.h"
-#include <hip/hip_cooperative_groups.h>
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -93,35 +92,7 @@ __global__ void __launch_bounds__(TPB) k_smooth_res(int n, int W_, ColView col,
   r[c] = bc - y;
 }
 
-// coarse levels (latency-bound): the first smoothing sweep from zero, the residual and its restriction
-// in one pass over the aggregates -- thread I owns coarse cell I, visits its fine members v in order
-// (x_v = omega b_v / D_v stored for the prolongation; a neighbour's x_j re-formed from b_j / D_j) and
-// sums their residuals: the same arithmetic, in the same order, as k_smooth_res + k_restrict
-template <class T, class TB>
-__global__ void __launch_bounds__(TPB) k_smooth_restrict(int nc, const int* __restrict__ mstart,
-                                                         const int* __restrict__ members, int n, int W,
-                                                         const int* __restrict__ col, const T* __restrict__ val,
-                                                         const T* __restrict__ D, const TB* __restrict__ b, T omega,
-                                                         T* __restrict__ x, T* __restrict__ bc, const double* act) {
-  const int I = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I >= nc || (act && *act == 0.0)) return;
-  T a = 0;
-  for (int e = mstart[I]; e < mstart[I + 1]; ++e) {
-    const int v = members[e];
-    const T bv = (T)b[v];
-    const T xv = omega * bv / D[v];
-    T y = D[v] * xv;
-    for (int k = 0; k < W; ++k) {
-      const int j = col[(long)k * n + v];
-      if (j < n) y += val[(long)k * n + v] * (omega * (T)b[j] / D[j]);
-    }
-    x[v] = xv;
-    a += bv - y;
-  }
-  bc[I] = a;
-}
-
-// a further level-0 pre-sweep on (x, r = b - A x): x += omega r / D, r' = r - A (omega r / D)
+// a further level-0 pre-sweep (amg.presweeps > 1): x += omega r / D, r_new = r - A (omega r / D)
 template <int WT, class T>
 __global__ void __launch_bounds__(TPB) k_smooth_step(int n, int W_, ColView col,
                                                      const T* __restrict__ val, const T* __restrict__ D,
@@ -527,107 +498,6 @@ __global__ void k_gc_bpack(int nmax, int nloc, const T* __restrict__ b, double* 
   if (I < nmax) out[I] = I < nloc ? (double)b[I] : 0.0;
 }
 
-// ---------------------------------------------------------------- coarse levels in one launch
-// Levels 1 .. L-1 of the V-cycle (down sweeps + restrictions, the coarsest solve, up sweeps) as ONE
-// cooperative kernel: a grid of one 1024-thread block per CU walks each level's cells in grid-stride
-// order and meets at a grid barrier between dependent phases, instead of a chain of 4-8 us launches
-// (the coarse levels are latency-bound: 13 launches per V-cycle, ~2 ms per step). Per phase the
-// arithmetic is k_smooth_res / k_restrict / k_coarsest / k_prolong_smooth's, in the same order, so
-// the V-cycle's result is bitwise the launch-chain's. The corrected x of level l >= 1 goes to xo[l].
-constexpr int PL = 10;
-template <class T> struct CoarseArgs {
-  int L;
-  int n[PL], W[PL];
-  const int* col[PL];
-  const T* val[PL];
-  const T* D[PL];
-  T* b[PL];
-  T* x[PL];
-  T* r[PL];
-  T* xo[PL];
-  const int* agg[PL];
-  const int* mstart[PL];
-  const int* members[PL];
-  T omega, sc;
-  int sweeps;
-  const double* act;
-};
-
-template <class T>
-__global__ void __launch_bounds__(CTPB) k_amg_coarse(CoarseArgs<T> a) {
-  if (a.act && *a.act == 0.0) return;   // uniform over the grid: no block reaches a barrier alone
-  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
-  const T om = a.omega;
-  for (int l = 1; l + 1 < a.L; ++l) {   // down: one sweep from zero + residual, then restriction
-    const int n = a.n[l], W = a.W[l];
-    const int* col = a.col[l];
-    const T *val = a.val[l], *D = a.D[l], *b = a.b[l];
-    for (int c = tid; c < n; c += nth) {
-      const T bc = b[c];
-      const T xc = om * bc / D[c];
-      T y = D[c] * xc;
-      for (int k = 0; k < W; ++k) {
-        const int j = col[(long)k * n + c];
-        if (j < n) y += val[(long)k * n + c] * (om * b[j] / D[j]);
-      }
-      a.x[l][c] = xc;
-      a.r[l][c] = bc - y;
-    }
-    grid.sync();
-    const int nc = a.n[l + 1];
-    for (int I = tid; I < nc; I += nth) {
-      T s = 0;
-      for (int e = a.mstart[l][I]; e < a.mstart[l][I + 1]; ++e) s += a.r[l][a.members[l][e]];
-      a.b[l + 1][I] = s;
-    }
-    grid.sync();
-  }
-  if (blockIdx.x == 0) {   // coarsest: weighted-Jacobi sweeps from zero, LDS-resident (k_coarsest)
-    __shared__ T xa[COARSEST], xb[COARSEST];
-    __shared__ T sv[LDS_ENT];
-    __shared__ int sc_[LDS_ENT];
-    __shared__ T sd[COARSEST], sb[COARSEST];
-    const int l = a.L - 1, n = a.n[l], W = a.W[l];
-    for (int e = threadIdx.x; e < n * W; e += CTPB) { sv[e] = a.val[l][e]; sc_[e] = a.col[l][e]; }
-    for (int c = threadIdx.x; c < n; c += CTPB) { sd[c] = a.D[l][c]; sb[c] = a.b[l][c]; xa[c] = om * a.b[l][c] / a.D[l][c]; }
-    __syncthreads();
-    T* cur = xa;
-    T* nxt = xb;
-    for (int s = 1; s < a.sweeps; ++s) {
-      for (int c = threadIdx.x; c < n; c += CTPB) {
-        T y = sd[c] * cur[c];
-        for (int k = 0; k < W; ++k) {
-          const int j = sc_[k * n + c];
-          if (j < n) y += sv[k * n + c] * cur[j];
-        }
-        nxt[c] = cur[c] + om * (sb[c] - y) / sd[c];
-      }
-      __syncthreads();
-      T* t = cur; cur = nxt; nxt = t;
-    }
-    for (int c = threadIdx.x; c < n; c += CTPB) a.x[l][c] = cur[c];
-  }
-  grid.sync();
-  for (int l = a.L - 2; l >= 1; --l) {   // up: prolongate the scaled coarse correction + one sweep
-    const int n = a.n[l], W = a.W[l];
-    const int* col = a.col[l];
-    const int* agg = a.agg[l];
-    const T *val = a.val[l], *D = a.D[l], *b = a.b[l], *x = a.x[l];
-    const T* xc = l + 1 == a.L - 1 ? a.x[l + 1] : a.xo[l + 1];
-    for (int c = tid; c < n; c += nth) {
-      const T yc = x[c] + a.sc * xc[agg[c]];
-      T ay = D[c] * yc;
-      for (int k = 0; k < W; ++k) {
-        const int j = col[(long)k * n + c];
-        if (j < n) ay += val[(long)k * n + c] * (x[j] + a.sc * xc[agg[j]]);
-      }
-      a.xo[l][c] = yc + om * (b[c] - ay) / D[c];
-    }
-    if (l > 1) grid.sync();
-  }
-}
-
 // ---------------------------------------------------------------- host: hierarchy
 // (aggregation in amg_graph.h, shared with the CPU-A baseline; here the result is uploaded)
 void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLevel& c, std::vector<int>& ccol,
@@ -646,7 +516,6 @@ void build_next(AmgLevel& f, const std::vector<int>& fcol, const Graph& g, AmgLe
   c.col.upload(ccol, st);
 }
 
-double env_d(const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; }
 
 // Levels 1 .. L-2 renumbered so that the (at most 8) members of every aggregate sit in one aligned group
 // of 8 consecutive cells: level l's cell of parent J, sibling m (members in their previous order) gets
@@ -823,33 +692,13 @@ void global_setup(Ctx& x, const std::vector<int>& col0, const std::vector<std::v
 
 void amg_setup(Ctx& x) {
   Amg& a = x.amg;
-  a.clear_graphs();
   a.lv.clear();
-  a.use_graph = env_d("DFMI_AMG_GRAPH", 0) != 0;
-  a.coop_blocks = 0;
-  // measured: 19.6 -> 26.4 ms/step (grid barriers cost more than the launches they replace); DFMI_AMG_COOP=1
-  if (env_d("DFMI_AMG_COOP", 0) != 0) {   // one co-resident 1024-thread block per CU (cooperative launch)
-    int dev = 0, coop = 0, ncu = 0, per_cu = 0;
-    DFMI_HIP(hipGetDevice(&dev));
-    DFMI_HIP(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
-    DFMI_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const void* k = a.fp32 ? (const void*)k_amg_coarse<float> : (const void*)k_amg_coarse<double>;
-    DFMI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, CTPB, 0));
-    if (coop && per_cu >= 1) a.coop_blocks = ncu;
-  }   // measured: 19.5 -> 19.9 ms/step with graphs (GPU-side latency, not host launches, bounds the coarse levels)
-  a.omega = env_d("DFMI_AMG_OMEGA", 0.9);   // 0.85 -> 0.9: p-iterations 13 -> 12 (one rank), 14.2 -> 13.7 (8 ranks)
-  a.coarse_sweeps = (int)env_d("DFMI_AMG_COARSE_SWEEPS", 8);
-  a.l0_sweeps = std::max(1, (int)env_d("DFMI_AMG_L0_SWEEPS", 1));
-  a.coarsest = std::min(COARSEST, std::max(8, (int)env_d("DFMI_AMG_COARSEST", 512)));
-  a.overcorr = env_d("DFMI_AMG_OVERCORR", 1.35);
-  // fused smoothing + restriction per level: measured slower (19.7 -> 21.8 ms/step with levels >= 1 fused,
-  // 22.2 with all): one thread per aggregate walks 8 members' rows serially -- 8x less parallelism on
-  // levels that are latency-bound already. Off by default, DFMI_AMG_FUSED=1/2 to re-measure.
-  a.fused_coarse = (int)env_d("DFMI_AMG_FUSED", 0);
-  {
-    const char* pe = std::getenv("DFMI_AMG_PREC");
-    a.fp32 = !(pe && std::string(pe) == "f64");
-  }
+  a.omega = x.opt("amg.omega");
+  a.coarse_sweeps = (int)x.opt("amg.coarsest_sweeps");
+  a.l0_sweeps = std::max(1, (int)x.opt("amg.presweeps"));
+  a.coarsest = std::min(COARSEST, std::max(8, (int)x.opt("amg.coarsest_size")));
+  a.overcorr = x.opt("amg.overcorrection");
+  a.fp32 = x.opt("amg.precision") != 64;
   const int C = x.C;
   // level 0: the solver ELL (columns >= C are halo entries, dropped in the preconditioner)
   std::vector<int> col((size_t)x.ell.W * C);
@@ -884,8 +733,7 @@ void amg_setup(Ctx& x) {
   std::vector<int> fcol = col;
   std::vector<std::vector<int>> aggs;   // host copies of each level's fine -> coarse map
   // several ranks: the rank-local levels stop at coarsest / nranks cells, below them the agglomerated level
-  const bool want_global = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_GLOBAL", 0) != 0 && !a.use_graph &&
-                           a.coop_blocks == 0;
+  const bool want_global = x.nranks > 1 && halo_active(x) && x.on("amg.global_coarse");
   const int cap = want_global ? std::max(8, a.coarsest / x.nranks) : a.coarsest;
   auto too_big = [&](const AmgLevel& l) { return l.n > cap || (size_t)l.n * l.W > 6144; };
   while (too_big(a.lv.back())) {
@@ -893,7 +741,7 @@ void amg_setup(Ctx& x) {
     std::vector<int> ccol;
     Graph cg;
     aggs.emplace_back();
-    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, a.lv.size() == 1 ? (int)env_d("DFMI_AMG_L0_PASSES", 3) : (int)env_d("DFMI_AMG_LN_PASSES", 3),
+    build_next(a.lv.back(), fcol, g, c, ccol, cg, x.stream, (int)x.opt(a.lv.size() == 1 ? "amg.pairwise_passes_l0" : "amg.pairwise_passes"),
                aggs.back());
     DFMI_HIP(hipStreamSynchronize(x.stream));
     const bool stalled = c.n * 2 > a.lv.back().n;
@@ -907,7 +755,7 @@ void amg_setup(Ctx& x) {
   a.global = false;
   std::vector<std::vector<int>> fin_aggs = aggs;
   std::vector<int> last_col = fcol;
-  if (env_d("DFMI_AMG_PADDED", 1) != 0) pad_levels(x, col, aggs, fin_aggs, last_col);
+  if (x.on("amg.padded")) pad_levels(x, col, aggs, fin_aggs, last_col);
   if (a.lv.size() == 1) a.fp32 = false;   // a single level writes z directly: keep it in double
   for (size_t l = 0; l < a.lv.size(); ++l) {
     AmgLevel& v = a.lv[l];
@@ -926,17 +774,15 @@ void amg_setup(Ctx& x) {
   }
   if (want_global) global_setup(x, col, fin_aggs, last_col);
   // measured (in-process ranks of 64^3): p-iterations per solve 14 / 17 / 19 -> 12 / 14 / 14-15 for 2 / 4 / 8
-  // ranks (one rank: 12) for two more halo exchanges per PCG iteration; DFMI_AMG_HALO_L0=0: block-Jacobi
-  a.halo_l0 = x.nranks > 1 && halo_active(x) && env_d("DFMI_AMG_HALO_L0", 1) != 0 && a.lv.size() >= 2 &&
-              a.l0_sweeps == 1 && a.fused_coarse == 0 && a.coop_blocks == 0 && !a.use_graph;
+  // ranks (one rank: 12) for two more halo exchanges per PCG iteration; amg.halo_l0 = 0: block-Jacobi
+  a.halo_l0 = x.nranks > 1 && halo_active(x) && x.on("amg.halo_l0") && a.lv.size() >= 2 && a.l0_sweeps == 1;
   if (a.halo_l0) a.hy.alloc((size_t)C + x.H);
-  // the last two levels as one single-workgroup launch (k_vtail; DFMI_AMG_TAIL=0: the launch chain)
+  // the last two levels as one single-workgroup launch (k_vtail; amg.tail = 0: the launch chain)
   {
     const int L = (int)a.lv.size();
-    a.tail = env_d("DFMI_AMG_TAIL", 1) != 0 && a.padded && a.fp32 && L >= 3 && a.lv[L - 2].n <= TAIL_N &&
+    a.tail = x.on("amg.tail") && a.padded && a.fp32 && L >= 3 && a.lv[L - 2].n <= TAIL_N &&
              a.lv[L - 2].n % 8 == 0 && a.lv[L - 2].W <= TAIL_W && a.lv[L - 1].n <= COARSEST &&
-             (size_t)a.lv[L - 1].n * a.lv[L - 1].W <= LDS_ENT && !a.global && a.coop_blocks == 0 &&
-             a.fused_coarse == 0;
+             (size_t)a.lv[L - 1].n * a.lv[L - 1].W <= LDS_ENT && !a.global;
   }
   a.ready = true;
 }
@@ -1029,43 +875,6 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   auto XV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fx.p; else return a.lv[l].x.p; };
   auto RV = [&](int l) -> T* { if constexpr (F) return a.lv[l].fr.p; else return a.lv[l].r.p; };
   auto XO = [&](int l) -> T* { if constexpr (F) return a.lv[l].fxo.p; else return a.lv[l].xo.p; };
-  if (a.coop_blocks > 0 && L >= 3 && !a.fused_coarse) {   // level 0 by launches, levels >= 1 in one
-    AmgLevel& f = a.lv[0];
-    const dim3 g(blocks_for(f.n, TPB));
-    {
-      KScope _ks(x, "k_smooth_res");
-      launch_w(f.W, g, x.stream, k_smooth_res<0, T, double>, k_smooth_res<6, T, double>, f.n, f.W, COL(0), VAL(0),
-               DD(0), r, om, XV(0), RV(0), act, FaceOp<T>{});
-    }
-    {
-      KScope _ks(x, "k_restrict");
-      hipLaunchKernelGGL(k_restrict<T>, dim3(blocks_for(a.lv[1].n, TPB)), dim3(TPB), 0, x.stream, a.lv[1].n,
-                         f.mstart.p, f.members.p, (const T*)RV(0), BV(1), act);
-    }
-    CoarseArgs<T> ca{};
-    ca.L = L;
-    for (int l = 1; l < L; ++l) {
-      AmgLevel& v = a.lv[l];
-      ca.n[l] = v.n; ca.W[l] = v.W; ca.col[l] = RAW(l); ca.val[l] = VAL(l); ca.D[l] = DD(l);
-      ca.b[l] = BV(l); ca.x[l] = XV(l); ca.r[l] = RV(l); ca.xo[l] = XO(l);
-      ca.agg[l] = v.agg.p; ca.mstart[l] = v.mstart.p; ca.members[l] = v.members.p;
-    }
-    ca.omega = om; ca.sc = sc; ca.sweeps = a.coarse_sweeps; ca.act = act;
-    {
-      KScope _ks(x, "k_amg_coarse");
-      void* args[] = {&ca};
-      DFMI_HIP(hipLaunchCooperativeKernel((const void*)k_amg_coarse<T>, dim3(a.coop_blocks), dim3(CTPB), args, 0,
-                                          x.stream));
-    }
-    {
-      KScope _ks(x, "k_prolong_smooth");
-      launch_w(f.W, dim3(nblk), x.stream, k_prolong_smooth<0, T, double, double>, k_prolong_smooth<6, T, double, double>,
-               f.n, f.W, COL(0), VAL(0), DD(0), r, (const T*)XV(0), (const int*)f.agg.p,
-               (const T*)(L == 2 ? XV(1) : XO(1)), om, sc, z, partial, act, FaceOp<T>{});
-    }
-    DFMI_HIP(hipGetLastError());
-    return;
-  }
   // the last two levels in one workgroup (k_vtail): the down loop stops above level L - 2
   const bool tail = F && a.tail;
   const int ldown = tail ? L - 2 : L - 1;
@@ -1073,17 +882,6 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   for (int l = 0; l < ldown; ++l) {
     AmgLevel& f = a.lv[l];
     const dim3 g(blocks_for(f.n, TPB));
-    if ((l > 0 && a.fused_coarse >= 1) || a.fused_coarse >= 2) {   // one launch per level instead of two
-      KScope _ks(x, "k_smooth_restrict");
-      const dim3 gc(blocks_for(a.lv[l + 1].n, TPB));
-      if (l == 0)
-        hipLaunchKernelGGL((k_smooth_restrict<T, double>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
-                           f.members.p, f.n, f.W, RAW(0), VAL(0), DD(0), r, om, XV(0), BV(1), act);
-      else
-        hipLaunchKernelGGL((k_smooth_restrict<T, T>), gc, dim3(TPB), 0, x.stream, a.lv[l + 1].n, f.mstart.p,
-                           f.members.p, f.n, f.W, RAW(l), VAL(l), DD(l), (const T*)BV(l), om, XV(l), BV(l + 1), act);
-      continue;
-    }
     if (l > 0 && a.padded) {   // aggregates in aligned groups of 8: smoothing and restriction in one launch
       KScope _ks(x, "k_smooth_res");
       launch_w(f.W, g, x.stream, k_smooth_res_r8<0, T>, k_smooth_res_r8<6, T>, f.n, f.W, RAW(l), VAL(l), DD(l),
@@ -1243,8 +1041,7 @@ AmgView<double> amg_view_f64(Ctx& x, const double* val0, const double* D0, const
 
 bool amg_l0_fusable(const Ctx& x) {
   const Amg& a = x.amg;
-  return a.fp32 && a.lv.size() >= 2 && a.l0_sweeps == 1 && a.fused_coarse == 0 &&
-         !(a.coop_blocks > 0 && a.lv.size() >= 3);
+  return a.fp32 && a.lv.size() >= 2 && a.l0_sweeps == 1;
 }
 
 void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const double* r, double* z,
@@ -1252,25 +1049,8 @@ void amg_apply(Ctx& x, const double* val0, const double* D0, ColView col0, const
   Amg& a = x.amg;
   DFMI_CHECK(!l0_done || amg_l0_fusable(x), "AMG: level-0 sweep fused on an unsupported configuration");
   CommTag _ct(x, x.comm.tag + " amg");
-  auto direct = [&] {
-    if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
-    else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
-  };
-  if (!a.use_graph || !x.ktimer.targets.empty() || stop.scal) { direct(); return; }
-  const std::array<uintptr_t, 8> key{(uintptr_t)val0, (uintptr_t)D0, (uintptr_t)col0.col, (uintptr_t)r, (uintptr_t)z,
-                                     (uintptr_t)partial, (uintptr_t)nblk * 2 + (l0_done ? 1 : 0), (uintptr_t)active};
-  auto it = a.graphs.find(key);
-  if (it == a.graphs.end()) {
-    hipGraph_t g;
-    DFMI_HIP(hipStreamBeginCapture(x.stream, hipStreamCaptureModeThreadLocal));
-    try { direct(); } catch (...) { (void)hipStreamEndCapture(x.stream, &g); throw; }
-    DFMI_HIP(hipStreamEndCapture(x.stream, &g));
-    hipGraphExec_t e;
-    DFMI_HIP(hipGraphInstantiate(&e, g, nullptr, nullptr, 0));
-    DFMI_HIP(hipGraphDestroy(g));
-    it = a.graphs.emplace(key, e).first;
-  }
-  DFMI_HIP(hipGraphLaunch(it->second, x.stream));
+  if (a.fp32) apply_t<float>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
+  else apply_t<double>(x, val0, D0, col0, r, z, partial, nblk, active, l0_done, stop);
 }
 
 }  // namespace dfmi

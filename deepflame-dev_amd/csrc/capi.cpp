@@ -967,6 +967,22 @@ int dfmi_hex_dims(dfmi_ctx* ctx, int* nx, int* ny, int* nz) {
   });
 }
 
+int dfmi_set_option(dfmi_ctx* ctx, const char* key, double value) {
+  return guard([&] {
+    Ctx& x = ctx->x;
+    (void)x.opt(key);   // throws for an unknown key
+    const std::string k(key);
+    const bool structural = k.rfind("amg.", 0) == 0 || k == "solver.even_odd" || k == "solver.row_classes";
+    DFMI_CHECK(!structural || (!x.amg.ready && !x.ell.ready),
+               "dfmi_set_option: '" + k + "' shapes the solver structures; set it before the first solve");
+    x.opts[k] = value;
+  });
+}
+
+int dfmi_get_option(dfmi_ctx* ctx, const char* key, double* value) {
+  return guard([&] { *value = ctx->x.opt(key); });
+}
+
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name) {
   return guard([&] {
     std::string e(eqn), n(name);

@@ -8,7 +8,7 @@
 // rates from NASA7 equilibrium constants.
 //
 // Integrator: ROS3 Rosenbrock (L-stable, order 3, embedded order-2 error estimate, one Jacobian and
-// one LU per step) with adaptive step size; alternative (DFMI_CHEM_METHOD=extrap): linearly-implicit
+// one LU per step) with adaptive step size; alternative (option chem.method = 1): linearly-implicit
 // Euler extrapolation with step sequence 1, 2, 3. Analytic Jacobian: mass action, third-body factors and
 // the fall-off rate constants' [M]-dependence (without the latter the stiff 1D-flame cells needed 2-5x
 // more steps: a Rosenbrock method loses order with an inexact Jacobian). Tolerances mirror the reference's CVODE settings (relTol 1e-6, absTol 1e-10 on
@@ -697,7 +697,7 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   const double* rho_rr = x.f(rho_field);
   if (h.fail.n == 0) h.fail.alloc(1);
   DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
-  if (const char* e = std::getenv("DFMI_CHEM_METHOD")) h.method = std::string(e) == "extrap" ? 1 : 0;
+  h.method = (int)x.opt("chem.method");
   const dim3 g((unsigned)blocks_for(x.C, LANES));
   // compiled-in mechanism? (bitwise the same arrays, NASA7 and weights)
   unsigned long long fp = 0xcbf29ce484222325ull;
@@ -709,11 +709,11 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   fp = fnv(fp, x.thermo.nasa.data(), x.thermo.nasa.size() * 8);
   fp = fnv(fp, x.thermo.W.data(), x.thermo.W.size() * 8);
   h.generated = 0;
-  if (!std::getenv("DFMI_CHEM_GENERIC") && h.method == 0) {
+  if (x.on("chem.generated") && h.method == 0) {
     if (fp == ChemGen_burke9::FINGERPRINT) h.generated = 1;
     else if (fp == ChemGen_es80::FINGERPRINT) h.generated = 2;
   }
-  if (const char* e = std::getenv("DFMI_CHEM_BIN")) h.bin = std::atoi(e) != 0;
+  h.bin = x.on("chem.binning");
   const int* perm = nullptr;
   if (h.bin) {
     KScope _ks(x, "k_bin");

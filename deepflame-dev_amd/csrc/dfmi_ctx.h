@@ -147,7 +147,7 @@ struct Chem {
   int max_steps = 100000;
   int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
   int generated = 0;            // last solve used a compiled-in mechanism (chem_gen_*.inc): 1 burke9, 2 es80
-  bool bin = true;              // order cells by the previous solve's step count (DFMI_CHEM_BIN=0: natural order)
+  bool bin = true;              // order cells by the previous solve's step count (option chem.binning = 0: natural order)
   DevBuf<int> perm, bcnt;       // cost-binned cell order; per-block bucket counts / offsets
   std::vector<int> h_idata, h_irs;
   std::vector<double> h_dd;
@@ -218,8 +218,56 @@ struct CommStats {
   ~CommStats() { for (auto e : pool) (void)hipEventDestroy(e); }
 };
 
+// Implementation options (dfmi_set_option; the role the reference's amgx*Options files and
+// CanteraTorchProperties switches play for its solvers): the AMG configuration of the p solver, the solver
+// and face-walk choices, the chemistry integrator. Every key and its default is listed here; an unknown key is
+// an error. They are read when the structure they shape is built (the AMG hierarchy and the solver rows at
+// the first solve) or at each call (everything else).
+struct OptDef { const char* key; double def; };
+inline const OptDef* option_defs(int& n) {
+  static const OptDef d[] = {
+    {"amg.omega", 0.9},               // weighted-Jacobi smoothing weight (0.85 -> 0.9: 13 -> 12 p-iterations)
+    {"amg.overcorrection", 1.35},     // coarse-correction scaling of the plain-aggregation V-cycle
+    {"amg.coarsest_sweeps", 8},       // Jacobi sweeps on the coarsest level (amgxpOptions coarsest_sweeps)
+    {"amg.coarsest_size", 512},       // coarsening stops at this many cells
+    {"amg.presweeps", 1},             // level-0 pre- and post-sweeps (amgxpOptions presweeps / postsweeps)
+    {"amg.pairwise_passes_l0", 3},    // pairwise-matching passes building level 1 (3: 2x2x2 aggregates; SIZE_2 x 3)
+    {"amg.pairwise_passes", 3},       // ... building the levels below
+    {"amg.precision", 32},            // 32: V-cycle in fp32 (AmgX mixed mode), 64: fp64
+    {"amg.padded", 1},                // coarse levels in aligned groups of 8 per aggregate (one launch per level)
+    {"amg.tail", 1},                  // the last two levels in one workgroup launch (k_vtail)
+    {"amg.halo_l0", 1},               // several ranks: level 0 keeps its processor couplings
+    {"amg.global_coarse", 0},         // several ranks: one agglomerated coarsest level
+    {"solver.even_odd", 1},           // U/Y/E: BiCGStab on the even-odd Schur complement where the rows 2-colour
+    {"solver.small", 1},              // one rank, <= 4096 cells: every solve in one workgroup
+    {"solver.row_classes", 1},        // solver rows decoded from one byte per cell where the mesh allows
+    {"pcg.face_form", 1},             // one rank, hex box: the p operator read face-wise
+    {"pcg.fuse_l0", 1},               // the PCG update fused with the V-cycle's level-0 first sweep
+    {"fv.hex_walk", 1},               // hex box in blockMesh order: face and neighbour indices computed
+    {"fv.csr_walk", 0},               // assembly faces walked from the CSR lists instead of the gather rows
+    {"fv.species_generic", 0},        // the species-chunked YEqn kernels at any species count (S > 16 always)
+    {"fv.yprep_brick", 1},            // k_y_prep staging 16x4x4 bricks in LDS (hex walk)
+    {"chem.method", 0},               // 0: ROS3 Rosenbrock, 1: linearly-implicit Euler extrapolation
+    {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
+    {"chem.binning", 1},              // cells launched in cost-binned order
+    {"dnn.tuned_gemm", 1},            // DF-ODENet layers by the shape-tuned kernels (0: k_mlp_gemm for every layer)
+  };
+  n = (int)(sizeof(d) / sizeof(d[0]));
+  return d;
+}
+
 struct Ctx {
   int device = 0;
+  std::map<std::string, double> opts;   // dfmi_set_option overrides
+  double opt(const char* key) const {
+    auto it = opts.find(key);
+    if (it != opts.end()) return it->second;
+    int n;
+    const OptDef* d = option_defs(n);
+    for (int i = 0; i < n; ++i) if (std::string(d[i].key) == key) return d[i].def;
+    throw Error(std::string("dfmi: unknown option '") + key + "'");
+  }
+  bool on(const char* key) const { return opt(key) != 0.0; }
   hipStream_t stream = nullptr;
   // sizes (dfMatrixDataBase::setConstantValues, dfMatrixDataBase.cu:114-147)
   int C = 0, Ctot = 0, F = 0, B = 0, P = 0, S = 0, nproc_faces = 0;
@@ -273,7 +321,6 @@ struct Ctx {
     DevBuf<int> ctab, stab;
     DevBuf<int> csStart, csSlot, scol;   // coupled slots per cell and their columns (FaceOp)
     int ncls = 0;
-    bool fv_classes = false;
     ColView cols() const {
       ColView v;
       v.col = col.p; v.W = W;
@@ -334,9 +381,9 @@ struct Ctx {
     m.cbStart = cbStart; m.cbSlot = cbSlot; m.bfc = bfc; m.partner = partner; m.sprim = sprim;
     m.Sf = Sf; m.magSf = magSf; m.w = w; m.dc = dc; m.V = V; m.bSf = bSf; m.bmagSf = bmagSf; m.bw = bw; m.bdc = bdc;
     m.ecol = ell.col; m.esrc = ell.src; m.W = ell.ready ? ell.W : 0;
-    // the assembly face loops and the ELL fold read explicit rows unless DFMI_ROW_CLASSES_FV=1 (their class
-    // lookups go through the global table: measured slower for these latency-bound gathers)
-    m.ecls = ell.ready && ell.ncls > 0 && ell.fv_classes ? ell.cls.p : nullptr;
+    // the assembly face loops and the ELL fold read explicit rows (class lookups through the global table
+    // measured slower for these latency-bound gathers, round 3)
+    m.ecls = nullptr;
     m.ectab = ell.ctab.p; m.estab = ell.stab.p;
     m.rdt = rdt;
     m.trav = trav.n ? trav.p : nullptr;
@@ -451,7 +498,7 @@ void bicg_layout(Ctx& x, int nsys, double** val, double** dS, double** rhs);
 void build_ell(Ctx& x);   // solver gather rows; also the face lists of the assembly kernels
 void bicg_rows_from_ldu_Y(Ctx& x);
 void bicg_rows_get(Ctx& x, int nsys, const std::string& part, double* host, long count);
-bool species_generic(int S);   // fv_kernels.hip: chunked kernels for S > 16 (or DFMI_SPECIES_GENERIC=1)
+bool species_generic(const Ctx& x);   // fv_kernels.hip: chunked kernels for S > 16 (or the option fv.species_generic)
 // iterations / initial and final relative residual of the last solve of `eqn` (synchronises)
 SolveStats solve_stats(Ctx& x, const std::string& eqn);
 // system-iterations of the solves of `eqn` since the last reset (synchronises)

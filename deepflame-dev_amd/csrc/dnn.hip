@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(256, 2)
 // VALU-bound, plus 10.9 GB of fp16 activations written. So the tile is small enough for four workgroups (16
 // waves) per CU to hide the GELU's dependent transcendental latencies behind one another: 128 x 128 x 64, 4 waves
 // (2 x 2) of 64 x 64 (4 x 4 MFMA blocks), the whole K staged by DMA at once (A and W 128 rows x 128 B each,
-// rows swizzled as in k_mlp_gemm_w), then the output tile staged through the same LDS (35 KiB) and written as
+// rows swizzled as the ping-pong kernel below), then the output tile staged through the same LDS (35 KiB) and written as
 // 16-B row chunks. Same MFMA order per output as k_mlp_gemm (K halves in order), so the same results.
 template <bool GELU, int BMI>
 __global__ void __launch_bounds__(256, BMI == 64 ? 6 : 4)
@@ -367,172 +367,11 @@ __global__ void __launch_bounds__(256, BMI == 64 ? 6 : 4)
   }
 }
 
-// Wide-layer variant (K % 64 == 0, the 1600 -> 800 layer of the DF-ODENet nets): block tile 256 x 256 x 64,
-// 8 waves (2 M x 4 N, each the same 128 x 64 wave tile of 8 x 4 accumulators), one block per CU, 2 x 64 KiB
-// LDS stages. Twice the K depth and twice the N width of k_mlp_gemm per staged byte and per barrier:
-// one barrier per 64-deep K tile, placed in the MIDDLE of the tile's MFMAs. Per tile t each wave
-//   issues its K-half-1 fragment reads of t, runs the 32 MFMAs of K-half 0 (fragments read before),
-//   waits for its own reads of t and its DMAs of t+1, barrier (t+1 visible everywhere, stage t free),
-//   DMAs tile t+2 into stage t, reads K-half 0 of t+1, runs the 32 MFMAs of K-half 1 of t.
-// So the fragment reads after a barrier are covered by 32 MFMAs already in hand, and a tile's DMA has a
-// whole tile of MFMAs to land. 128-B LDS rows (8 chunks of 16 B): chunk c of row r at c ^ ((r >> 1) & 7),
-// which puts each ds_read_b128 lane group ({0-3,12-15,20-27}, ... : rows 0-15 of a 16-row block at two
-// adjacent logical chunks) on 16 distinct 16-B bank slots; DMA pieces are 8 rows x 128 B (1 KiB contiguous,
-// the swizzle applied on the source address).
-template <bool GELU, bool IL>
-__global__ void __launch_bounds__(512, 1)
-    k_mlp_gemm_w(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
-                 long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC) {
-  constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512;
-  constexpr int TILE_A = BMW * BKW, STAGE = TILE_A + BNW * BKW;   // halves: 2 x 32 KiB per stage
-  constexpr int CLD = BNW + 8;
-  constexpr int LDS_H = 2 * STAGE > BMW * CLD ? 2 * STAGE : BMW * CLD;
-  __shared__ __attribute__((aligned(16))) _Float16 lds[LDS_H];
-  const int z = blockIdx.z;
-  A += z * sA; W += z * sW; bias += z * sb; Cout += z * sC;
-  const int ntn = (N + BNW - 1) / BNW, ntm = (M + BMW - 1) / BMW, nwg = ntn * ntm;
-  const int orig = blockIdx.x;
-  const int xcd = orig % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int m0 = (wg / ntn) * BMW, n0 = (wg % ntn) * BNW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // staging: wave w fills A rows and W rows [32 w, 32 w + 32), 8 rows per DMA
-  const _Float16* pa[4];
-  const _Float16* pw[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + (lane >> 3), ch = (lane & 7) ^ ((row >> 1) & 7);
-    pa[i] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
-    pw[i] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    _Float16* la = lds + buf * STAGE;
-    _Float16* lw = la + TILE_A;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(pa[i] + k0, la + (wave * 32 + i * 8) * BKW);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(pw[i] + k0, lw + (wave * 32 + i * 8) * BKW);
-  };
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
-  const int r = lane & 15, g = lane >> 4;
-  // lane's fragment offset inside a 16-row block (rows 16 i + r: (row >> 1) & 7 == r >> 1), per K half
-  const int fo[2] = {r * BKW + ((g) ^ (r >> 1)) * 8, r * BKW + ((4 + g) ^ (r >> 1)) * 8};
-  auto frag_reads = [&](int buf, int kh, half8 (&af)[8], half8 (&bf)[4]) {
-    const _Float16* la = lds + buf * STAGE + fo[kh];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const half8*>(la + TILE_A + (wn + 16 * j) * BKW);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const half8*>(la + (wm + 16 * i) * BKW);
-  };
-  const int nk = K / BKW;
-  // the K loop, specialised on the number of 16-column blocks of this wave that hold output columns (the
-  // padded tail of the last N tile issues no MFMAs): no divergent branch inside the loop, so the compiler's
-  // LDS-read waits stay counted (a merge of paths with different outstanding reads makes them lgkmcnt(0))
-  auto kloop = [&](auto jl_c) {
-    constexpr int JL = decltype(jl_c)::value;
-    auto mfmas = [&](const half8 (&af)[8], const half8 (&bf)[4]) {
-#pragma unroll
-      for (int j = 0; j < JL; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    };
-    // pieces of the above for the interleaved schedule: MFMAs q0, q0 + 1 (q -> column block q / 8, row block
-    // q % 8), one fragment read (B blocks first), one DMA piece (A rows, then W rows)
-    auto mfma_pair = [&](const half8 (&af)[8], const half8 (&bf)[4], int q0) {
-#pragma unroll
-      for (int q = q0; q < q0 + 2; ++q)
-        if (q / 8 < JL) acc[q % 8][q / 8] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[q % 8], bf[q / 8], acc[q % 8][q / 8], 0, 0, 0);
-    };
-    auto frag_one = [&](int buf, int kh, int q, half8 (&af)[8], half8 (&bf)[4]) {
-      const _Float16* la = lds + buf * STAGE + fo[kh];
-      if (q < 4) bf[q] = *reinterpret_cast<const half8*>(la + TILE_A + (wn + 16 * q) * BKW);
-      else af[q - 4] = *reinterpret_cast<const half8*>(la + (wm + 16 * (q - 4)) * BKW);
-    };
-    auto stage_piece = [&](int buf, int k0, int p) {
-      _Float16* la = lds + buf * STAGE;
-      if (p < 4) glds16(pa[p] + k0, la + (wave * 32 + p * 8) * BKW);
-      else glds16(pw[p - 4] + k0, la + TILE_A + (wave * 32 + (p - 4) * 8) * BKW);
-    };
-    // no scalar (kernel-argument) load left outstanding into the loop: with one pending, the compiler can only
-    // wait lgkmcnt(0), which would also wait for the K-half-1 reads issued before the K-half-0 MFMAs
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (nk > 1) stage(1, BKW);
-    half8 a0[8], b0[4], a1[8], b1[4];
-    frag_reads(0, 0, a0, b0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      // K-half 0's reads (issued a K half of MFMAs ago) are done: waiting for them BEFORE issuing the next
-      // 12 (the LGKM counter holds 15) lets the K-half-0 MFMAs start with the K-half-1 reads in flight
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-      if constexpr (!IL) frag_reads(cur, 1, a1, b1);
-      if constexpr (IL) {   // one read between every two MFMAs (the reads' issue hidden among them)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (q < 12) frag_one(cur, 1, q, a1, b1);
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_pair(a0, b0, 2 * q);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(a0, b0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // my reads of tile kt retired, my DMAs of tile kt+1 landed; after the barrier: everyone's
-      __builtin_amdgcn_s_waitcnt(0);        // vmcnt(0) lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (IL) {
-        // the two tiles past the end re-stage the last tile (in bounds, never read; drained before the epilogue)
-        // so the region has no branch and the 8 DMAs and 12 reads interleave with the 32 MFMAs
-        const int kn = min(kt + 2, nk - 1) * BKW;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (q < 8) stage_piece(cur, kn, q);
-          if (q < 12) frag_one(cur ^ 1, 0, q, a0, b0);
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_pair(a1, b1, 2 * q);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        if (kt + 2 < nk) stage(cur, (kt + 2) * BKW);
-        frag_reads(cur ^ 1, 0, a0, b0);   // unconditional (the last tile's reads hit a stale stage, unused)
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(a1, b1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_s_waitcnt(0);   // no DMA in flight into the LDS the epilogue reuses
-  };
-  switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
-    case 4: kloop(std::integral_constant<int, 4>{}); break;
-    case 3: kloop(std::integral_constant<int, 3>{}); break;
-    case 2: kloop(std::integral_constant<int, 2>{}); break;
-    case 1: kloop(std::integral_constant<int, 1>{}); break;
-    default: kloop(std::integral_constant<int, 0>{}); break;
-  }
-  // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
-  __syncthreads();
-  _Float16* cs = lds;
-  stage_out_tile<GELU, CLD>(acc, cs, wm, wn, n0, N, bias, lane);
-  __syncthreads();
-#pragma unroll 4
-  for (int it = 0; it < BMW * BNW / 8 / NT; ++it) {
-    const int idx = tid + it * NT, rl = idx / (BNW / 8), ch = idx % (BNW / 8);
-    const int row = m0 + rl, col = n0 + ch * 8;
-    if (row < M && col < ldc)
-      *reinterpret_cast<half8*>(Cout + (long)row * ldc + col) = *reinterpret_cast<const half8*>(cs + rl * CLD + ch * 8);
-  }
-}
+// 128-B LDS rows (8 chunks of 16 B): chunk c of row r at c ^ ((r >> 1) & 7), which puts each ds_read_b128 lane
+// group ({0-3,12-15,20-27}, ... : rows 0-15 of a 16-row block at two adjacent logical chunks) on 16 distinct 16-B
+// bank slots; DMA pieces are 8 rows x 128 B (1 KiB contiguous, the swizzle applied on the source address).
+// (Round 5: the single-group 256 x 256 x 64 variants, 9.77 / 10.07 ms per chunk against the ping-pong kernel's
+// 8.72, are removed.)
 
 // Ping-pong variant of the wide-layer GEMM (the guide's 256x256 eight-phase schedule, cdna_hip_programming.md
 // section 5): the same 256 x 256 x 64 tile and 8 waves, but each 64-deep K tile runs as four phases, one per
@@ -564,8 +403,7 @@ template <bool GELU, bool OUT = false, int TS = 0>
 __global__ void __launch_bounds__(512, 1)
     k_mlp_gemm_pp(int M, int N, int K, const _Float16* __restrict__ A, int lda, long sA, const _Float16* __restrict__ W,
                   long sW, const float* __restrict__ bias, long sb, _Float16* __restrict__ Cout, int ldc, long sC,
-                  const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0,
-                  int ilv_ok = 1) {
+                  const _Float16* __restrict__ wo = nullptr, long swo = 0, float* __restrict__ P = nullptr, long sP = 0) {
   constexpr bool TAIL = TS > 0;
   static_assert(!(OUT && TAIL) && (TS == 0 || TS == 16 || TS == 32), "tail strips: 16 or 32 columns, no OUT");
   constexpr int BMW = 256, BNW = 256, BKW = 64, NT = 512, TW = TS, NJT = TS / 16, NSTRIP = TAIL ? 32 / TS : 0;
@@ -589,12 +427,6 @@ __global__ void __launch_bounds__(512, 1)
   // DMA sources: half-tile h, piece q: half-row hr = 16 wave + 8 q + (lane >> 3), 16-B chunk lane & 7 of the
   // LDS row holding logical chunk (lane & 7) ^ ((hr >> 1) & 7). A half h < 2: tile row (hr / 64) 128 + 64 h +
   // hr % 64 (rows of both wave rows); W half h = 2 + jh: tile row (hr / 32) 64 + 32 jh + hr % 32 (all columns)
-  // OUT, last tile partially live (N = 400: 144 of 256 columns): its live column blocks interleaved over the four
-  // wave columns (block 4 b + wc in the wave's local block b: 3 / 2 / 2 / 2 live blocks instead of 4 / 4 / 1 / 0),
-  // so that the SIMDs share its MFMAs (waves 4 r + c run on SIMD c); the partial sums stay per 64 consecutive
-  // columns (the activations go through LDS), bitwise the contiguous form
-  const bool ilv = OUT && ilv_ok && n0 + BNW > N;
-  const int nblk = (N - n0 + 15) / 16;   // live 16-column blocks of this tile (> 4 w.r.t. a wave: clamped below)
   const _Float16* src[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
@@ -605,9 +437,7 @@ __global__ void __launch_bounds__(512, 1)
         const int row = (hr >> 6) * 128 + h * 64 + (hr & 63);
         src[h][q] = A + (long)min(m0 + row, M - 1) * lda + ch * 8;   // clamped rows masked on store
       } else {
-        const int lc = (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31);   // the wave-column-major LDS position
-        // interleaved last OUT tile: wave column w's local block b holds tile column block 4 b + w
-        const int row = ilv ? 16 * (4 * ((lc >> 4) & 3) + (lc >> 6)) + (lc & 15) : lc;
+        const int row = (hr >> 5) * 64 + (h - 2) * 32 + (hr & 31);   // the wave-column-major LDS position
         src[h][q] = W + (long)min(n0 + row, N - 1) * K + ch * 8;
       }
     }
@@ -760,7 +590,7 @@ __global__ void __launch_bounds__(512, 1)
     if (tail_tile) kloop(std::integral_constant<int, 4>{}, std::true_type{});
     else kloop(std::integral_constant<int, 4>{}, std::false_type{});
   } else {
-    switch (ilv ? min(4, max(0, (nblk - wc + 3) / 4)) : min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
+    switch (min(4, max(0, (N - (n0 + wn) + 15) / 16))) {
       case 4: kloop(std::integral_constant<int, 4>{}, std::false_type{}); break;
       case 3: kloop(std::integral_constant<int, 3>{}, std::false_type{}); break;
       case 2: kloop(std::integral_constant<int, 2>{}, std::false_type{}); break;
@@ -769,66 +599,7 @@ __global__ void __launch_bounds__(512, 1)
     }
   }
   if constexpr (OUT) {   // the fused output layer (no LDS use: the drained stages are not touched)
-    if (!ilv) {
-      out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
-      return;
-    }
-    // interleaved tile: the fp16 activations of the wave's blocks into LDS, then each wave's partials over its
-    // natural 64 columns from there (the same values and operation order as out_layer_partials)
-    __syncthreads();
-    _Float16* cs = lds;
-    const int g4 = 4 * (lane >> 4);
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int cb = 4 * b + wc;   // tile column block
-      if (cb >= nblk) continue;
-      const int cl = 16 * cb + (lane & 15), col = n0 + cl;
-      const bool live = col < N;
-      const float bv = live ? bias[col] : 0.0f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int rl = wm + 16 * i + g4 + e;
-          f32x2 v = round16(f32x2{acc[i][b][e], acc[i][b][e + 1]} + bv);
-          if (GELU) v = gelu_fast2(v);
-          const half2v h = to16(v);
-          cs[rl * CLD + cl] = h.x;
-          cs[(rl + 1) * CLD + cl] = h.y;
-        }
-    }
-    __syncthreads();
-    float wv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-      wv[j] = col < N ? (float)wo[col] : 0.0f;
-    }
-    float* Pw = P + (long)(4 * (wg % ntn) + wc) * M;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rl = wm + 16 * i + g4 + e;
-        f32x2 sa = {0.0f, 0.0f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (n0 + wn + 16 * j >= N) break;
-          const int cl = wn + 16 * j + (lane & 15);
-          const f32x2 hq = {(float)cs[rl * CLD + cl], (float)cs[(rl + 1) * CLD + cl]};
-          sa = __builtin_elementwise_fma(hq, f32x2(wv[j]), sa);
-        }
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) {
-          sa.x += __shfl_xor(sa.x, off);
-          sa.y += __shfl_xor(sa.y, off);
-        }
-        const int row = m0 + rl;
-        if ((lane & 15) == 0) {
-          if (row < M) Pw[row] = sa.x;
-          if (row + 1 < M) Pw[row + 1] = sa.y;
-        }
-      }
+    out_layer_partials<GELU>(acc, P + (long)(4 * (wg % ntn) + wc) * M, M, m0, wm, wn, n0, N, bias, wo, lane);
     return;
   }
   // epilogue: bias + GELU in registers, the fp16 tile staged through LDS, written back as 16-B row chunks
@@ -1068,23 +839,11 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   d.last_reacting = nr;
   if (nr == 0) return;
   const int chunk = std::min(nr, d.chunk);
-  // the wide layers (K % 64 == 0, N >= 512: the 1600 -> 800 layer) through the 256x256x64 ping-pong kernel
-  // (DFMI_DNN_WIDE=3, default): 8.72 ms per 65,536-row chunk against k_mlp_gemm's 9.66 (DFMI_DNN_WIDE=0);
-  // 1 / 2: the single-group variants, 9.77 / 10.07 ms
-  const int wide = [] { const char* e = std::getenv("DFMI_DNN_WIDE"); return e ? std::atoi(e) : 3; }();   // A/B: 256x256x64 kernel for the wide layers
-  // tail strips of N = 256 q + t (t <= 32) layers: DFMI_DNN_TAIL=16 (default: two 16-column strips in the last two
-  // tiles), 32 (one strip in the last tile; 1 means 32), 0 (a (q+1)-th tile)
-  const int tail_strip = [] {
-    const char* e = std::getenv("DFMI_DNN_TAIL");
-    const int v = e ? std::atoi(e) : 16;
-    return v == 1 ? 32 : (v == 16 || v == 32 ? v : 0);
-  }();
-  // the fused-output layer's partially live last tile with its column blocks interleaved over the wave columns
-  // (DFMI_DNN_OUT_ILV=1; default 0: contiguous)
-  const int out_ilv = [] { const char* e = std::getenv("DFMI_DNN_OUT_ILV"); return e ? std::atoi(e) : 0; }();
-  // K = 64 layers through the 128 x 128 four-blocks-per-CU kernel (DFMI_DNN_IN=1, default); 0: k_mlp_gemm
-  // (2: a 64 x 128 tile, six workgroups per CU)
-  const int in_tile = [] { const char* e = std::getenv("DFMI_DNN_IN"); return e ? std::atoi(e) : 1; }();
+  // the wide layers (K % 64 == 0, N >= 512: the 1600 -> 800 layer) through the 256x256x64 ping-pong kernel (8.72 ms
+  // per 65,536-row chunk against k_mlp_gemm's 9.66), N = 256 q + t (t <= 32) with two 16-column tail strips in the
+  // last two tiles (7.48-7.57 against 7.62-7.64 for one 32-column strip and 8.48 for a (q+1)-th tile); K = 64 layers
+  // (the 55 -> 1600 input layer) through the 128 x 128 four-blocks-per-CU kernel (2.93 against 3.01 ms for a
+  // 64 x 128 tile); DESIGN.md 8
   // activation buffers for one chunk: ping-pong [module][chunk][width]
   size_t wmax = 0;
   for (int l = 1; l < L; ++l) wmax = std::max(wmax, (size_t)d.Kp[l]);
@@ -1102,7 +861,8 @@ void dnn_solve(Ctx& x, const char* rho_field) {
     int lda = d.Kp[0];
     // the last hidden layer by the ping-pong kernel where its K allows (four 64-column partials per 256-wide
     // tile) or by k_mlp_gemm (two per 128-wide tile): partial sums per row of the fused output layer
-    const bool pp_out = wide == 3 && d.Kp[L - 2] % 64 == 0 && d.Kp[L - 2] >= 512;
+    const bool tuned = x.on("dnn.tuned_gemm");
+    const bool pp_out = tuned && d.Kp[L - 2] % 64 == 0 && d.Kp[L - 2] >= 512;
     const int nq = pp_out ? 4 * blocks_for(d.dims[L - 1], 256) : 2 * blocks_for(d.dims[L - 1], BN);
     const long sP = (long)nq * n;
     if (d.part.n < (size_t)d.nmod * sP) d.part.alloc((size_t)d.nmod * sP);
@@ -1117,41 +877,26 @@ void dnn_solve(Ctx& x, const char* rho_field) {
         if (pp_out)
           hipLaunchKernelGGL((k_mlp_gemm_pp<true, true>), dim3(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod),
                              dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
-                             ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1], d.part.p, sP, out_ilv);
+                             ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1], d.part.p, sP);
         else
           hipLaunchKernelGGL((k_mlp_gemm<true, true>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, d.W[L - 1].p, (long)d.Kp[L - 1],
                              d.part.p, sP);
-      } else if (wide && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
+      } else if (tuned && K % 64 == 0 && K >= 512 && N >= 512) {   // the 1600 -> 800 layer
         const dim3 gw(blocks_for(N, 256) * blocks_for(n, 256), 1, d.nmod);
-        // N = 256 q + t, 0 < t <= 32 (the 800-wide layer): q tiles, the last one or two with the tail strips
-        const bool tail = tail_strip > 0 && N % 256 != 0 && N % 256 <= 32 && ldc <= N / 256 * 256 + 64 &&
-                          N / 256 >= 32 / tail_strip;
+        // N = 256 q + t, 0 < t <= 16 q: q tiles, the last two with 16-column tail strips
+        const bool tail = N % 256 != 0 && N % 256 <= 32 && ldc <= N / 256 * 256 + 64 && N / 256 >= 2;
         const dim3 gt(N / 256 * blocks_for(n, 256), 1, d.nmod);
-        if (wide == 3 && tail && tail_strip == 16)
+        if (tail)
           hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, 16>), gt, dim3(512), 0, x.stream, n, N, K, in, lda, sIn,
                              d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
-        else if (wide == 3 && tail)
-          hipLaunchKernelGGL((k_mlp_gemm_pp<true, false, 32>), gt, dim3(512), 0, x.stream, n, N, K, in, lda, sIn,
-                             d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);
-        else if (wide == 3)
+        else
           hipLaunchKernelGGL((k_mlp_gemm_pp<true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                              (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
-        else if (wide == 2)
-          hipLaunchKernelGGL((k_mlp_gemm_w<true, false>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
-        else
-          hipLaunchKernelGGL((k_mlp_gemm_w<true, true>), gw, dim3(512), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
-                             (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc);
-      } else if (in_tile && K == 64) {   // the 55 -> 1600 input layer of the 53-species nets
-        if (in_tile == 2)
-          hipLaunchKernelGGL((k_mlp_gemm_in<true, 64>), dim3(blocks_for(N, 128) * blocks_for(n, 64), 1, d.nmod), dim3(256),
-                             0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out, ldc,
-                             (long)n * ldc);
-        else
-          hipLaunchKernelGGL((k_mlp_gemm_in<true, 128>), dim3(blocks_for(N, 128) * blocks_for(n, 128), 1, d.nmod),
-                             dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
-                             ldc, (long)n * ldc);
+      } else if (tuned && K == 64) {   // the 55 -> 1600 input layer of the 53-species nets
+        hipLaunchKernelGGL((k_mlp_gemm_in<true, 128>), dim3(blocks_for(N, 128) * blocks_for(n, 128), 1, d.nmod),
+                           dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p, (long)N * K, d.b[l].p, (long)N, out,
+                           ldc, (long)n * ldc);
       } else {
         hipLaunchKernelGGL((k_mlp_gemm<true, false>), g, dim3(256), 0, x.stream, n, N, K, in, lda, sIn, d.W[l].p,
                            (long)N * K, d.b[l].p, (long)N, out, ldc, (long)n * ldc, nullptr, 0L, nullptr, 0L);

@@ -1243,312 +1243,7 @@ __global__ void __launch_bounds__(TPB) k_y_prep_brick(MeshView m, const int8_t* 
 // species per staged chunk: all (S <= 5) or about half (LDS 2 SC YNB doubles: 9 species -> 5 = 52 KiB)
 constexpr int ybrick_sc(int S) { return S <= 5 ? S : (S + 1) / 2; }
 
-// k_y_prep on a hex box in blockMesh order, z-marching (2.5D blocking): one ZTX x ZTY column tile of cells
-// per workgroup walks a segment of kz planes, one thread per column. Per plane the tile's Y_s, hai_s and
-// alpha and the plane's face halo (one ring of 2 ZTX + 2 ZTY cells) are staged in LDS once, so every cell
-// value is read from HBM once (plus the ring, shared in L2 with the tiles beside it that the XCD runs at the
-// same time, and one extra plane per segment) -- the brick kernel re-read 288 halo cells per 256.
-// The z faces are evaluated ONCE: a cell's +z face (its last face) is computed from the next plane's
-// values, which the thread has already loaded into registers for the next plane's staging, and carried in
-// registers (Sf, the interpolated Y_s and the laplacian term) to serve as the next cell's -z face (its
-// first); the same values with the opposite sign, as the face loop of k_y_prep<S, -1> forms them. The x/y
-// faces read both cells from LDS and their geometry by coalesced loads of the owner's face slots (the
-// neighbour-side copy is the adjacent lane's line, an L1/L2 hit): evaluating those twice costs FP64 issue,
-// not HBM bytes. The cell's own values stay in registers through the tail (no hai re-read). Faces, their
-// order and every product are those of k_y_prep<S, -1>: results are bitwise the face walk's.
-constexpr int ZTX = 16, ZTY = 16, ZPX = ZTX + 2, ZNP = ZPX * (ZTY + 2);
-static_assert(ZTX * ZTY == TPB, "one thread per tile column");
-template <int S, int MINB>
-__global__ void __launch_bounds__(TPB, MINB) k_y_prep_zm(MeshView m, int kz, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
-    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
-    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
-    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
-    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
-  __shared__ double sY[S][ZNP], sH[S][ZNP], sA[ZNP];
-  const int nx = m.hx, ny = m.hy, nz = m.hz, nxy = nx * ny;
-  const int ntx = nx / ZTX, nty = ny / ZTY;
-  const int bid = xcd_block();
-  const int tx = bid % ntx, tt = bid / ntx, ty = tt % nty, seg = tt / nty;
-  const int k0 = seg * kz, k1 = min(nz, k0 + kz);
-  if (k0 >= nz) return;   // whole workgroup
-  const int t = threadIdx.x, li = t % ZTX, lj = t / ZTX;
-  const int i = tx * ZTX + li, j = ty * ZTY + lj;
-  const int me = (li + 1) + ZPX * (lj + 1);
-  const long C = m.C, F = m.F, B = m.B;
-  const int hxp = i < nx - 1, hyp = j < ny - 1;
-  const int cxy = i + nx * j;
-  // the ring cell staged by thread t < 2 (ZTX + ZTY): LDS index hl (-1: none / outside the box), column hg
-  int hl = -1, hg = 0;
-  if (t < 2 * (ZTX + ZTY)) {
-    int a, b;
-    if (t < ZTY) { a = -1; b = t; }
-    else if (t < 2 * ZTY) { a = ZTX; b = t - ZTY; }
-    else if (t < 2 * ZTY + ZTX) { a = t - 2 * ZTY; b = -1; }
-    else { a = t - 2 * ZTY - ZTX; b = ZTY; }
-    const int gi = tx * ZTX + a, gj = ty * ZTY + b;
-    if (gi >= 0 && gi < nx && gj >= 0 && gj < ny) { hl = (a + 1) + ZPX * (b + 1); hg = gi + nx * gj; }
-  }
-  double nY[S], nH[S], nA;   // the own column's next plane (staged at the next step; the +z neighbour now)
-  auto load_own = [&](int k, double (&y)[S], double (&h)[S], double& a) {
-    const long c = cxy + (long)nxy * k;
-    a = alpha[c];
-#pragma unroll
-    for (int s = 0; s < S; ++s) { y[s] = Y[s * C + c]; h[s] = hai[s * C + c]; }
-  };
-  // the carried z face: Sf, interpolated Y_s and laplacian term of the +z face of the cell below
-  double zs0 = 0.0, zs1 = 0.0, zs2 = 0.0, zy[S], zv[S];
-  auto zface = [&](long f, auto yo, auto ho, double ao, const double (&yn)[S], const double (&hn)[S], double an) {
-    const double w = m.w[f], ms = m.magSf[f], dcf = m.dc[f];
-    zs0 = m.Sf[f]; zs1 = m.Sf[F + f]; zs2 = m.Sf[2 * F + f];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const double ys = yo(s);
-      zy[s] = interp_f(w, ys, yn[s]);
-      const double gam = interp_f(w, ao * ho(s), an * hn[s]);
-      zv[s] = gam * ms * (dcf * (yn[s] - ys));
-    }
-  };
-  load_own(k0, nY, nH, nA);
-  if (k0 > 0) {   // the segment's first -z face, from the plane below
-    double pY[S], pH[S], pA;
-    load_own(k0 - 1, pY, pH, pA);
-    zface((long)(hxp + hyp) * C + cxy + (long)nxy * (k0 - 1), [&](int s) { return pY[s]; }, [&](int s) { return pH[s]; },
-          pA, nY, nH, nA);
-  }
-  for (int k = k0; k < k1; ++k) {
-    const int c = cxy + nxy * k;
-    __syncthreads();   // every thread done with the previous plane's neighbour values
-#pragma unroll
-    for (int s = 0; s < S; ++s) { sY[s][me] = nY[s]; sH[s][me] = nH[s]; }
-    sA[me] = nA;
-    if (hl >= 0) {
-      const long hc = hg + (long)nxy * k;
-      sA[hl] = alpha[hc];
-#pragma unroll
-      for (int s = 0; s < S; ++s) { sY[s][hl] = Y[s * C + hc]; sH[s][hl] = hai[s * C + hc]; }
-    }
-    const double ac = nA;
-    if (k + 1 < nz) {   // the next plane's Y and alpha in flight across the barrier and the x/y faces (its hai
-      const long cn = c + nxy;   // is loaded at the +z face: registers)
-      nA = alpha[cn];
-#pragma unroll
-      for (int s = 0; s < S; ++s) nY[s] = Y[s * C + cn];
-    }
-    __syncthreads();
-    // the cell's own values are read back from its LDS slot where needed (registers: the accumulators, the
-    // next plane and the carried face fill the 256 of two waves per SIMD)
-    auto yc = [&](int s) { return sY[s][me]; };
-    auto hc = [&](int s) { return sH[s][me]; };
-    double g[S][3], lap[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) { g[s][0] = 0.0; g[s][1] = 0.0; g[s][2] = 0.0; lap[s] = 0.0; }
-    if (k > 0) {   // -z: the carried face (owner below)
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        g[s][0] -= zs0 * zy[s]; g[s][1] -= zs1 * zy[s]; g[s][2] -= zs2 * zy[s];
-        lap[s] -= zv[s];
-      }
-    }
-    auto face = [&](long f, int lo, bool own) {
-      const double w = m.w[f], sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
-      const double ms = m.magSf[f], dcf = m.dc[f];
-      const double an = sA[lo];
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const double yn = sY[s][lo];
-        const double ahn = an * sH[s][lo];
-        const double ycs = yc(s), ahc = ac * hc(s);
-        const double yf = own ? interp_f(w, ycs, yn) : interp_f(w, yn, ycs);
-        const double v0 = sf0 * yf, v1 = sf1 * yf, v2 = sf2 * yf;
-        const double gam = own ? interp_f(w, ahc, ahn) : interp_f(w, ahn, ahc);
-        const double dy = own ? yn - ycs : ycs - yn;
-        const double v = gam * ms * (dcf * dy);
-        if (own) { g[s][0] += v0; g[s][1] += v1; g[s][2] += v2; lap[s] += v; }
-        else { g[s][0] -= v0; g[s][1] -= v1; g[s][2] -= v2; lap[s] -= v; }
-      }
-    };
-    if (j > 0) face((long)hxp * C + c - nx, me - ZPX, false);
-    if (i > 0) face(c - 1, me - 1, false);
-    if (hxp) face(c, me + 1, true);
-    if (hyp) face((long)hxp * C + c, me + ZPX, true);
-    if (k < nz - 1) {   // +z: evaluated once, carried to the cell above
-#pragma unroll
-      for (int s = 0; s < S; ++s) nH[s] = hai[s * C + c + nxy];
-      zface((long)(hxp + hyp) * C + c, yc, hc, ac, nY, nH, nA);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        g[s][0] += zs0 * zy[s]; g[s][1] += zs1 * zy[s]; g[s][2] += zs2 * zy[s];
-        lap[s] += zv[s];
-      }
-    }
-    each_slot(m, tyY, c, [&](int b, int tb) {
-      const double bs0 = m.bSf[b], bs1 = m.bSf[B + b], bs2 = m.bSf[2 * B + b];
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const double yf = bface(m, tb, Y + s * C, bY + s * B, b, c);
-        g[s][0] += bs0 * yf; g[s][1] += bs1 * yf; g[s][2] += bs2 * yf;
-        const double ahc = ac * hc(s), ycs = yc(s);
-        double v;
-        if (bc_coupled(tb)) {
-          const int pc = m.partner[b];
-          const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
-          v = interp_b(m.bw[b], ahc, an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - ycs));
-        } else {
-          const double sng = (tb == FIXED_VALUE || tb == CALCULATED || tb == FIXED_ENERGY || bc_mixed(tb)) ? m.bdc[b] * (bY[s * B + b] - ycs) : 0.0;
-          v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
-        }
-        lap[s] += v;
-      }
-    });
-    double ycv[S], hcv[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) { ycv[s] = yc(s); hcv[s] = hc(s); }
-    y_prep_tail<S>(m, tyY, Y, bY, rhoD, brhoD, hcv, bhai, sumE, bsumE, hD, bhD, dAD, gout, c, g, lap, ycv);
-  }
-}
-// planes per workgroup segment: about two workgroups per CU over the whole box, at least 4 planes
-inline int yzm_kz(int nx, int ny, int nz) {
-  if (const char* e = std::getenv("DFMI_ZM_KZ")) return std::max(1, std::atoi(e));   // A/B: planes per segment
-  const int tiles = (nx / ZTX) * (ny / ZTY);
-  const int nseg = std::max(1, std::min(512 / std::max(1, tiles), nz / 4));
-  return (nz + nseg - 1) / nseg;
-}
 
-// k_y_prep, species-outer over the solver's gather rows (hex meshes, W = 6): the cell's six faces'
-// indices, geometry and neighbour alpha are loaded once up front, then each species loads its twelve
-// neighbour values (Y, hai at the six neighbours) together -- two dependent memory levels per cell instead
-// of the face walk's two to three per face, so a thread keeps up to twelve gathers in flight. Per species
-// the faces are summed in the same sequential order (then the cell's boundary slots), so every
-// accumulator is bitwise the face walk's.
-template <int S>
-__global__ void __launch_bounds__(TPB) k_y_prep_rows(MeshView m, const int8_t* __restrict__ tyY, const double* __restrict__ Y,
-    const double* __restrict__ bY, const double* __restrict__ rhoD, const double* __restrict__ brhoD,
-    const double* __restrict__ hai, const double* __restrict__ bhai, const double* __restrict__ alpha,
-    const double* __restrict__ balpha, double* __restrict__ sumE, double* __restrict__ bsumE,
-    double* __restrict__ hD, double* __restrict__ bhD, double* __restrict__ dAD, double* __restrict__ gout) {
-  constexpr int WT = 6;
-  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
-  if (c >= m.C) return;
-  const long C = m.C, F = m.F, B = m.B;
-  int es[WT], cs[WT];
-  const int cl = ecls_of(m, c);
-#pragma unroll
-  for (int k = 0; k < WT; ++k) erow(m, cl, k, c, cs[k], es[k]);
-  double fw[WT], f0[WT], f1[WT], f2[WT], fms[WT], fdc[WT], fan[WT];
-#pragma unroll
-  for (int k = 0; k < WT; ++k) {
-    const bool live = es[k] >= 0;
-    const int f = live ? es[k] >> 1 : 0;
-    const int o2 = live ? cs[k] : c;
-    fw[k] = m.w[f]; f0[k] = m.Sf[f]; f1[k] = m.Sf[F + f]; f2[k] = m.Sf[2 * F + f];
-    fms[k] = m.magSf[f]; fdc[k] = m.dc[f]; fan[k] = alpha[o2];
-  }
-  const double ac = alpha[c];
-  const double vol = m.V[c];
-  const int sb0 = m.cbStart[c], sb1 = m.cbStart[c + 1];
-  double g[S][3];
-  double dad = 0.0;
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const double yc = Y[s * C + c];
-    const double ahc = ac * hai[s * C + c];
-    double yn[WT], hn[WT];
-#pragma unroll
-    for (int k = 0; k < WT; ++k) {
-      const int o2 = es[k] >= 0 ? cs[k] : c;
-      yn[k] = Y[s * C + o2];
-      hn[k] = hai[s * C + o2];
-    }
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0, lap = 0.0;
-#pragma unroll
-    for (int k = 0; k < WT; ++k) {
-      if (es[k] < 0) continue;
-      const bool own = (es[k] & 1) != 0;
-      const double w = fw[k];
-      const double ahn = fan[k] * hn[k];
-      const double yf = own ? interp_f(w, yc, yn[k]) : interp_f(w, yn[k], yc);
-      const double v0 = f0[k] * yf, v1 = f1[k] * yf, v2 = f2[k] * yf;
-      const double gam = own ? interp_f(w, ahc, ahn) : interp_f(w, ahn, ahc);
-      const double dy = own ? yn[k] - yc : yc - yn[k];
-      const double v = gam * fms[k] * (fdc[k] * dy);
-      if (own) { g0 += v0; g1 += v1; g2 += v2; lap += v; }
-      else { g0 -= v0; g1 -= v1; g2 -= v2; lap -= v; }
-    }
-    for (int kk = sb0; kk < sb1; ++kk) {
-      const int b = m.cbSlot[kk];
-      const int t = tyY[b];
-      if (t == EMPTY) continue;
-      const double yf = bface(m, t, Y + s * C, bY + s * B, b, c);
-      g0 += m.bSf[b] * yf; g1 += m.bSf[B + b] * yf; g2 += m.bSf[2 * B + b] * yf;
-      double v;
-      if (bc_coupled(t)) {
-        const int pc = m.partner[b];
-        const double an = pc >= 0 ? alpha[pc] * hai[s * C + pc] : balpha[b] * bhai[s * B + b];
-        v = interp_b(m.bw[b], ahc, an) * m.bmagSf[b] * (m.bdc[b] * (nbrv(m, Y + s * C, bY + s * B, b) - yc));
-      } else {
-        const double sng = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - yc) : 0.0;
-        v = balpha[b] * bhai[s * B + b] * m.bmagSf[b] * sng;
-      }
-      lap += v;
-    }
-    g[s][0] = g0 / vol; g[s][1] = g1 / vol; g[s][2] = g2 / vol;
-    dad = dad + lap / vol;
-  }
-  if (gout) {
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) gout[(3L * s + k) * C + c] = g[s][k];
-  }
-  double se[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const double rd = rhoD[s * C + c];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) se[k] += rd * g[s][k];
-  }
-  double hd[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const double rd = rhoD[s * C + c], h = hai[s * C + c], yc = Y[s * C + c];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) hd[k] += h * (rd * g[s][k] - yc * se[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) { sumE[k * C + c] = se[k]; hD[k * C + c] = hd[k]; }
-  dAD[c] = dad;
-  // boundary fields of the non-coupled slots (as k_y_prep)
-  each_slot(m, tyY, c, [&](int b, int t) {
-    if (bc_coupled(t)) return;
-    const double ms = m.bmagSf[b];
-    const double nv[3] = {m.bSf[b] / ms, m.bSf[B + b] / ms, m.bSf[2 * B + b] / ms};
-    double bg[S][3];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const double sn = (t == FIXED_VALUE || t == CALCULATED || t == FIXED_ENERGY || bc_mixed(t)) ? m.bdc[b] * (bY[s * B + b] - Y[s * C + c]) : 0.0;
-      const double corr = sn - (nv[0] * g[s][0] + nv[1] * g[s][1] + nv[2] * g[s][2]);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) bg[s][k] = g[s][k] + nv[k] * corr;
-    }
-    double bse[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      double a = 0.0;
-#pragma unroll
-      for (int s = 0; s < S; ++s) a += brhoD[s * B + b] * bg[s][k];
-      bse[k] = a;
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      double a = 0.0;
-#pragma unroll
-      for (int s = 0; s < S; ++s)
-        a += bhai[s * B + b] * (brhoD[s * B + b] * bg[s][k] - bY[s * B + b] * bse[k]);
-      bsumE[k * B + b] = bse[k];
-      bhD[k * B + b] = a;
-    }
-  });
-}
 
 // phiUc = linearInterpolate(sumYDiffError) & Sf
 __global__ void k_phiuc_face(MeshView m, const double* __restrict__ sumE, double* __restrict__ phiUc) {
@@ -1713,152 +1408,6 @@ __global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t
   }
 }
 
-// k_y_assemble_ell on a hex box in blockMesh order, z-marching like k_y_prep_zm: one 16 x 16 column tile
-// per workgroup walks a segment of planes. Per plane the tile's rhoD_s and the plane's face ring are staged
-// in LDS once (the x/y neighbours' rhoD from LDS instead of global gathers); the +z neighbour's rhoD is
-// the thread's own prefetch of the next plane, and the +z face's data (phi, phiUc, the upwind weight, w,
-// deltaCoeffs, |Sf|) and the cell's rhoD stay in registers to serve the next cell's -z face: every cell
-// value and every face value is read from HBM once. Faces, order and products are those of
-// k_y_assemble_ell<S, -1>: bitwise the same rows.
-template <int S>
-__global__ void __launch_bounds__(TPB) k_y_assemble_ell_zm(MeshView m, int kz, const int8_t* __restrict__ tyY, int inert,
-    const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
-    const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
-    const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
-    const double* __restrict__ phiUc, const double* __restrict__ bphiUc, int W, long Ce, double* __restrict__ val,
-    double* __restrict__ dS, double* __restrict__ rhs, MixBC mxY, const double* __restrict__ wY,
-    const double* __restrict__ bwY) {
-  __shared__ double sR[S][ZNP];
-  const int nx = m.hx, ny = m.hy, nz = m.hz, nxy = nx * ny;
-  const int ntx = nx / ZTX, nty = ny / ZTY;
-  const int bid = xcd_block();
-  const int tx = bid % ntx, tt = bid / ntx, ty = tt % nty, seg = tt / nty;
-  const int k0 = seg * kz, k1 = min(nz, k0 + kz);
-  if (k0 >= nz) return;   // whole workgroup
-  const int t = threadIdx.x, li = t % ZTX, lj = t / ZTX;
-  const int i = tx * ZTX + li, j = ty * ZTY + lj;
-  const int me = (li + 1) + ZPX * (lj + 1);
-  const long C = m.C, B = m.B;
-  const int hxp = i < nx - 1, hyp = j < ny - 1;
-  const int cxy = i + nx * j;
-  int hl = -1, hg = 0;   // the ring cell staged by thread t < 2 (ZTX + ZTY)
-  if (t < 2 * (ZTX + ZTY)) {
-    int a, b;
-    if (t < ZTY) { a = -1; b = t; }
-    else if (t < 2 * ZTY) { a = ZTX; b = t - ZTY; }
-    else if (t < 2 * ZTY + ZTX) { a = t - 2 * ZTY; b = -1; }
-    else { a = t - 2 * ZTY - ZTX; b = ZTY; }
-    const int gi = tx * ZTX + a, gj = ty * ZTY + b;
-    if (gi >= 0 && gi < nx && gj >= 0 && gj < ny) { hl = (a + 1) + ZPX * (b + 1); hg = gi + nx * gj; }
-  }
-  // face data of one face: phi, phiUc, upwind weight, w, deltaCoeffs, |Sf|
-  struct FD { double ph, pu, wu, w, dcf, ms; };
-  auto load_face = [&](long f) {
-    FD d;
-    d.ph = phi[f]; d.pu = phiUc[f];
-    d.wu = wY ? wY[f] : (d.ph >= 0 ? 1.0 : 0.0);
-    d.w = m.w[f]; d.dcf = m.dc[f]; d.ms = m.magSf[f];
-    return d;
-  };
-  double nR[S], pR[S];   // rhoD of the own column: next plane (prefetched), plane below (the -z neighbour)
-  FD zf{};               // the -z face (the +z face of the cell below)
-  {
-    const long c0 = cxy + (long)nxy * k0;
-#pragma unroll
-    for (int s = 0; s < S; ++s) nR[s] = rhoD[s * C + c0];
-    if (k0 > 0) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) pR[s] = rhoD[s * C + c0 - nxy];
-      zf = load_face((long)(hxp + hyp) * C + c0 - nxy);
-    }
-  }
-  for (int kp = k0; kp < k1; ++kp) {
-    const int c = cxy + nxy * kp;
-    const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
-    __syncthreads();   // every thread done with the previous plane's neighbour values
-    double rc[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) { rc[s] = nR[s]; sR[s][me] = rc[s]; }
-    if (hl >= 0) {
-      const long hc = hg + (long)nxy * kp;
-#pragma unroll
-      for (int s = 0; s < S; ++s) sR[s][hl] = rhoD[s * C + hc];
-    }
-    if (kp + 1 < nz) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) nR[s] = rhoD[s * C + c + nxy];
-    }
-    __syncthreads();
-    double d1 = 0.0, d2 = 0.0;
-    double dL[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) dL[s] = 0.0;
-    int k = 0;
-    auto face = [&](const FD& fd, auto rn, bool own) {
-      const double L1 = -fd.wu * fd.ph, U1 = L1 + fd.ph;
-      const double L2 = -fd.wu * fd.pu, U2 = L2 + fd.pu;
-      if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
-      const double Ls = L1 + L2, Us = U1 + U2;
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (s == inert) continue;
-        const int ss = s < inert ? s : s - 1;
-        const double r = rn(s);
-        const double UL = fd.dcf * ((own ? interp_f(fd.w, rc[s], r) : interp_f(fd.w, r, rc[s])) * fd.ms);
-        dL[s] -= UL;
-        val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
-      }
-      ++k;
-    };
-    if (kp > 0) face(zf, [&](int s) { return pR[s]; }, false);
-    if (j > 0) face(load_face((long)hxp * C + c - nx), [&](int s) { return sR[s][me - ZPX]; }, false);
-    if (i > 0) face(load_face(c - 1), [&](int s) { return sR[s][me - 1]; }, false);
-    if (hxp) face(load_face(c), [&](int s) { return sR[s][me + 1]; }, true);
-    if (hyp) face(load_face((long)hxp * C + c), [&](int s) { return sR[s][me + ZPX]; }, true);
-    if (kp < nz - 1) {
-      zf = load_face((long)(hxp + hyp) * C + c);
-      face(zf, [&](int s) { return nR[s]; }, true);
-    }
-#pragma unroll
-    for (int s = 0; s < S; ++s) pR[s] = rc[s];
-    const double vol = m.V[c];
-    const double dd = m.rdt * rho[c] * vol + (d1 + d2);
-    const double ro = m.rdt * rho_old[c];
-    double dg[S], sr[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      dg[s] = dd - dL[s];
-      sr[s] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
-    }
-    each_slot(m, tyY, c, [&](int b, int tb) {
-      const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
-      const bool cp = bc_coupled(tb);
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        if (s == inert) continue;
-        const int ss = s < inert ? s : s - 1;
-        const BCoef qc = bcoef_f(tb, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
-        const BCoef ql = bcoef_f(tb, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
-        const double gam = cp ? interp_b(m.bw[b], rc[s], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
-        const double pG = gam * m.bmagSf[b];
-        const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
-        const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
-        dg[s] += icv;
-        if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
-        else sr[s] += bcv;
-      }
-      if (cp) ++k;
-    });
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      if (s == inert) continue;
-      const int ss = s < inert ? s : s - 1;
-      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
-      dS[ss * Ce + pc] = dg[s];
-      rhs[ss * Ce + pc] = sr[s];
-    }
-  }
-}
 
 template <int S>
 __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
@@ -1888,6 +1437,7 @@ __global__ void k_y_inert(int C, int inert, double* __restrict__ Y) {
 // sumYDiffError, so a second pass re-forms the gradients chunk by chunk (neighbour values come from
 // L2 the second time; cheaper than spilling S x 3 gradients per cell to HBM).
 constexpr int YCH = 8;
+constexpr int YPREP_LCH = 8, YASM_LCH = 8;   // species per launch of the chunked y_prep / y_assemble_ell kernels
 
 // gradient (and, with LAP, the diffAlphaD laplacian) of species s0 .. s0+CH-1 at cell c, divided by V
 template <int CH, bool LAP, int WT>
@@ -2353,35 +1903,17 @@ template <template <int> class K, class... A> void dispatch_S(int S, dim3 g, dim
        DFMI_HIP(hipGetLastError()); } while (0)
 
 // kernels templated on the ELL width: the unrolled path for hex meshes (W = 6), the CSR walk otherwise
-// (DFMI_FACE_CSR=1 forces the CSR walk everywhere: A/B measurement and parity of both paths)
-bool face_rows(const Ctx& x) {
-  const char* e = std::getenv("DFMI_FACE_CSR");
-  return x.ell.W == 6 && !(e && std::atoi(e) != 0);
-}
-// hex boxes in blockMesh order: the computed face walk (each_face<-1>) everywhere (DFMI_FACE_HEX=0: off)
-bool face_hex(const Ctx& x) {
-  const char* e = std::getenv("DFMI_FACE_HEX");
-  return x.hex[0] > 0 && !(e && std::atoi(e) == 0);
-}
+// (option fv.csr_walk forces the CSR walk everywhere: A/B measurement and parity of both paths)
+bool face_rows(const Ctx& x) { return x.ell.W == 6 && !x.on("fv.csr_walk"); }
+// hex boxes in blockMesh order: the computed face walk (each_face<-1>) everywhere (fv.hex_walk = 0: off)
+bool face_hex(const Ctx& x) { return x.hex[0] > 0 && x.on("fv.hex_walk") && !x.on("fv.csr_walk"); }
 #define LAUNCH_W(kern, n, ...) \
   do { if (face_hex(x)) LAUNCH(kern<-1>, n, __VA_ARGS__); else if (face_rows(x)) LAUNCH(kern<6>, n, __VA_ARGS__); \
        else LAUNCH(kern<0>, n, __VA_ARGS__); } while (0)
-// species-chunked kernels for large mechanisms: the CSR face walk measured faster than the face rows
-// (2M cells x 53 species: y_prep 9.5 vs 17.5 ms, y_assemble_ell 4.5 vs 6.1 ms); DFMI_GEN_ROWS=1 for the rows
-bool gen_rows(const Ctx& x) {
-  const char* e = std::getenv("DFMI_GEN_ROWS");
-  return face_rows(x) && e && std::atoi(e) != 0;
-}
-// the chunked kernels walk the CSR face lists on hex boxes too: 2M cells x 53 species, y_assemble_ell 4.43
-// against 5.84 ms per step by the computed hex walk (its 179 VGPRs: two waves per SIMD), y_prep 8.61 against
-// 8.71 (scripts/c4_ab.sh); DFMI_GEN_HEX=1 for the hex walk
-bool gen_hex(const Ctx& x) {
-  const char* e = std::getenv("DFMI_GEN_HEX");
-  return face_hex(x) && e && std::atoi(e) != 0;
-}
-#define LAUNCH_SWG(kern, NS, n, ...) \
-  do { if (gen_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (gen_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
-       else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
+// species-chunked kernels for large mechanisms walk the CSR face lists on every mesh: 2M cells x 53 species,
+// y_prep 9.5 against 17.5 ms by the face rows and 8.61 against 8.71 ms by the computed hex walk (its 179 VGPRs:
+// two waves per SIMD), y_assemble_ell 4.5 / 4.43 against 6.1 / 5.84 ms (round 4, scripts/c4_ab.sh)
+#define LAUNCH_SWG(kern, NS, n, ...) LAUNCH((kern<NS, 0>), n, __VA_ARGS__)
 #define LAUNCH_SW(kern, NS, n, ...) \
   do { if (face_hex(x)) LAUNCH((kern<NS, -1>), n, __VA_ARGS__); else if (face_rows(x)) LAUNCH((kern<NS, 6>), n, __VA_ARGS__); \
        else LAUNCH((kern<NS, 0>), n, __VA_ARGS__); } while (0)
@@ -2492,10 +2024,9 @@ void p_assemble(Ctx& x) {
   Matrix& A = x.mP;
   MeshView m = x.view();
   {
-    // the cell walk over the owner-slot storage (measured 176 -> 150 us on the 2M box), else face-parallel;
-    // one timer name for both (bench rooflines)
-    const char* ep = std::getenv("DFMI_PFACE_CELL");
-    const bool cellw = x.fslot && !(ep && std::atoi(ep) == 0);
+    // the cell walk over the owner-slot storage (measured 176 -> 150 us on the 2M box), else (face order)
+    // face-parallel; one timer name for both (bench rooflines)
+    const bool cellw = x.fslot;
     KScope _ks(x, "k_p_face");
     if (cellw && x.C > 0)
       hipLaunchKernelGGL(k_p_face_cell, dim3(blocks_for(x.C, TPB)), dim3(TPB), 0, x.stream, m, x.f("rho"), x.f("rAU"),
@@ -2532,13 +2063,10 @@ void p_post_solve(Ctx& x) {
 }
 
 // species count: register-resident templates for 2..16 species, the chunked kernels above otherwise
-// (or always, with DFMI_SPECIES_GENERIC=1 -- the parity tests run both on the same mechanisms)
-bool species_generic(int S) {
-  const char* e = std::getenv("DFMI_SPECIES_GENERIC");
-  return S > 16 || (e && std::atoi(e) != 0);
-}
+// (or always, with the option fv.species_generic -- the parity tests run both on the same mechanisms)
+bool species_generic(const Ctx& x) { return x.S > 16 || x.on("fv.species_generic"); }
 #define DFMI_SWITCH_S(S, CALL, GEN)                                                              \
-  if (species_generic(S)) { GEN; } else switch (S) {                                             \
+  if (species_generic(x)) { GEN; } else switch (S) {                                             \
     case 2: CALL(2); break; case 3: CALL(3); break; case 4: CALL(4); break; case 5: CALL(5); break; \
     case 6: CALL(6); break; case 7: CALL(7); break; case 8: CALL(8); break; case 9: CALL(9); break; \
     case 10: CALL(10); break; case 11: CALL(11); break; case 12: CALL(12); break;                  \
@@ -2648,50 +2176,15 @@ void y_prep(Ctx& x) {
   MeshView m = x.view();
   double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
 // (k_y_prep: the CSR walk measured faster than the gather rows -- 667 vs 848 us on the 2M box; its
-// 243 VGPRs leave no room for the up-front row loads)
-// (DFMI_YPREP_ROWS=1: the species-outer row kernel k_y_prep_rows on hex meshes)
-  const char* erows = std::getenv("DFMI_YPREP_ROWS");
-  const bool prep_rows = face_rows(x) && erows && std::atoi(erows) != 0;
-  // LDS-staged brick kernel on hex boxes whose dimensions the brick divides (DFMI_YPREP_BRICK=0: off,
-  // 2: all species staged at once)
-  const char* eb = std::getenv("DFMI_YPREP_BRICK");
-  const int bmode = eb ? std::atoi(eb) : 1;
-  const int brick = (face_hex(x) && !x.trav.n && x.hex[0] % YBX == 0 && x.hex[1] % YBY == 0 && x.hex[2] % YBZ == 0 &&
-                     bmode > 0) ? (bmode == 2 ? 2 : 1) : 0;
-  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YPREP_ZM=1|2)
-  const char* ez = std::getenv("DFMI_YPREP_ZM");
-  const int zmode = ez ? std::atoi(ez) : 0;   // 1: two workgroups per CU (launch bound), 2: the compiler's choice
-  // (off by default: measured slower than the brick kernel)
-  const bool zm = face_hex(x) && !x.trav.n && x.hex[0] % ZTX == 0 && x.hex[1] % ZTY == 0 && zmode > 0;
-  const int zkz = zm ? yzm_kz(x.hex[0], x.hex[1], x.hex[2]) : 0;
-  const int zgrid = zm ? (x.hex[0] / ZTX) * (x.hex[1] / ZTY) * ((x.hex[2] + zkz - 1) / zkz) : 0;
+// 243 VGPRs leave no room for the up-front row loads). Measured slower and removed (round 5): the species-outer
+// row kernel (767-793 vs 657-673 us) and the z-marching tiles (811 vs 620 us), DESIGN.md 8.
+  // LDS-staged brick kernel on hex boxes whose dimensions the brick divides (fv.yprep_brick = 0: off)
+  const bool brick = face_hex(x) && !x.trav.n && x.hex[0] % YBX == 0 && x.hex[1] % YBY == 0 && x.hex[2] % YBZ == 0 &&
+                     x.on("fv.yprep_brick");
 #define CALL(NS)                                                                                                     \
   do {                                                                                                               \
-    if (zm && !prep_rows) {                                                                                          \
-      KScope _ks(x, "k_y_prep");                                                                                     \
-      if (zmode == 2)                                                                                                \
-        hipLaunchKernelGGL((k_y_prep_zm<NS, 1>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.f("Y"),  \
-               x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"),  \
-               x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),     \
-               x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                             \
-      else                                                                                                           \
-        hipLaunchKernelGGL((k_y_prep_zm<NS, 2>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.f("Y"),  \
-               x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"),  \
-               x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),     \
-               x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                             \
-      DFMI_HIP(hipGetLastError());                                                                                   \
-    } else if (prep_rows)                                                                                            \
-      LAUNCH_AS("k_y_prep", (k_y_prep_rows<NS>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), \
-             x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), x.f("sumYDiffError"),             \
-             x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
-             gout);                                                                                                  \
-    else if (brick == 1)                                                                                             \
+    if (brick)                                                                                                       \
       LAUNCH_AS("k_y_prep", (k_y_prep_brick<NS, ybrick_sc(NS)>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"),    \
-             x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
-             x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                              \
-             x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                               \
-    else if (brick == 2)                                                                                             \
-      LAUNCH_AS("k_y_prep", (k_y_prep_brick<NS, (NS < 10 ? NS : ybrick_sc(NS))>), x.C, m, x.st("Y"), x.f("Y"), x.f("boundary_Y"),               \
              x.f("rhoD"), x.f("boundary_rhoD"), x.f("hai"), x.f("boundary_hai"), x.f("alpha"), x.f("boundary_alpha"), \
              x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),                              \
              x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), gout);                                               \
@@ -2706,13 +2199,12 @@ void y_prep(Ctx& x) {
              x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"),  \
              gout);                                                                                                  \
   } while (0)
-  // the chunked kernel in species ranges of DFMI_YPREP_LCH species per launch (default 8; 0: all in one), pass 1
-  // over every range, then pass 2 (it reads the finished sumYDiffError)
-  const char* elch = std::getenv("DFMI_YPREP_LCH");
-  const int lch_req = elch ? std::atoi(elch) : 8;
+  // the chunked kernel (4 species per chunk: 7.0 ms against 7.4-9.5 for chunks of 2 / 3 / 8 on 2M x 53 species) in
+  // species ranges of YPREP_LCH species per launch (L2 locality of the neighbour gathers: 8.74 -> 8.56-8.62 ms
+  // with 8 or 16), pass 1 over every range, then pass 2 (it reads the finished sumYDiffError)
 #define GEN(CH)                                                                                                      \
   do {                                                                                                               \
-    const int lch = lch_req > 0 ? std::max(CH, lch_req / CH * CH) : x.S;                                            \
+    constexpr int lch = YPREP_LCH / CH * CH;                                                                         \
     for (int pass = 1; pass <= 2; ++pass)                                                                            \
       for (int s_lo = 0; s_lo < x.S; s_lo += lch)                                                                    \
         LAUNCH_SWG(k_y_prep_gen, CH, x.C, m, s_lo, std::min(x.S, s_lo + lch), pass, x.st("Y"), x.f("Y"),             \
@@ -2720,15 +2212,7 @@ void y_prep(Ctx& x) {
                    x.f("boundary_alpha"), x.f("sumYDiffError"), x.f("boundary_sumYDiffError"), x.f("hDiffCorrFlux"),  \
                    x.f("boundary_hDiffCorrFlux"), x.f("diffAlphaD"), pass == 1 ? gout : nullptr);                   \
   } while (0)
-  // DFMI_YPREP_CH=2|3|4|8: species per chunk of the chunked kernel (default 4 for S > 16; set, it also
-  // replaces the full-S kernels of S <= 16, an A/B knob)
-  const char* ech = std::getenv("DFMI_YPREP_CH");
-  const int ch = ech ? std::atoi(ech) : 0;
-  if (ch == 2) GEN(2);
-  else if (ch == 3) GEN(3);
-  else if (ch == 8) GEN(8);
-  else if (ch == 4) GEN(4);
-  else DFMI_SWITCH_S(x.S, CALL, GEN(4))
+  DFMI_SWITCH_S(x.S, CALL, GEN(4))
 #undef GEN
 #undef CALL
   halo_fields(x, {"sumYDiffError", "hDiffCorrFlux"});
@@ -2751,41 +2235,23 @@ void y_assemble(Ctx& x) {
 
 void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs) {
   MeshView m = x.view();
-  // z-marching tile kernel on hex boxes whose x/y dimensions the 16 x 16 tile divides (DFMI_YASM_ZM=1)
-  const char* ez = std::getenv("DFMI_YASM_ZM");
-  // (off by default: measured slower than the cell-parallel kernel)
-  const bool zm = face_hex(x) && !x.trav.n && x.hex[0] % ZTX == 0 && x.hex[1] % ZTY == 0 && ez && std::atoi(ez) != 0;
-  const int zkz = zm ? yzm_kz(x.hex[0], x.hex[1], x.hex[2]) : 0;
-  const int zgrid = zm ? (x.hex[0] / ZTX) * (x.hex[1] / ZTY) * ((x.hex[2] + zkz - 1) / zkz) : 0;
+  // (the z-marching tile form measured slower than this cell-parallel kernel, 961 vs 622 us, and is removed)
 #define CALL(NS)                                                                                                     \
-  do {                                                                                                               \
-    if (zm) {                                                                                                        \
-      KScope _ks(x, "k_y_assemble_ell");                                                                             \
-      hipLaunchKernelGGL((k_y_assemble_ell_zm<NS>), dim3(zgrid), dim3(TPB), 0, x.stream, m, zkz, x.st("Y"), x.inert, \
-                         x.f("Y"), x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"),      \
-                         x.f("rho_old"), x.f("phi"), x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, \
-                         val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1));                                      \
-      DFMI_HIP(hipGetLastError());                                                                                   \
-    } else                                                                                                           \
-      LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),          \
-                x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                             \
-                x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1)); \
-  } while (0)
-  // species ranges of DFMI_YASM_LCH species per launch (default 8; 0: all in one launch)
-  const char* elch = std::getenv("DFMI_YASM_LCH");
-  const int lch_req = elch ? std::atoi(elch) : 8;
+  LAUNCH_SW(k_y_assemble_ell, NS, x.C, m, x.st("Y"), x.inert, x.f("Y"), x.f("boundary_Y"), x.f("rhoD"),              \
+            x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"),                                 \
+            x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"), x.sch_w(0), x.sch_w(1))
+  // chunked kernel: 8 species per chunk, species ranges of YASM_LCH per launch (assembly 5.98 -> 5.86 ms per step
+  // on 2M x 53 species with 8)
 #define GEN(CH)                                                                                                      \
   do {                                                                                                               \
-    const int lch = lch_req > 0 ? std::max(CH, lch_req / CH * CH) : x.S;                                            \
+    constexpr int lch = YASM_LCH / CH * CH;                                                                          \
     for (int s_lo = 0; s_lo < x.S; s_lo += lch)                                                                      \
       LAUNCH_SWG(k_y_assemble_ell_gen, CH, x.C, m, s_lo, std::min(x.S, s_lo + lch), x.st("Y"), x.inert, x.f("Y"),    \
                  x.f("boundary_Y"), x.f("rhoD"), x.f("boundary_rhoD"), x.f("RR"), x.f("rho"), x.f("rho_old"), x.f("phi"), \
                  x.f("boundary_phi"), x.f("phiUc"), x.f("boundary_phiUc"), W, Ce, val, dS, rhs, mixbc(x, "Y"),       \
                  x.sch_w(0), x.sch_w(1));                                                                            \
   } while (0)
-  const char* ech = std::getenv("DFMI_YASM_CH");   // species per chunk, A/B knob (default 8)
-  const int ch = ech ? std::atoi(ech) : 8;
-  DFMI_SWITCH_S(x.S, CALL, if (ch == 4) GEN(4); else GEN(8))
+  DFMI_SWITCH_S(x.S, CALL, GEN(8))
 #undef GEN
 #undef CALL
 }

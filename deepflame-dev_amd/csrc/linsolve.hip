@@ -28,18 +28,13 @@ namespace {
 constexpr int TPB = 256;
 constexpr int NW = TPB / 64;
 constexpr int MAX_BLOCKS = 2048;
-// blocks of the even-odd half-row passes (DFMI_EO_BLOCKS): measured 256 / 512 / 768 / 1024 / 2048 / 3072 / 4096
+// blocks of the even-odd half-row passes: measured 256 / 512 / 768 / 1024 / 2048 / 3072 / 4096
 // -> 42.8 / 34.7 / 36.7 / 32.8 / 35.1 / 47.7 / 45.0 us per Schur application (the partial sums every consumer
 // block re-sums grow with the grid; fewer blocks leave too few waves)
-inline int eo_max_blocks() {
-  static const int v = [] { const char* e = std::getenv("DFMI_EO_BLOCKS"); return e ? std::max(64, std::atoi(e)) : 1024; }();
-  return v;
-}
-// blocks of the PCG kernels (DFMI_CG_BLOCKS, A/B)
-inline int cg_max_blocks() {
-  static const int v = [] { const char* e = std::getenv("DFMI_CG_BLOCKS"); return e ? std::max(64, std::min(MAX_BLOCKS, std::atoi(e))) : MAX_BLOCKS; }();
-  return v;
-}
+constexpr int EO_BLOCKS = 1024;
+inline int eo_max_blocks() { return EO_BLOCKS; }
+// blocks of the PCG kernels (1024 / 1536 / 2048: 43.2 / 38.9 / 37.8 us per k_cg_spmv, round 4)
+inline int cg_max_blocks() { return MAX_BLOCKS; }
 constexpr int PAD = INT_MIN;
 constexpr int NSCAL = 16;
 
@@ -1095,11 +1090,10 @@ int spmv_with_halo(Ctx& x, std::initializer_list<double*> vecs, int nsys, long C
   return 2 * nblk;
 }
 
-// one rank, no halo, a few thousand cells: each solve in one workgroup launch (DFMI_SMALL_SOLVE=0: off)
+// one rank, no halo, a few thousand cells: each solve in one workgroup launch (solver.small = 0: off)
 bool small_solve(const Ctx& x) {
   if (x.nranks != 1 || halo_active(x) || x.C > SMALL_C || x.C == 0) return false;
-  const char* e = std::getenv("DFMI_SMALL_SOLVE");
-  return !(e && std::atoi(e) == 0);
+  return x.on("solver.small");
 }
 
 // Convergence polling without draining the stream: after an iteration the solver state is copied into
@@ -1289,13 +1283,12 @@ void build_ell(Ctx& x) {
   // of odd extent does not colour and keeps the Jacobi path). Several ranks: each rank's (connected) local
   // graph is coloured, the colours across every processor face are exchanged, and the ranks' flips are solved
   // from the all-gathered relations so that every processor face couples the two colours too -- the same
-  // decision on every rank. DFMI_BCG_EO=0: off
+  // decision on every rank. solver.even_odd = 0: off
   x.ell.eo = 0;
   x.ell.eo_ncls = 0;
   x.ell.h_eo_pos.clear();
   const bool multi = x.nranks > 1 && x.halo != nullptr;
-  if (const char* e = std::getenv("DFMI_BCG_EO");
-      !(e && std::atoi(e) == 0) && !small_solve(x) && (multi || !halo_active(x))) {
+  if (x.on("solver.even_odd") && !small_solve(x) && (multi || !halo_active(x))) {
     std::vector<int> colr(C, 0), q;
     std::vector<char> seen(C, 0);
     bool bip = C >= 2;
@@ -1437,12 +1430,7 @@ void build_ell(Ctx& x) {
   // row classes: per cell the W (column offset, source code) pairs; coupled slots keep explicit sources
   // (slot ids are not relative to the cell) and processor columns explicit columns
   x.ell.ncls = 0;
-  {
-    const char* fv = std::getenv("DFMI_ROW_CLASSES_FV");
-    x.ell.fv_classes = fv && std::atoi(fv) != 0;
-  }
-  const char* rc = std::getenv("DFMI_ROW_CLASSES");
-  if (x.fslot && !(rc && std::atoi(rc) == 0)) {
+  if (x.fslot && x.on("solver.row_classes")) {
     std::map<std::vector<int>, int> ids;
     std::vector<uint8_t> cls(C);
     std::vector<int> key(2 * W);
@@ -1774,11 +1762,8 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, 0); }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());
-  // the symmetric p operator read face-wise on a hex box (FaceOp, one rank; DFMI_P_FACEFORM=0: the ELL values)
-  const bool face = [&] {
-    const char* e = std::getenv("DFMI_P_FACEFORM");
-    return x.hex[0] > 0 && x.fslot && x.nranks == 1 && !halo_active(x) && !small_solve(x) && !(e && std::atoi(e) == 0);
-  }();
+  // the symmetric p operator read face-wise on a hex box (FaceOp, one rank; pcg.face_form = 0: the ELL values)
+  const bool face = x.hex[0] > 0 && x.fslot && x.nranks == 1 && !halo_active(x) && !small_solve(x) && x.on("pcg.face_form");
   FaceOp<double> fo{};
   if (face) fo = FaceOp<double>{1, x.hex[0], x.hex[1], x.hex[2], C, upper, bc, x.ell.csStart.p, x.ell.csSlot.p,
                                 x.ell.scol.p};
@@ -1851,9 +1836,8 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   Poller poll(x, WS.scal.p, 1, std::string(eqn) + (amg ? "/amg" : "/jacobi"));
   double* pold = v.pa;
   double* pnew = v.pb;
-  // one rank: the update kernel also does the V-cycle's level-0 first sweep (DFMI_CG_FUSE=0: separate)
-  const bool fuse_l0 = amg && x.nranks == 1 && !halo_active(x) && amg_l0_fusable(x) && [] {
-    const char* e = std::getenv("DFMI_CG_FUSE"); return !(e && std::atoi(e) == 0); }();
+  // one rank: the update kernel also does the V-cycle's level-0 first sweep (pcg.fuse_l0 = 0: separate)
+  const bool fuse_l0 = amg && x.nranks == 1 && !halo_active(x) && amg_l0_fusable(x) && x.on("pcg.fuse_l0");
   for (int it = 0;; ++it) {
     const int np = spmv_with_halo(x, {v.z, pold}, 1, Ce, nblk, [&](RowSet rs) {
       dispatch_W(W, [&](auto wt) {

@@ -68,6 +68,7 @@ SIGNATURES = {
     "dfmi_solver_stats": [_P, C.c_char_p, _IP, _DP, _DP],
     "dfmi_solver_work": [_P, C.c_char_p, _DP, C.c_int],
     "dfmi_set_preconditioner": [_P, C.c_char_p, C.c_char_p],
+    "dfmi_set_option": [_P, C.c_char_p, C.c_double], "dfmi_get_option": [_P, C.c_char_p, _DP],
     "dfmi_amg_info": [_P, C.c_int, _IP, _IP, _IP],
     "dfmi_row_classes": [_P, _IP],
     "dfmi_hex_dims": [_P, _IP, _IP, _IP],
@@ -158,6 +159,21 @@ def _i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
+# Implementation options (include/dfmi.h dfmi_set_option) applied to every new HIP-library Context: the entries of
+# DEFAULT_OPTIONS (tests set them around a case) and of the environment variable DFMI_OPTIONS ("key=value,..."; for
+# runs in child processes and bench A/B runs). The library itself reads no option from the environment.
+DEFAULT_OPTIONS: dict = {}
+
+
+def env_options() -> dict:
+    out = {}
+    for item in os.environ.get("DFMI_OPTIONS", "").split(","):
+        if item.strip():
+            k, v = item.split("=")
+            out[k.strip()] = float(v)
+    return out
+
+
 class Context:
     """One device-resident database (one rank, one GPU)."""
 
@@ -167,6 +183,9 @@ class Context:
         self._keep = []
         self._call("dfmi_create", C.byref(h), device)
         self.h = h
+        if lib_path is None or os.path.abspath(lib_path) == LIB_PATH:
+            for k, v in {**env_options(), **DEFAULT_OPTIONS}.items():
+                self.set_option(k, v)
 
     def _call(self, name, *args):
         rc = getattr(self.lib, name)(*args)
@@ -297,6 +316,15 @@ class Context:
 
     def set_solver(self, eqn, max_iter, tol, abs_tol=0.0):
         self._call("dfmi_set_solver", self.h, eqn.encode(), int(max_iter), float(tol), float(abs_tol))
+
+    def set_option(self, key: str, value: float):
+        """implementation option (include/dfmi.h dfmi_set_option; INTEGRATION.md lists the keys)"""
+        self._call("dfmi_set_option", self.h, key.encode(), float(value))
+
+    def get_option(self, key: str) -> float:
+        v = C.c_double()
+        self._call("dfmi_get_option", self.h, key.encode(), C.byref(v))
+        return v.value
 
     def set_preconditioner(self, eqn, name):
         self._call("dfmi_set_preconditioner", self.h, eqn.encode(), name.encode())

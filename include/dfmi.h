@@ -191,8 +191,18 @@ int dfmi_set_solver(dfmi_ctx* ctx, const char* eqn, int max_iter, double tol, do
 /* preconditioner: "jacobi" (all) or "amg" (p; aggregation AMG V-cycle, the amgxpOptions
  * AGGREGATION solver's role) -- p defaults to "amg", U/Y/E to "jacobi" */
 int dfmi_set_preconditioner(dfmi_ctx* ctx, const char* eqn, const char* name);
+/* implementation options by key (the role of the reference's amgx*Options files, e.g.
+ * examples/dfLowMachFoam/notorch/threeD_reactingTGV/H2/cvodeIntegrator/system/amgxpOptions:1-18, and of the
+ * CanteraTorchProperties switches): "amg.*" (omega, overcorrection, coarsest_sweeps, coarsest_size,
+ * presweeps, pairwise_passes_l0, pairwise_passes, precision 32|64, padded, tail, halo_l0, global_coarse),
+ * "solver.*" (even_odd, small, row_classes), "pcg.*" (face_form, fuse_l0), "fv.*" (hex_walk, csr_walk,
+ * species_generic, yprep_brick), "chem.*" (method 0 ROS3 | 1 extrapolation, generated, binning),
+ * "dnn.tuned_gemm"; keys and
+ * defaults in INTEGRATION.md. Solver-structure keys must be set before the first solve; unknown keys fail. */
+int dfmi_set_option(dfmi_ctx* ctx, const char* key, double value);
+int dfmi_get_option(dfmi_ctx* ctx, const char* key, double* value);
 /* AMG hierarchy after the first p solve: level count, cells and ELL width per level (with several ranks
- * and DFMI_AMG_GLOBAL=1 the agglomerated coarsest level of all ranks is listed last) */
+ * and the option amg.global_coarse the agglomerated coarsest level of all ranks is listed last) */
 int dfmi_amg_info(dfmi_ctx* ctx, int max_levels, int* n_levels, int* cells, int* width);
 /* gather-row classes in use (0: explicit columns): after the first solve, the number of distinct
  * (column offset, coefficient source) rows the solver / assembly gathers decode from one byte per cell

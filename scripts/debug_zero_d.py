@@ -15,7 +15,7 @@ t = read_thermo_table(os.path.join(golden, "thermo_ES80_H2-7-16.txt"), ym["speci
 out = {}
 for tag, rtol, atol, generic in (("r10", 1e-10, 1e-20, 0), ("r12", 1e-12, 1e-22, 0), ("r10g", 1e-10, 1e-20, 1)):
     if generic:
-        os.environ["DFMI_CHEM_GENERIC"] = "1"
+        os.environ["DFMI_OPTIONS"] = "chem.generated=0"
     m = hex_box(2, 2, 2, lengths=(5e-3,) * 3, periodic=(False,) * 3)
     ctx = Context(0)
     case.setup_context(ctx, m, t, ym["species"].index("N2"), ref["dt"])
@@ -33,6 +33,6 @@ for tag, rtol, atol, generic in (("r10", 1e-10, 1e-20, 0), ("r12", 1e-12, 1e-22,
     out[tag] = np.array(T)
     out[tag + "_stats"] = np.array(steps)
     ctx.close()
-    os.environ.pop("DFMI_CHEM_GENERIC", None)
+    os.environ.pop("DFMI_OPTIONS", None)
     print(tag, "T_end", T[-1], "max dT vs oracle", np.abs(np.array(T) - np.array(ref["T"])).max(), flush=True)
 np.savez(os.path.join(ROOT, "gpurun_out", "zerod_traj.npz"), **out)

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 port=29555
-for v in ${VARS:-halo: bj:DFMI_AMG_HALO_L0=0}; do
+for v in ${VARS:-halo: bj:DFMI_OPTIONS=amg.halo_l0=0}; do
   name="${v%%:*}"; envs="${v#*:}"; port=$((port + 1))
   ( for e in $(echo "$envs" | tr ',' ' '); do export "$e"; done
     DFMI_RCCL_SPLIT_HOSTS=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

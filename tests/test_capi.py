@@ -83,3 +83,33 @@ def test_cpp_caller_runs_time_steps():
     assert r.returncode == 0, r.stderr + r.stdout
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["finite"] and d["cells"] == 4096 and d["mass_rel_change"] < 1e-6
+
+
+def test_environment_knobs_are_few_and_documented():
+    """the library reads at most a couple of process-level switches from the environment; everything else is a
+    dfmi_set_option key (knob sprawl), and every switch and key is in INTEGRATION.md's tables"""
+    csrc = os.path.join(ROOT, "deepflame-dev_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            names |= set(re.findall(r'getenv\("(DFMI_[A-Z0-9_]+)"\)', open(os.path.join(csrc, f)).read()))
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert len(names) <= 15, sorted(names)
+    assert all(f"`{n}`" in doc for n in names), sorted(names)
+    ctx_h = open(os.path.join(csrc, "dfmi_ctx.h")).read()
+    keys = re.findall(r'\{"([a-z0-9_]+\.[a-z0-9_]+)", ', ctx_h)
+    assert len(keys) >= 20
+    assert all(f"`{k}`" in doc or f"`{k.split('.')[0]}.{k.split('.')[1]}`" in doc or k in doc for k in keys), \
+        [k for k in keys if k not in doc]
+
+
+@pytest.mark.gpu
+def test_options_roundtrip_and_unknown_key():
+    from dfmi.lib import Context, DfmiError
+    ctx = Context(0)
+    assert ctx.get_option("amg.omega") == 0.9
+    ctx.set_option("amg.omega", 0.85)
+    assert ctx.get_option("amg.omega") == 0.85
+    with pytest.raises(DfmiError):
+        ctx.set_option("amg.no_such_key", 1)
+    ctx.close()

@@ -1,4 +1,4 @@
-"""The V-cycle's last two levels in one workgroup (amg.hip: k_vtail, DFMI_AMG_TAIL) must give bitwise the same
+"""The V-cycle's last two levels in one workgroup (amg.hip: k_vtail, option amg.tail) must give bitwise the same
 pressure solve as the launch chain it replaces (k_smooth_res_r8 + k_coarsest + k_prolong_smooth on those
 levels): the same expressions in the same order, the restriction summed over the same 8 lanes."""
 import os
@@ -12,11 +12,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(tail, dims):
-    from dfmi.lib import Context
+    from dfmi.lib import Context, DEFAULT_OPTIONS
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
-    os.environ["DFMI_AMG_TAIL"] = str(tail)
+    DEFAULT_OPTIONS["amg.tail"] = tail
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
         t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
@@ -38,7 +38,7 @@ def _run(tail, dims):
         ctx.close()
         return out
     finally:
-        os.environ.pop("DFMI_AMG_TAIL", None)
+        DEFAULT_OPTIONS.pop("amg.tail", None)
 
 
 # > 4096 cells (the batched solver, not the one-workgroup small solve); the second mesh puts a full 4096-cell

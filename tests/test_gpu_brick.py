@@ -1,7 +1,7 @@
 """LDS-staged YEqn preparation (fv_kernels.hip k_y_prep_brick): on a hex box in blockMesh order whose
 dimensions a 16 x 4 x 4 brick divides, Y_s and alpha hai_s of the brick and its face halo are staged in LDS
 and the face terms read them there. The faces, their order and every product are the face walk's, so the
-prepared fields and a whole outer iteration must be bitwise those of the plain kernel (DFMI_YPREP_BRICK=0)
+prepared fields and a whole outer iteration must be bitwise those of the plain kernel (option fv.yprep_brick = 0)
 -- with the species staged in two chunks (default) and all at once (=2), periodic and walled."""
 import os
 
@@ -14,13 +14,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(mode, periodic, mech="burke9"):
-    from dfmi.lib import Context
+    from dfmi.lib import Context, DEFAULT_OPTIONS
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
     files = {"burke9": ("Burke2012_s9r23.yaml", "thermo_Burke2012_s9r23.txt"),
              "es80": ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt")}[mech]
-    os.environ["DFMI_YPREP_BRICK"] = str(mode)
+    DEFAULT_OPTIONS["fv.yprep_brick"] = mode
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, files[0]))
         t = read_thermo_table(os.path.join(GOLDEN, files[1]), ym["species"])
@@ -41,7 +41,7 @@ def _run(mode, periodic, mech="burke9"):
         ctx.close()
         return out
     finally:
-        os.environ.pop("DFMI_YPREP_BRICK", None)
+        DEFAULT_OPTIONS.pop("fv.yprep_brick", None)
 
 
 @pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "walls"])

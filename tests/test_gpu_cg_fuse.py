@@ -1,4 +1,4 @@
-"""The PCG update fused with the AMG's level-0 first sweep (linsolve.hip: k_cg_x_smooth, DFMI_CG_FUSE)
+"""The PCG update fused with the AMG's level-0 first sweep (linsolve.hip: k_cg_x_smooth, option pcg.fuse_l0)
 must give bitwise the same pressure solve as the separate k_cg_x + k_smooth_res launches: the same
 residual expression for every neighbour, the same V-cycle precision and the same r.r block partials."""
 import os
@@ -12,11 +12,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(fuse):
-    from dfmi.lib import Context
+    from dfmi.lib import Context, DEFAULT_OPTIONS
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
-    os.environ["DFMI_CG_FUSE"] = str(fuse)
+    DEFAULT_OPTIONS["pcg.fuse_l0"] = fuse
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
         t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
@@ -38,7 +38,7 @@ def _run(fuse):
         ctx.close()
         return out
     finally:
-        os.environ.pop("DFMI_CG_FUSE", None)
+        DEFAULT_OPTIONS.pop("pcg.fuse_l0", None)
 
 
 def test_fused_pcg_update_is_bitwise_the_separate_launches():

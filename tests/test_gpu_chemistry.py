@@ -55,9 +55,10 @@ def _states(ym, n, seed=0):
                                   ("ES80_H2-7-16.yaml", "thermo_ES80_H2-7-16.txt")])
 def test_chem_rr_matches_oracle(mech, method, monkeypatch):
     from chem_oracle import Kinetics
-    monkeypatch.setenv("DFMI_CHEM_METHOD", method.split("-")[0])
+    from dfmi import lib
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "chem.method", 1 if method == "extrap" else 0)
     if method.endswith("generic"):
-        monkeypatch.setenv("DFMI_CHEM_GENERIC", "1")
+        monkeypatch.setitem(lib.DEFAULT_OPTIONS, "chem.generated", 0)
     ctx, m, ym, mc = _setup(*mech)
     C = m.n_cells
     T, p, rho, Y = _states(ym, C)
@@ -107,8 +108,9 @@ def test_chem_in_time_step():
 def test_chem_cost_binning_bitwise(mech, generic, monkeypatch):
     """Cells handed to the integrator in cost-binned order (the second solve is binned by the first
     one's step counts) give bitwise the results of the natural order."""
+    from dfmi import lib
     if generic:
-        monkeypatch.setenv("DFMI_CHEM_GENERIC", "1")
+        monkeypatch.setitem(lib.DEFAULT_OPTIONS, "chem.generated", 0)
     ctx, m, ym, mc = _setup(*mech, n=(16, 16, 8))
     C = m.n_cells
     T, p, rho, Y = _states(ym, C, seed=3)
@@ -116,7 +118,7 @@ def test_chem_cost_binning_bitwise(mech, generic, monkeypatch):
     ctx.chem_set_options(1)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("DFMI_CHEM_BIN", flag)
+        ctx.set_option("chem.binning", int(flag))
         ctx.set_field("chem_stats", np.zeros((3, C)))   # same start: no carried step sizes
         ctx.chem_solve(1e-6)
         ctx.chem_solve(1e-6)

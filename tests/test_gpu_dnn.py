@@ -148,14 +148,16 @@ def _check_half_semantics(RR, mods, T, p, rho, Y, xmu, xstd, ymu, ystd):
     assert per_species.max() < 4e-3, per_species
 
 
-@pytest.mark.parametrize("wide", ["0", "1", "2", "3"])
-def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
+@pytest.mark.parametrize("tuned", [0, 1])
+def test_dnn_53_species_matches_torch_fp32(tuned, monkeypatch):
     """BASELINE config 4's surrogate shape: 53 species, 52 nets [55, 1600, 800, 400, 1] with
     seeded weights and synthetic normalisation, on a small mesh; the context takes 53 species for the
-    surrogate path (the FV kernels are not instantiated for it). wide: the 1600 -> 800 layer through
-    k_mlp_gemm (0, production) or the 256x256x64 A/B kernels (1 interleaved, 2 not, 3 ping-pong)."""
+    surrogate path (the FV kernels are not instantiated for it). tuned: the production shape-tuned kernels
+    (option dnn.tuned_gemm = 1: the ping-pong 256x256x64 wide-layer kernel with tail strips, the 128x128
+    input-layer kernel, the fused output layer) or k_mlp_gemm for every layer (0)."""
     import torch
-    monkeypatch.setenv("DFMI_DNN_WIDE", wide)
+    from dfmi import lib
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "dnn.tuned_gemm", tuned)
     from dfmi.mesh import hex_box
     from dfmi.lib import Context
     from dfmi import case, dnn_model
@@ -217,9 +219,9 @@ def test_dnn_53_species_matches_torch_fp32(wide, monkeypatch):
 
 
 def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
-    """The 256x256x64 wide-layer kernels (DFMI_DNN_WIDE=1 interleaved, 3 ping-pong: staggered wave groups,
-    one-phase half-tile restaging) and the 128x128 input-layer kernel (DFMI_DNN_IN=1, four workgroups per CU)
-    issue the same MFMA sequence per output as k_mlp_gemm, so the source
+    """The 256x256x64 ping-pong wide-layer kernel (staggered wave groups, one-phase half-tile restaging, the
+    800-wide layer's tail columns as two 16-column strips) and the 128x128 input-layer kernel (four workgroups per
+    CU) issue the same MFMA sequence per output as k_mlp_gemm (option dnn.tuned_gemm = 0), so the source
     terms of 32,768 reacting cells x 52 nets agree bitwise -- a race in a pipeline's LDS reuse would show here
     (128 row tiles x 4 column tiles x 52 nets per launch, every CU busy)."""
     from dfmi.mesh import hex_box
@@ -237,19 +239,9 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
     p = np.full(C, 101325.0)
     rho = p / (300.0 * T)
     out = {}
-    # (DFMI_DNN_WIDE, DFMI_DNN_IN, DFMI_DNN_TAIL): "0" = k_mlp_gemm for every layer; "3" the ping-pong kernel with
-    # the 800-wide layer's tail columns as two 16-column strips in its second and third tiles, "3w" as one
-    # 32-column strip in the third, "3n" in a fourth tile
-    # "3i": the 64-row input-layer tile; "3v": the fused-output layer's last tile with its column blocks
-    # interleaved over the wave columns (DFMI_DNN_OUT_ILV=1)
-    variants = {"0": ("0", "0", "0", "0"), "1": ("1", "1", "0", "0"), "3": ("3", "1", "16", "0"),
-                "3w": ("3", "1", "32", "0"), "3n": ("3", "1", "0", "0"), "3i": ("3", "2", "16", "0"),
-                "3v": ("3", "1", "16", "1")}
-    for wide, (w, i, t, o) in variants.items():
-        monkeypatch.setenv("DFMI_DNN_WIDE", w)
-        monkeypatch.setenv("DFMI_DNN_IN", i)
-        monkeypatch.setenv("DFMI_DNN_TAIL", t)
-        monkeypatch.setenv("DFMI_DNN_OUT_ILV", o)
+    from dfmi import lib
+    for wide in ("0", "1"):
+        monkeypatch.setitem(lib.DEFAULT_OPTIONS, "dnn.tuned_gemm", int(wide))
         ctx = Context(0)
         pt = case.default_patch_types(m)
         rows, cols = m.proc_rows_cols()
@@ -269,5 +261,4 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
         out[wide] = ctx.get_field("RR", (S, C))
         ctx.close()
     assert np.isfinite(out["0"]).all()
-    for wide in ("1", "3", "3w", "3n", "3i", "3v"):
-        assert np.array_equal(out[wide], out["0"]), (wide, np.abs(out[wide] - out["0"]).max())
+    assert np.array_equal(out["1"], out["0"]), np.abs(out["1"] - out["0"]).max()

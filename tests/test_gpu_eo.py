@@ -5,10 +5,10 @@ Jacobi-scaled system is solved on the colour-1 Schur complement and colour 0 is 
 Same stopping test as the Jacobi path (AmgX RELATIVE_INI_CORE on the full residual): at tight tolerances
 one outer iteration reaches the oracle's exact solves (the same 1e-9..1e-11 bounds as
 test_gpu_parity.test_full_outer_iteration); at production tolerances it needs no more iterations than the
-Jacobi path (DFMI_BCG_EO=0) and agrees with it to the solver tolerance; it is bitwise repeatable. A mesh
+Jacobi path (option solver.even_odd = 0) and agrees with it to the solver tolerance; it is bitwise repeatable. A mesh
 that does not 2-colour (a periodic direction of odd extent) keeps the Jacobi path.
 The layout is decided when the gather rows are built, so the environment is set before the context
-exists; DFMI_SMALL_SOLVE=0 keeps these small meshes off the one-workgroup path.
+exists; solver.small = 0 keeps these small meshes off the one-workgroup path.
 """
 import numpy as np
 import pytest
@@ -43,8 +43,9 @@ CASES = {
 
 
 def _make(name, monkeypatch, eo=True):
-    monkeypatch.setenv("DFMI_SMALL_SOLVE", "0")
-    monkeypatch.setenv("DFMI_BCG_EO", "1" if eo else "0")
+    from dfmi import lib
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "solver.small", 0)
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "solver.even_odd", 1 if eo else 0)
     kw, _ = CASES[name]
     return _case(**kw)
 

@@ -101,19 +101,20 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
         except Exception as e:   # surfaced below
             err[r] = e
 
-    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work), `env` (AMG knobs) at the
-    # first pressure solve
+    # DFMI_HALO_OVERLAP is read when a rank's communicator is set up (inside work); `env` holds AMG options
+    # (dfmi_set_option) every rank's context takes at creation
+    from dfmi import lib
     prev = os.environ.get("DFMI_HALO_OVERLAP")
     os.environ["DFMI_HALO_OVERLAP"] = "1" if overlap else "0"
     for k, v in (env or {}).items():
-        os.environ[k] = v
+        lib.DEFAULT_OPTIONS[k] = v
     th = [threading.Thread(target=work, args=(r,)) for r in range(nr)]
     for x in th:
         x.start()
     for x in th:
         x.join(timeout=300)
     for k in (env or {}):
-        os.environ.pop(k, None)
+        lib.DEFAULT_OPTIONS.pop(k, None)
     if prev is None:
         os.environ.pop("DFMI_HALO_OVERLAP", None)
     else:
@@ -324,8 +325,8 @@ def test_overlapped_halo_walls_two_steps():
         assert e < 1e-9, (n, e)
 
 
-@pytest.mark.parametrize("env", [{"DFMI_AMG_HALO_L0": "0"}, {"DFMI_AMG_GLOBAL": "1"},
-                                 {"DFMI_AMG_GLOBAL": "1", "DFMI_AMG_HALO_L0": "0"}], ids=["blockjacobi", "global", "global-bj"])
+@pytest.mark.parametrize("env", [{"amg.halo_l0": 0}, {"amg.global_coarse": 1},
+                                 {"amg.global_coarse": 1, "amg.halo_l0": 0}], ids=["blockjacobi", "global", "global-bj"])
 def test_decomposed_amg_variants_match_oracle(env):
     """the decomposed-AMG variants (level 0 smoothed with its processor couplings -- the default -- or
     block-Jacobi; the opt-in agglomerated coarsest level of all ranks) precondition the same PCG: one outer
@@ -343,7 +344,7 @@ def test_halo_coupled_level0_needs_fewer_pcg_iterations():
     """the V-cycle's level 0 with its processor couplings (default) against block-Jacobi across ranks: the same
     solution, fewer p-iterations (2 x 2 x 2 ranks of 16^3)"""
     ref, hal = _run(32, 32, 32, (2, 2, 2), n_steps=2)
-    _, bj = _run(32, 32, 32, (2, 2, 2), n_steps=2, env={"DFMI_AMG_HALO_L0": "0"})
+    _, bj = _run(32, 32, 32, (2, 2, 2), n_steps=2, env={"amg.halo_l0": 0})
     print("p-iterations: halo-coupled", hal["p_iters"], "block-Jacobi", bj["p_iters"])
     assert hal["p_iters"] < bj["p_iters"], (hal["p_iters"], bj["p_iters"])
     for n in ("T", "p", "rho", "he", "U", "Y"):

@@ -102,30 +102,22 @@ def _oracle(m, t, st, pt, inert, dt):
 
 
 # es80 / burke9: register-resident species templates; "-generic": the same cases through the
-# species-chunked kernels (DFMI_SPECIES_GENERIC=1) that large mechanisms run; gri53: 53 species
+# species-chunked kernels (option fv.species_generic) that large mechanisms run; gri53: 53 species
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
                                         "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
-                                        "mixed", "mixed-generic", "walls-trav", "burke9-zm", "walls-zm", "gri53-walls-split"])
+                                        "mixed", "mixed-generic", "walls-trav"])
 def periodic(request):
-    zm = request.param.endswith("-zm")      # the z-marching YEqn kernels (A/B path, 16 x 16 column tiles)
-    if zm:
-        for k in ("DFMI_YPREP_ZM", "DFMI_YASM_ZM", "DFMI_ZM_KZ"):
-            os.environ[k] = "3" if k == "DFMI_ZM_KZ" else "1"
-            request.addfinalizer(lambda k=k: os.environ.pop(k, None))
+    from dfmi import lib
     generic = request.param.endswith("-generic")
     if generic:
-        os.environ["DFMI_SPECIES_GENERIC"] = "1"
-        request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
+        lib.DEFAULT_OPTIONS["fv.species_generic"] = 1
+        request.addfinalizer(lambda: lib.DEFAULT_OPTIONS.pop("fv.species_generic", None))
     if request.param.endswith("-csr"):     # face loops by the CSR walk instead of the gather rows
-        os.environ["DFMI_FACE_CSR"] = "1"
-        request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
-    if request.param.endswith("-split"):   # other species ranges per launch of the chunked YEqn kernels
-        for k, v in (("DFMI_YPREP_LCH", "4"), ("DFMI_YASM_LCH", "16")):
-            os.environ[k] = v
-            request.addfinalizer(lambda k=k: os.environ.pop(k, None))
+        lib.DEFAULT_OPTIONS["fv.csr_walk"] = 1
+        request.addfinalizer(lambda: lib.DEFAULT_OPTIONS.pop("fv.csr_walk", None))
     traversal = request.param.endswith("-trav")
-    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "").replace("-zm", "").replace("-split", "")
+    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
@@ -156,10 +148,8 @@ def periodic(request):
             return fv
         # "distorted": the same walls on a non-orthogonal mesh read from constant/polyMesh files
         return _case(periodic=False, walls=walls, mech=mech, distorted=param == "distorted", renumber=renumber,
-                     mixed=mixed, traversal=traversal, nx=16 if (traversal or zm) else 6,
-                     ny=16 if zm else 12 if traversal else 5, nz=8 if (traversal or zm) else 4)
-    if zm:   # 16 x 16 x 8 in segments of 3 planes: a short last segment, -z faces across segment starts
-        return _case(mech=param, nx=16, ny=16, nz=8)
+                     mixed=mixed, traversal=traversal, nx=16 if traversal else 6,
+                     ny=12 if traversal else 5, nz=8 if traversal else 4)
     return _case(mech=param, renumber=renumber, nx=16 if renumber else 6, ny=8 if renumber else 5,
                  nz=4 if renumber else 4)
 
@@ -353,8 +343,9 @@ def test_amg_pcg_full_step(coarsest, prec, monkeypatch):
     """AMG-preconditioned p solves (multi-level hierarchy forced on a small mesh) reach the oracle's
     exact solution with the V-cycle in fp32 (default) or fp64 -- the preconditioner's precision
     changes the iteration count, not the attainable accuracy; AMG needs fewer iterations than Jacobi."""
-    monkeypatch.setenv("DFMI_AMG_COARSEST", coarsest)
-    monkeypatch.setenv("DFMI_AMG_PREC", prec)
+    from dfmi import lib
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.coarsest_size", int(coarsest))
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.precision", 64 if prec == "f64" else 32)
     ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
     for e in ("U", "Y", "E"):
         ctx.set_solver(e, 300, 1e-15, 1e-300)
@@ -378,17 +369,17 @@ def test_amg_pcg_full_step(coarsest, prec, monkeypatch):
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 def test_small_solves_match_batched_path(prec, monkeypatch):
     """Systems of <= 4096 cells on one rank are solved in one workgroup per system (k_bcg_small /
-    k_pcg_small with the V-cycle inside); the batched multi-launch path (DFMI_SMALL_SOLVE=0) is what
+    k_pcg_small with the V-cycle inside); the batched multi-launch path (option solver.small = 0) is what
     larger meshes run. Same formulas and stopping tests, reductions grouped differently: the two reach
     the same solution (tight tolerances) and the same iteration counts (within one) at production
     tolerances."""
-    from dfmi import case
-    monkeypatch.setenv("DFMI_AMG_PREC", prec)
-    monkeypatch.setenv("DFMI_AMG_COARSEST", "64")      # a multi-level hierarchy on this mesh
+    from dfmi import case, lib
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.precision", 64 if prec == "f64" else 32)
+    monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.coarsest_size", 64)      # a multi-level hierarchy on this mesh
     ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
     res = {}
     for small in ("1", "0"):
-        monkeypatch.setenv("DFMI_SMALL_SOLVE", small)
+        ctx.set_option("solver.small", int(small))
         out = {}
         for tight in (True, False):
             case.push_state(ctx, st)

@@ -2,7 +2,7 @@
 gather row is one of 27 (column offset, coefficient source) patterns, so the solver SpMVs, the AMG level-0
 sweeps and the assembly face loops decode a cell's row from one byte instead of reading 2 W explicit ints.
 The decoded columns and sources are the explicit ones, so a whole outer iteration must be bitwise the run
-with DFMI_ROW_CLASSES=0 -- periodic (cyclic partner offsets in the table), walled (padding entries) and
+with the option solver.row_classes = 0 -- periodic (cyclic partner offsets in the table), walled (padding entries) and
 decomposed (processor halo columns read explicitly) meshes."""
 import os
 
@@ -15,13 +15,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(classes, periodic, env=None):
-    from dfmi.lib import Context
+    from dfmi.lib import Context, DEFAULT_OPTIONS
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
-    os.environ["DFMI_ROW_CLASSES"] = str(classes)
+    DEFAULT_OPTIONS["solver.row_classes"] = classes
     for k, v in (env or {}).items():
-        os.environ[k] = v
+        DEFAULT_OPTIONS[k] = v
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
         t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
@@ -41,9 +41,9 @@ def _run(classes, periodic, env=None):
         ctx.close()
         return out
     finally:
-        os.environ.pop("DFMI_ROW_CLASSES", None)
+        DEFAULT_OPTIONS.pop("solver.row_classes", None)
         for k in (env or {}):
-            os.environ.pop(k, None)
+            DEFAULT_OPTIONS.pop(k, None)
 
 
 @pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "walls"])
@@ -59,8 +59,8 @@ def test_row_classes_bitwise_explicit_rows(periodic):
 def test_hex_face_walk_bitwise_explicit_rows(periodic):
     """the computed hex face walk (each_face<-1>) against the ELL-row and CSR walks: bitwise"""
     a = _run(1, periodic)
-    b = _run(1, periodic, {"DFMI_FACE_HEX": "0"})
-    c = _run(1, periodic, {"DFMI_FACE_HEX": "0", "DFMI_FACE_CSR": "1"})
+    b = _run(1, periodic, {"fv.hex_walk": 0})
+    c = _run(1, periodic, {"fv.hex_walk": 0, "fv.csr_walk": 1})
     assert a["hex"] == (20, 18, 14), a["hex"]
     assert a["iters"] == b["iters"] == c["iters"], (a["iters"], b["iters"], c["iters"])
     for k in ("p", "T", "rho", "he", "U", "Y"):
@@ -72,7 +72,7 @@ def test_face_form_pressure_operator_bitwise_ell(periodic):
     """the symmetric p operator read face-wise (FaceOp: PCG SpMVs and the fp32 AMG level 0 from the face and
     slot coefficients) against the ELL values: the same entries in the same order, so bitwise"""
     a = _run(1, periodic)
-    b = _run(1, periodic, {"DFMI_P_FACEFORM": "0"})
+    b = _run(1, periodic, {"pcg.face_form": 0})
     assert a["iters"] == b["iters"], (a["iters"], b["iters"])
     for k in ("p", "T", "rho", "he", "U", "Y"):
         assert np.array_equal(a[k], b[k]), k

@@ -52,13 +52,14 @@ def _walls(mixed=False):
 @pytest.fixture(scope="module", params=["ref-periodic", "ll-periodic", "ll-walls", "ref-distorted", "ll-mixed",
                                         "ll-periodic-generic", "ll-walls-csr", "ref-gri53"])
 def sc(request):
+    from dfmi import lib
     p = request.param
     if p.endswith("-generic"):
-        os.environ["DFMI_SPECIES_GENERIC"] = "1"
-        request.addfinalizer(lambda: os.environ.pop("DFMI_SPECIES_GENERIC", None))
+        lib.DEFAULT_OPTIONS["fv.species_generic"] = 1
+        request.addfinalizer(lambda: lib.DEFAULT_OPTIONS.pop("fv.species_generic", None))
     if p.endswith("-csr"):
-        os.environ["DFMI_FACE_CSR"] = "1"
-        request.addfinalizer(lambda: os.environ.pop("DFMI_FACE_CSR", None))
+        lib.DEFAULT_OPTIONS["fv.csr_walk"] = 1
+        request.addfinalizer(lambda: lib.DEFAULT_OPTIONS.pop("fv.csr_walk", None))
     schemes = REF if p.startswith("ref") else LL
     kind = p.split("-")[1]
     if kind == "periodic":
