@@ -91,6 +91,28 @@ template <class T> struct PinnedBuf {
   }
 };
 
+// Convergence record a solver kernel posts into host-coherent pinned memory (linsolve.hip Poller): the host
+// spins on `seq` (stored last, system-scope release) instead of waiting on an event behind a copy.
+struct PollRec {
+  long long seq;       // snapshot number, written last
+  int stopped;         // every system of the solve has stopped
+  int iters;           // the largest iteration count among the systems
+};
+struct HostRecs {      // two alternating records, mapped into the device's address space
+  PollRec* h = nullptr;
+  PollRec* d = nullptr;
+  HostRecs() = default;
+  HostRecs(const HostRecs&) = delete;
+  HostRecs& operator=(const HostRecs&) = delete;
+  ~HostRecs() { if (h) (void)hipHostFree(h); }
+  void ensure() {
+    if (h) return;
+    DFMI_HIP(hipHostMalloc((void**)&h, 2 * sizeof(PollRec), hipHostMallocCoherent | hipHostMallocMapped));
+    for (int i = 0; i < 2; ++i) { h[i].seq = 0; h[i].stopped = 0; h[i].iters = 0; }
+    DFMI_HIP(hipHostGetDevicePointer((void**)&d, h, 0));
+  }
+};
+
 inline int blocks_for(long n, int tpb) { return (int)((n + tpb - 1) / tpb); }
 
 // Columns of the per-cell gather rows [W][C] (the solver ELL, linsolve.hip build_ell). Row classes: on

@@ -350,8 +350,8 @@ struct Ctx {
   struct SolverWs {
     DevBuf<double> buf, scal, red_local, red_all;
     DevBuf<int> sysmap;
-    PinnedBuf<double> poll;          // two convergence snapshots (linsolve.hip: Poller)
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    HostRecs poll;                   // convergence records the device posts (linsolve.hip: Poller)
+    long long poll_seq = 0;          // records posted so far
   } ws, ws_y;
   // the YEqn batch has its own solver workspace (its rows are assembled while the UEqn solve may still be
   // running on the other stream, dfmi_time_step); linsolve.hip reaches the current one through sws()

@@ -145,8 +145,7 @@ void halo_destroy(Halo* h) { delete h; }
 Ctx::~Ctx() {
   halo_destroy(halo);
   halo = nullptr;
-  for (auto& e : ws.ev) if (e) (void)hipEventDestroy(e);
-  for (auto& e : ws_y.ev) if (e) (void)hipEventDestroy(e);
+  if (stream) (void)hipStreamSynchronize(stream);   // no posted convergence record in flight into freed memory
   if (stream2) { (void)hipStreamSynchronize(stream2); (void)hipStreamDestroy(stream2); }
   if (ev_fork) (void)hipEventDestroy(ev_fork);
   if (ev_join) (void)hipEventDestroy(ev_join);

@@ -1096,53 +1096,79 @@ bool small_solve(const Ctx& x) {
   return x.on("solver.small");
 }
 
-// Convergence polling without draining the stream: after an iteration the solver state is copied into
-// pinned host memory behind an event, and the host reads the snapshot of an EARLIER check -- the GPU is
-// already running the next iteration(s) by then (systems that stopped turn every kernel into an early
-// return), so the queue never empties inside a solve. The decision is a pure function of the globally
-// reduced scalars, identical on every rank.
+// Convergence polling without draining the stream: after an iteration a one-wave kernel posts the solve's state
+// (every system stopped?, iterations) into host-coherent pinned memory, and the host reads the record of an
+// EARLIER check -- the GPU is already running the next iteration(s) by then (systems that stopped turn every
+// kernel into an early return), so the queue never empties inside a solve. The decision is a pure function of
+// the globally reduced scalars, identical on every rank.
 // Cadence (round 5): the iterations the previous solve of the same equation needed (`expect`, 0 = none yet)
-// place the checks. Before expect - 1 a snapshot every 4 iterations (a solve that converges early costs a
-// few early-return launches more); from there a snapshot after EVERY iteration, each check reading the one
-// an iteration back, so a converged solve is stopped one iteration after the one that set its flag. The
-// round-4 cadence (a snapshot every 2 iterations, read 2 later) ran 3-4 iterations of early-return launches
-// after every solve (~4.7 us each: 0.3 ms per p-solve, ~1.2 ms per step, profiles/r05_timeline.json).
+// place the checks. Before expect - 1 a record every 4 iterations (a solve that converges early costs a few
+// early-return launches more); from there a record after EVERY iteration, each check reading the one an
+// iteration back, so a converged solve is stopped one iteration after the one that set its flag. The round-4
+// cadence (a snapshot every 2 iterations, read 2 later) ran 3-4 iterations of early-return launches after every
+// solve (~4.7 us each: 0.3 ms per p-solve, ~1.2 ms per step, profiles/r05_timeline_poll.json), and each
+// snapshot was a device-to-host copy plus an event (~10 us of the stream); the posted record is one small launch.
+__global__ void k_poll_post(const double* __restrict__ scal, int nsys, PollRec* rec, long long seq) {
+  const int lane = threadIdx.x;   // one wave; lane s reads system s (vector loads, vector stores)
+  int act = 0, it = 0;
+  for (int s = lane; s < nsys; s += 64) {
+    act |= scal[s * NSCAL + 6] != 0.0;
+    it = max(it, (int)scal[s * NSCAL + 7]);
+  }
+  for (int o = 32; o > 0; o >>= 1) { act |= __shfl_xor(act, o, 64); it = max(it, __shfl_xor(it, o, 64)); }
+  if (lane == 0) {
+    PollRec* r = rec + (seq & 1);
+    r->stopped = act ? 0 : 1;
+    r->iters = it;
+    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 struct Poller {
   Ctx& x;
   const double* scal;
-  int nsys, slot = 0, pending = -1;
+  int nsys;
+  long long pending = 0;   // the record a check waits for (0: none)
   int expect;
   std::string key;
   Poller(Ctx& c, const double* s, int n, const std::string& k) : x(c), scal(s), nsys(n), key(k) {
-    x.sws().poll.ensure((size_t)2 * n * NSCAL);
-    for (auto& e : x.sws().ev)
-      if (!e) DFMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    x.sws().poll.ensure();
     auto f = x.solve_expect.find(key);
     expect = f == x.solve_expect.end() ? 0 : f->second;
   }
-  // after iteration `it` (0-based) has been enqueued: snapshot when the cadence says so; true when an
-  // earlier snapshot shows every system stopped (its iteration count becomes the next solve's `expect`)
+  // wait (spinning) until record `seq` or a later one is posted; a stream that drained without posting it
+  // (a failed launch) is an error rather than a hang
+  const PollRec& wait(long long seq) {
+    const PollRec* r = x.sws().poll.h + (seq & 1);
+    for (long spins = 0;; ++spins) {
+      if (__atomic_load_n(&r->seq, __ATOMIC_ACQUIRE) >= seq) return *r;
+      if ((spins & 0xfff) == 0xfff) {
+        const hipError_t q = hipStreamQuery(x.stream);
+        if (q != hipErrorNotReady && __atomic_load_n(&r->seq, __ATOMIC_ACQUIRE) < seq) {
+          DFMI_HIP(q);
+          throw Error("solver poll: the stream drained without posting its convergence record");
+        }
+      }
+    }
+  }
+  // after iteration `it` (0-based) has been enqueued: post a record when the cadence says so; true when an
+  // earlier record shows every system stopped (its iteration count becomes the next solve's `expect`)
   bool after(int it) {
     const int n = it + 1;
     const bool snap = expect > 0 ? (n >= expect - 1 || n % 4 == 0) : (n % 2 == 0);
     if (!snap) return false;
-    double* dst = x.sws().poll.p + (size_t)slot * nsys * NSCAL;
-    DFMI_HIP(hipMemcpyAsync(dst, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
-    DFMI_HIP(hipEventRecord(x.sws().ev[slot], x.stream));
+    const long long seq = ++x.sws().poll_seq;
+    hipLaunchKernelGGL(k_poll_post, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.sws().poll.d, seq);
+    DFMI_HIP(hipGetLastError());
     bool done = false;
-    if (pending >= 0) {
-      DFMI_HIP(hipEventSynchronize(x.sws().ev[pending]));
-      const double* h = x.sws().poll.p + (size_t)pending * nsys * NSCAL;
-      done = true;
-      int iters = 0;
-      for (int s = 0; s < nsys; ++s) {
-        done = done && h[s * NSCAL + 6] == 0.0;
-        iters = std::max(iters, (int)h[s * NSCAL + 7]);
+    if (pending > 0) {
+      const PollRec& r = wait(pending);
+      if (r.stopped) {
+        done = true;
+        x.solve_expect[key] = r.iters;
       }
-      if (done) x.solve_expect[key] = iters;
     }
-    pending = slot;
-    slot ^= 1;
+    pending = seq;
     return done;
   }
 };
