@@ -33,6 +33,7 @@
 
 #define DFMI_HD   // the generated kinetics run on the host here
 #define DFMI_SCHED_FENCE()   // scheduling barrier of the device build only
+#define DFMI_CONTRACT() do {} while (0)   // FMA contraction of the device build only
 #pragma GCC diagnostic push
 #pragma GCC diagnostic ignored "-Wunused-variable"
 #include "../../deepflame-dev_amd/csrc/chem_gen_burke9.inc"

@@ -27,6 +27,7 @@ struct AmgLevel {
 // the preconditioner's HBM traffic halves. amg.precision = 64 keeps the whole hierarchy in double.
 struct Amg {
   bool ready = false;
+  bool reuse_ok = false;   // set by dfmi_time_step for its later correctors (option amg.reuse)
   bool fp32 = true;
   double omega = 0.9;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)

@@ -662,7 +662,9 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
       thermo_rho_from_psi(x);
       thermo_psip0(x);
       u_hbya(x);
+      x.amg.reuse_ok = i > 0;         // a later corrector may precondition with this step's first hierarchy
       do_p(x);
+      x.amg.reuse_ok = false;
       thermo_correct_psip_rho(x);
       rho_process(x, false);
     }

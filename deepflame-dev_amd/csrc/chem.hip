@@ -538,6 +538,9 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 // between the reactions of the fused rates + Jacobian pass: nothing is scheduled across, so one reaction's
 // temporaries die before the next one's loads are issued (the register peak is J plus one reaction)
 #define DFMI_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// products contracted into FMAs inside the generated kinetics (the library builds with -ffp-contract=off for the
+// bitwise FV kernels; the chemistry is checked against SciPy BDF to a tolerance, not bitwise)
+#define DFMI_CONTRACT() _Pragma("clang fp contract(fast)") do {} while (0)
 #include "chem_gen_burke9.inc"
 #include "chem_gen_es80.inc"
 #pragma clang diagnostic pop

@@ -238,6 +238,8 @@ inline const OptDef* option_defs(int& n) {
     {"amg.tail", 1},                  // the last two levels in one workgroup launch (k_vtail)
     {"amg.halo_l0", 1},               // several ranks: level 0 keeps its processor couplings
     {"amg.global_coarse", 0},         // several ranks: one agglomerated coarsest level
+    {"amg.reuse", 1},                 // later correctors of a time step precondition with the step's first V-cycle
+                                      // operators (level-0 fp32 copy, Galerkin levels) instead of rebuilding them
     {"solver.even_odd", 1},           // U/Y/E: BiCGStab on the even-odd Schur complement where the rows 2-colour
     {"solver.small", 1},              // one rank, <= 4096 cells: every solve in one workgroup
     {"solver.row_classes", 1},        // solver rows decoded from one byte per cell where the mesh allows

@@ -1797,7 +1797,10 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     if (!x.amg.ready) amg_setup(x);
     x.amg.face = face && amg_l0_fusable(x) && x.amg.l0_sweeps == 1;
     x.amg.dfo = fo;
-    amg_galerkin(x, val, v.dS);
+    // a later corrector of the same step (amg.reuse): the V-cycle keeps the operators the first corrector built --
+    // a fixed SPD preconditioner of a matrix that changed by the density update only, so PCG still converges to
+    // this system's own tolerance; the fp32 rounding and Galerkin sums of one solve are saved
+    if (!(x.amg.reuse_ok && x.on("amg.reuse") && x.nranks == 1)) amg_galerkin(x, val, v.dS);
     if (x.amg.halo_l0) {   // the level-0 diagonal across processor faces, once per solve
       halo_vecs(x, {v.dS}, 1, Ce);
       x.amg.dS_full = v.dS;

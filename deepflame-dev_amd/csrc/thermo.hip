@@ -56,6 +56,9 @@ template <int S>
 __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, double& he, double p, const double* y,
                                              double& psi, double& rho, double& mu, double& alpha, double* rhoD,
                                              double* hai) {
+  // products contracted into FMAs (the result agrees with the oracle to rounding either way): ~30 % fewer
+  // VALU instructions in the O(S^2) rows of this FP64-issue-bound kernel
+#pragma clang fp contract(fast)
   double X[S], rw[S], ryw[S];
   double sum = 0.;
 #pragma unroll
