@@ -878,7 +878,8 @@ void apply_t(Ctx& x, const double* val0, const double* D0, ColView col0, const d
   // the last two levels in one workgroup (k_vtail): the down loop stops above level L - 2
   const bool tail = F && a.tail;
   const int ldown = tail ? L - 2 : L - 1;
-  // down: smooth from zero + residual, restrict
+  // down: smooth from zero + residual, restrict (folding the level-0 restriction into level 1's launch, each level-1
+  // thread summing its own and its six neighbours' member residuals, measured 14.6 -> 15.1-15.3 ms per step, round 5)
   for (int l = 0; l < ldown; ++l) {
     AmgLevel& f = a.lv[l];
     const dim3 g(blocks_for(f.n, TPB));

@@ -348,22 +348,35 @@ __device__ bool ros3(const ChemMech& m, const Lane<S>& L, double T, const double
 
 // ---- cost binning: a wave runs as long as its slowest lane, so cells are handed to the integrator
 // ordered by the integrator steps (accepted + rejected) they took in the previous solve, most
-// expensive first. Counting sort over NBIN buckets, stable inside a bucket (ascending cell index, so
-// the gathers of T, rho, Y stay mostly coalesced). Every cell's integration is independent of its
-// position, so the order changes timing only, never results.
-constexpr int NBIN = 32, BCB = 256, BCELLS = 4096;   // 4096 cells per binning block, 16 passes of 256
+// expensive first. The unit is a group of GRP consecutive cells (costed by its most expensive cell). GRP = 1:
+// single cells. Measured (round 5, 2M headline): single-cell binning scatters a bucket's cells over the mesh (PMC
+// traffic 1.8 GB per solve, 4.4x the state's 0.42 GB) but keeps every wave's lanes at the same cost (wave
+// efficiency 1.0): 1.05 ms; groups of 8 (whole 64-B lines per wave: 0.6 GB, 1.44x) lose that (efficiency 0.61):
+// 1.25 ms -- the kernel is bound by its FP64 issue, not by these bytes. Counting sort over NBIN buckets, stable
+// inside a bucket (ascending group index). Every cell's integration is independent of its position, so the
+// order changes timing only, never results.
+constexpr int NBIN = 32, BCB = 256, BCELLS = 4096, GRP = 1;   // 4096 groups per binning block, 16 passes of 256
 __device__ inline int cost_bin(double st, double rj) {
   const int c = (int)(st + rj);
   return NBIN - 1 - (c < 0 ? NBIN - 1 : (c > NBIN - 1 ? NBIN - 1 : c));   // bucket 0 = most expensive
 }
+// bucket of group g: its most expensive cell (steps + rejects; a failed cell, steps < 0, is most expensive)
+__device__ inline int group_bin(long n, const double* __restrict__ stats, long g) {
+  int b = NBIN - 1;
+  for (long c = g * GRP; c < n && c < (g + 1) * GRP; ++c) b = min(b, cost_bin(stats[c], stats[n + c]));
+  return b;
+}
+// the cell lane t integrates: group perm[t / GRP], its (t % GRP)-th cell (>= n: no cell)
+__device__ inline long bin_cell(const int* perm, long t) { return perm ? (long)perm[t / GRP] * GRP + t % GRP : t; }
 // per-block bucket counts, bucket-major [NBIN][nb]
 __global__ void __launch_bounds__(BCB) k_bin_count(long n, const double* __restrict__ stats, int nb, int* __restrict__ cnt) {
+  const long ng = (n + GRP - 1) / GRP;
   __shared__ int h[NBIN];
   if (threadIdx.x < NBIN) h[threadIdx.x] = 0;
   __syncthreads();
   for (int i = 0; i < BCELLS / BCB; ++i) {
-    const long c = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
-    if (c < n) atomicAdd(&h[cost_bin(stats[c], stats[n + c])], 1);
+    const long g = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
+    if (g < ng) atomicAdd(&h[group_bin(n, stats, g)], 1);
   }
   __syncthreads();
   if (threadIdx.x < NBIN) cnt[(long)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
@@ -387,13 +400,14 @@ __global__ void __launch_bounds__(1024) k_bin_scan(int total, int* __restrict__ 
 }
 __global__ void __launch_bounds__(BCB) k_bin_scatter(long n, const double* __restrict__ stats, int nb,
                                                      const int* __restrict__ off, int* __restrict__ perm) {
+  const long ng = (n + GRP - 1) / GRP;
   __shared__ int wc[BCB / 64][NBIN];
   __shared__ int base[NBIN];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x < NBIN) base[threadIdx.x] = off[(long)threadIdx.x * nb + blockIdx.x];
   for (int i = 0; i < BCELLS / BCB; ++i) {
-    const long c = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
-    const int k = c < n ? cost_bin(stats[c], stats[n + c]) : -1;
+    const long g = (long)blockIdx.x * BCELLS + i * BCB + threadIdx.x;
+    const int k = g < ng ? group_bin(n, stats, g) : -1;
     int rank = 0;
     for (int b = 0; b < NBIN; ++b) {
       const unsigned long long m = __ballot(k == b);
@@ -404,7 +418,7 @@ __global__ void __launch_bounds__(BCB) k_bin_scatter(long n, const double* __res
     if (k >= 0) {
       int pos = base[k] + rank;
       for (int v = 0; v < w; ++v) pos += wc[v][k];
-      perm[pos] = (int)c;
+      perm[pos] = (int)g;
     }
     __syncthreads();
     if (threadIdx.x < NBIN) {
@@ -450,8 +464,8 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
   L.ikc = lds + 2L * m.R * LANES;
   L.A = lds + 3L * m.R * LANES;
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
-  if (t >= n) return;   // no block-level synchronisation below: early exit is safe
-  const long c = perm ? perm[t] : t;
+  const long c = bin_cell(perm, t);
+  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n) || c >= n) return;   // no block-level synchronisation below
   const double T = Tf[c], rho_rr = rhof[c];
   double Y0[S], y[S];
 #pragma unroll
@@ -573,8 +587,8 @@ __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __rest
   __shared__ double kl[G::NK * LANES];
   KLds kh{kl, (int)threadIdx.x};
   const long t = (long)blockIdx.x * LANES + threadIdx.x;
-  if (t >= n) return;
-  const long c = perm ? perm[t] : t;
+  const long c = bin_cell(perm, t);
+  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n) || c >= n) return;
   const double T = Tf[c];
   double y[S];
   double rho;
@@ -701,7 +715,9 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   if (h.fail.n == 0) h.fail.alloc(1);
   DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
   h.method = (int)x.opt("chem.method");
-  const dim3 g((unsigned)blocks_for(x.C, LANES));
+  h.bin = x.on("chem.binning");
+  const long ng = (x.C + GRP - 1) / GRP;   // binning groups
+  const dim3 g((unsigned)blocks_for(h.bin ? ng * GRP : (long)x.C, LANES));
   // compiled-in mechanism? (bitwise the same arrays, NASA7 and weights)
   unsigned long long fp = 0xcbf29ce484222325ull;
   const int S32 = x.S;
@@ -716,12 +732,11 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
     if (fp == ChemGen_burke9::FINGERPRINT) h.generated = 1;
     else if (fp == ChemGen_es80::FINGERPRINT) h.generated = 2;
   }
-  h.bin = x.on("chem.binning");
   const int* perm = nullptr;
   if (h.bin) {
     KScope _ks(x, "k_bin");
-    const int nb = blocks_for(x.C, BCELLS);
-    if (h.perm.n < (size_t)x.C) h.perm.alloc(x.C);
+    const int nb = blocks_for(ng, BCELLS);
+    if (h.perm.n < (size_t)ng) h.perm.alloc(ng);
     if (h.bcnt.n < (size_t)nb * NBIN) h.bcnt.alloc((size_t)nb * NBIN);
     hipLaunchKernelGGL(k_bin_count, dim3(nb), dim3(BCB), 0, x.stream, (long)x.C, (const double*)stats, nb, h.bcnt.p);
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, x.stream, nb * NBIN, h.bcnt.p);

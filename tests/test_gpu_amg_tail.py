@@ -11,12 +11,13 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _run(tail, dims):
+def _run(tail, dims, opts=None):
     from dfmi.lib import Context, DEFAULT_OPTIONS
     from dfmi.mesh import hex_box
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
     DEFAULT_OPTIONS["amg.tail"] = tail
+    DEFAULT_OPTIONS.update(opts or {})
     try:
         ym = read_yaml_mechanism(os.path.join(GOLDEN, "ES80_H2-7-16.yaml"))
         t = read_thermo_table(os.path.join(GOLDEN, "thermo_ES80_H2-7-16.txt"), ym["species"])
@@ -39,6 +40,8 @@ def _run(tail, dims):
         return out
     finally:
         DEFAULT_OPTIONS.pop("amg.tail", None)
+        for k in (opts or {}):
+            DEFAULT_OPTIONS.pop(k, None)
 
 
 # > 4096 cells (the batched solver, not the one-workgroup small solve); the second mesh puts a full 4096-cell
@@ -50,3 +53,4 @@ def test_vcycle_tail_is_bitwise_the_launch_chain(dims):
     assert a["launches"] > 0 and b["launches"] == 0, (a["launches"], b["launches"])
     for k in ("p", "T", "rho", "U"):
         assert np.array_equal(a[k], b[k]), k
+
