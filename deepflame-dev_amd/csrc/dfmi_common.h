@@ -144,7 +144,33 @@ struct ColView {
     }
     return col[k * C + c];
   }
+  // all W columns of the row before any gather: the class offsets (LDS) and the explicit columns a row
+  // needs are read first, so the row's W gathers issue together instead of each waiting at the join of
+  // the class / explicit branch for every load before it (get() per entry serialises the gathers).
+  // Measured on the even-odd kernels: 40.4 -> 40.2 us per launch -- with 8 waves per SIMD in flight they
+  // were bandwidth- rather than latency-bound already; the same change to face_row made k_cg_spmv slower
+  // (44.7 -> 49.7 us: more VGPRs, loads for the absent neighbours) and was not kept.
+  template <int W> __device__ __forceinline__ void get_all(const int* sh, int rb, long C, int c,
+                                                           int (&j)[W]) const {
+    int o[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) o[k] = rb >= 0 ? sh[rb + k] : CEXPL;
+#pragma unroll
+    for (int k = 0; k < W; ++k) j[k] = o[k] != CEXPL ? c + o[k] : col[k * C + c];
+  }
 };
+// f(k, j) over row c's entries: columns first (get_all) when the width is a compile-time WT > 0
+template <int WT, class F>
+__device__ __forceinline__ void for_cols(const ColView& col, const int* sh, int rb, long C, int W, int c, F&& f) {
+  if constexpr (WT > 0) {
+    int j[WT];
+    col.get_all<WT>(sh, rb, C, c, j);
+#pragma unroll
+    for (int k = 0; k < WT; ++k) f(k, j[k]);
+  } else {
+    for (int k = 0; k < W; ++k) f(k, col.get(sh, rb, C, k, c));
+  }
+}
 
 // The symmetric pressure operator read face-wise on a hex box in blockMesh order (FaceOp::on; the cell's
 // rows are the ELL's, checked at build_ell): faces from the computed (i, j, k) walk with their coefficient at

@@ -371,8 +371,7 @@ __global__ void __launch_bounds__(TPB) k_eo_init_e(long C, long Ce, int ne, int 
     const long ii = s * Ce + i;
     const int rb = col.row(i);
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) o += vs[k * C + i] * xw[col.get(s_ct, rb, C, k, i)];
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * xw[j]; });
     const double d = b.dS[ii], rh = b.rhs[ii];
     b.p[ii] = (rh - o) / d;
     const double res = rh - d * xw[i] - o;
@@ -399,13 +398,11 @@ __global__ void __launch_bounds__(TPB) k_eo_init_o(long C, long Ce, int ne, int 
     const long ii = s * Ce + i;
     const int rb = col.row(i);
     double o1 = 0.0, o2 = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col.get(s_ct, rb, C, k, i);
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) {
       const double a = vs[k * C + i];
       o1 += a * xw[j];
       o2 += a * ps[j];
-    }
+    });
     const double d = b.dS[ii], rh = b.rhs[ii], xo = xw[i];
     const double res = rh - d * xo - o1;
     const double r = (rh - o2) / d - xo;
@@ -457,8 +454,7 @@ __global__ void __launch_bounds__(TPB) k_eo_a(long C, long Ce, int ne, int W_, C
   for_half(ne, [&](int i) {
     const int rb = col.row(i);
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) o += vs[k * C + i] * ps[col.get(s_ct, rb, C, k, i)];
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * ps[j]; });
     ps[i] = o / b.dS[s * Ce + i];
   });
 }
@@ -479,12 +475,12 @@ __global__ void __launch_bounds__(TPB) k_eo_b(long C, long Ce, int ne, int no, i
     const int i = ne + m;
     const long ii = s * Ce + i;
     const int rb = col.row(i);
+    const double r0 = b.r0[ii];   // before the store: b.v may alias it as far as the compiler knows
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) o += vs[k * C + i] * ps[col.get(s_ct, rb, C, k, i)];
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * ps[j]; });
     const double y = ps[i] - o / b.dS[ii];
     b.v[ii] = y;
-    acc[0] += b.r0[ii] * y;
+    acc[0] += r0 * y;
   });
   block_partials<1>(acc, partial, s);
 }
@@ -510,11 +506,7 @@ __global__ void __launch_bounds__(TPB) k_eo_c(long C, long Ce, int ne, int W_, C
   for_half(ne, [&](int i) {
     const int rb = col.row(i);
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int j = col.get(s_ct, rb, C, k, i);
-      o += vs[k * C + i] * (rs[j] - alpha * ws[j]);
-    }
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * (rs[j] - alpha * ws[j]); });
     ts[i] = o / b.dS[s * Ce + i];
   });
 }
@@ -537,13 +529,12 @@ __global__ void __launch_bounds__(TPB) k_eo_d(long C, long Ce, int ne, int no, i
     const int i = ne + m;
     const long ii = s * Ce + i;
     const int rb = col.row(i);
+    const double r0 = b.r0[ii];
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) o += vs[k * C + i] * ts[col.get(s_ct, rb, C, k, i)];
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * ts[j]; });
     const double sc = b.r[ii] - alpha * b.v[ii];
     const double y = sc - o / b.dS[ii];
     ts[i] = y;
-    const double r0 = b.r0[ii];
     acc[0] += y * sc;
     acc[1] += y * y;
     acc[2] += r0 * y;
@@ -597,8 +588,7 @@ __global__ void __launch_bounds__(TPB) k_eo_final(long C, long Ce, int ne, int n
   for_half(ne, [&](int i) {
     const int rb = col.row(i);
     double o = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) o += vs[k * C + i] * xw[col.get(s_ct, rb, C, k, i)];
+    for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * xw[j]; });
     xv[eocell[i]] = (b.rhs[s * Ce + i] - o) / b.dS[s * Ce + i];
   });
   for_half(no, [&](int m) { xv[eocell[ne + m]] = xw[ne + m]; });
