@@ -514,15 +514,19 @@ def chem_step_stats(ctx, C):
     pad = (-C) % 64
     nat = np.concatenate([cost, np.zeros(pad)]).reshape(-1, 64).max(axis=1).mean()
     srt = np.concatenate([np.sort(cost)[::-1], np.zeros(pad)]).reshape(-1, 64).max(axis=1).mean()
-    # the launch bins groups of 8 consecutive cells by their most expensive cell (chem.hip GRP)
+    # binning unit = groups of 8 consecutive cells by their most expensive cell (chem.hip GRP = 8, measured slower)
     g = np.concatenate([cost, np.zeros((-C) % 8)]).reshape(-1, 8)
     gs = g[np.argsort(-g.max(axis=1), kind="stable")]
     gs = np.concatenate([gs, np.zeros(((-len(gs)) % 8, 8))]).reshape(-1, 64)
     grp = gs.max(axis=1).mean()
+    # chem.binning = 2: cells sorted inside each tile of 4096
+    t = np.concatenate([cost, np.zeros((-C) % 4096)]).reshape(-1, 4096)
+    tile = (-np.sort(-t, axis=1)).reshape(-1, 64).max(axis=1).mean()
     return {"steps_mean": float(st[0].mean()), "rejects_mean": float(st[1].mean()), "steps_max": float(cost.max()),
             "wave_eff_natural": float(cost.mean() / nat) if nat else None,
             "wave_eff_sorted": float(cost.mean() / srt) if srt else None,
-            "wave_eff_groups_of_8": float(cost.mean() / grp) if grp else None}
+            "wave_eff_groups_of_8": float(cost.mean() / grp) if grp else None,
+            "wave_eff_tiles_4096": float(cost.mean() / tile) if tile else None}
 
 
 def decomposition(world: int):

@@ -354,7 +354,9 @@ __device__ bool ros3(const ChemMech& m, const Lane<S>& L, double T, const double
 // efficiency 1.0): 1.05 ms; groups of 8 (whole 64-B lines per wave: 0.6 GB, 1.44x) lose that (efficiency 0.61):
 // 1.25 ms -- the kernel is bound by its FP64 issue, not by these bytes. Counting sort over NBIN buckets, stable
 // inside a bucket (ascending group index). Every cell's integration is independent of its position, so the
-// order changes timing only, never results.
+// order changes timing only, never results. Default: the sort inside 4096-cell tiles (chem.binning = 2, below):
+// traffic 2.06 -> 0.72 GB per solve at wave efficiency 0.977, k_chem 1.029 -> 1.046 ms and the binning
+// passes 0.074 -> 0.056 ms (no global scan): the same 1.10 ms per step (profiles/r05_pmc_traffic*.json).
 constexpr int NBIN = 32, BCB = 256, BCELLS = 4096, GRP = 1;   // 4096 groups per binning block, 16 passes of 256
 __device__ inline int cost_bin(double st, double rj) {
   const int c = (int)(st + rj);
@@ -368,6 +370,17 @@ __device__ inline int group_bin(long n, const double* __restrict__ stats, long g
 }
 // the cell lane t integrates: group perm[t / GRP], its (t % GRP)-th cell (>= n: no cell)
 __device__ inline long bin_cell(const int* perm, long t) { return perm ? (long)perm[t / GRP] * GRP + t % GRP : t; }
+// chem.binning = 2 (tile-local): the counting sort runs inside each tile of BCELLS groups (one binning block) rather
+// than over the whole mesh, so a wave's cells come from one tile; the 64-wave tile runs on one XCD (one L2) and every
+// line of the state it reads is fetched once for the tile instead of once per cost bucket. XCD x's k-th workgroup
+// (hardware order: workgroup p on XCD p % 8) takes block k % TILE_B of tile (k / TILE_B) * 8 + x -- consecutive tiles
+// on different XCDs, so a costly region of the mesh spreads over all eight. The grid is padded to 8 tiles.
+constexpr int TILE_B = BCELLS * GRP / LANES;
+__device__ inline long chem_thread(int tiled) {
+  long b = blockIdx.x;
+  if (tiled) { const long x = b % 8, k = b / 8; b = ((k / TILE_B) * 8 + x) * TILE_B + k % TILE_B; }
+  return b * LANES + threadIdx.x;
+}
 // per-block bucket counts, bucket-major [NBIN][nb]
 __global__ void __launch_bounds__(BCB) k_bin_count(long n, const double* __restrict__ stats, int nb, int* __restrict__ cnt) {
   const long ng = (n + GRP - 1) / GRP;
@@ -397,6 +410,13 @@ __global__ void __launch_bounds__(1024) k_bin_scan(int total, int* __restrict__ 
   }
   a = part[threadIdx.x] - a;
   for (int i = b0; i < b1; ++i) { const int v = cnt[i]; cnt[i] = a; a += v; }
+}
+// chem.binning = 2: exclusive offsets inside each binning block's own range of perm (bucket order, block by block)
+__global__ void __launch_bounds__(BCB) k_bin_scan_local(int nb, int* __restrict__ cnt) {
+  const int blk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= nb) return;
+  int a = blk * BCELLS;
+  for (int b = 0; b < NBIN; ++b) { const int v = cnt[(long)b * nb + blk]; cnt[(long)b * nb + blk] = a; a += v; }
 }
 __global__ void __launch_bounds__(BCB) k_bin_scatter(long n, const double* __restrict__ stats, int nb,
                                                      const int* __restrict__ off, int* __restrict__ perm) {
@@ -455,7 +475,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
                                                 const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                 double dt, double rtol, double atol, double Tmin, int max_steps,
                                                 int method, double* __restrict__ RR, double* __restrict__ stats,
-                                                int* __restrict__ fail) {
+                                                int* __restrict__ fail, int tiled) {
   extern __shared__ double lds[];
   Lane<S> L;
   L.lane = threadIdx.x;
@@ -463,9 +483,10 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
   L.k0 = lds + (long)m.R * LANES;
   L.ikc = lds + 2L * m.R * LANES;
   L.A = lds + 3L * m.R * LANES;
-  const long t = (long)blockIdx.x * LANES + threadIdx.x;
+  const long t = chem_thread(tiled);
+  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n)) return;   // no block-level synchronisation below
   const long c = bin_cell(perm, t);
-  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n) || c >= n) return;   // no block-level synchronisation below
+  if (c >= n) return;
   const double T = Tf[c], rho_rr = rhof[c];
   double Y0[S], y[S];
 #pragma unroll
@@ -577,7 +598,7 @@ template <class G>
 __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __restrict__ perm,
     const double* __restrict__ Tf, const double* __restrict__ pf, const double* __restrict__ rhof,
     const double* __restrict__ Yf, double dt, double rtol, double atol, double Tmin, int max_steps,
-    double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail) {
+    double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail, int tiled) {
   constexpr int S = G::S, SA = G::SA;
   constexpr double g = 0.43586652150845899941601945119356;
   constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
@@ -586,9 +607,10 @@ __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __rest
   constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
   __shared__ double kl[G::NK * LANES];
   KLds kh{kl, (int)threadIdx.x};
-  const long t = (long)blockIdx.x * LANES + threadIdx.x;
+  const long t = chem_thread(tiled);
+  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n)) return;   // no block-level synchronisation below
   const long c = bin_cell(perm, t);
-  if (t >= (perm ? (n + GRP - 1) / GRP * GRP : n) || c >= n) return;
+  if (c >= n) return;
   const double T = Tf[c];
   double y[S];
   double rho;
@@ -715,9 +737,12 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   if (h.fail.n == 0) h.fail.alloc(1);
   DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
   h.method = (int)x.opt("chem.method");
-  h.bin = x.on("chem.binning");
+  h.bin = (int)x.opt("chem.binning");
   const long ng = (x.C + GRP - 1) / GRP;   // binning groups
-  const dim3 g((unsigned)blocks_for(h.bin ? ng * GRP : (long)x.C, LANES));
+  const int tiled = h.bin == 2;
+  long nblk = blocks_for(h.bin ? ng * GRP : (long)x.C, LANES);
+  if (tiled) nblk = (nblk + 8L * TILE_B - 1) / (8L * TILE_B) * (8L * TILE_B);   // whole groups of 8 tiles
+  const dim3 g((unsigned)nblk);
   // compiled-in mechanism? (bitwise the same arrays, NASA7 and weights)
   unsigned long long fp = 0xcbf29ce484222325ull;
   const int S32 = x.S;
@@ -739,7 +764,8 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
     if (h.perm.n < (size_t)ng) h.perm.alloc(ng);
     if (h.bcnt.n < (size_t)nb * NBIN) h.bcnt.alloc((size_t)nb * NBIN);
     hipLaunchKernelGGL(k_bin_count, dim3(nb), dim3(BCB), 0, x.stream, (long)x.C, (const double*)stats, nb, h.bcnt.p);
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, x.stream, nb * NBIN, h.bcnt.p);
+    if (tiled) hipLaunchKernelGGL(k_bin_scan_local, dim3(blocks_for(nb, BCB)), dim3(BCB), 0, x.stream, nb, h.bcnt.p);
+    else hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, x.stream, nb * NBIN, h.bcnt.p);
     hipLaunchKernelGGL(k_bin_scatter, dim3(nb), dim3(BCB), 0, x.stream, (long)x.C, (const double*)stats, nb,
                        (const int*)h.bcnt.p, h.perm.p);
     perm = h.perm.p;
@@ -747,7 +773,7 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   if (h.generated) {
     KScope _ks(x, "k_chem");
 #define GEN(G) hipLaunchKernelGGL((k_chem_gen<G>), g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"), x.f("p"),  \
-                                  rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats, h.fail.p)
+                                  rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats, h.fail.p, tiled)
     if (h.generated == 1) GEN(ChemGen_burke9); else GEN(ChemGen_es80);
 #undef GEN
     DFMI_HIP(hipGetLastError());
@@ -758,7 +784,7 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \
     hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, perm, m, x.f("T"), x.f("p"), rho_rr,      \
-                       x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats, h.fail.p);     \
+                       x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats, h.fail.p, tiled); \
   } while (0)
   switch (x.S) {
     case 4: CALL(4); break; case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break;

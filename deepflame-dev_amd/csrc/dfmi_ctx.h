@@ -147,7 +147,7 @@ struct Chem {
   int max_steps = 100000;
   int method = 0;               // 0 ROS3 Rosenbrock, 1 linearly-implicit Euler extrapolation
   int generated = 0;            // last solve used a compiled-in mechanism (chem_gen_*.inc): 1 burke9, 2 es80
-  bool bin = true;              // order cells by the previous solve's step count (option chem.binning = 0: natural order)
+  int bin = 2;                  // order cells by the previous solve's step count (option chem.binning: 0 natural order, 1 whole mesh, 2 per tile)
   DevBuf<int> perm, bcnt;       // cost-binned cell order; per-block bucket counts / offsets
   std::vector<int> h_idata, h_irs;
   std::vector<double> h_dd;
@@ -251,7 +251,7 @@ inline const OptDef* option_defs(int& n) {
     {"fv.yprep_brick", 1},            // k_y_prep staging 16x4x4 bricks in LDS (hex walk)
     {"chem.method", 0},               // 0: ROS3 Rosenbrock, 1: linearly-implicit Euler extrapolation
     {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
-    {"chem.binning", 1},              // cells launched in cost-binned order
+    {"chem.binning", 2},              // cells launched in cost-binned order: 1 over the mesh, 2 inside 4096-cell tiles
     {"dnn.tuned_gemm", 1},            // DF-ODENet layers by the shape-tuned kernels (0: k_mlp_gemm for every layer)
   };
   n = (int)(sizeof(d) / sizeof(d[0]));
