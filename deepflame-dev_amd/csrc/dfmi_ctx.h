@@ -109,6 +109,10 @@ struct Thermo {
   // species-minor copies for the cooperative S > 16 kernel (lanes own consecutive species i, so a
   // coefficient load over a group is one contiguous run): nasa [15][S], bdiff [j][5][i], vc [j][i]
   DevBuf<double> dnasaT, dbdiffT, dvc1T, dvc2T;
+  // the same kernel's packed forms: vc1 / vc2 interleaved [j][i][2] (one 16-B load per pair), and, for a symmetric
+  // binary-diffusion table, its unique pairs in rotation order [d - 1][i][6] = coefficients of the pair
+  // (i, (i + d) mod S), d = 1 .. S / 2, padded to 6 (three 16-B loads)
+  DevBuf<double> dvcP, dbdR;
 };
 
 struct Halo;   // RCCL processor-patch exchange (halo.hip)

@@ -23,6 +23,7 @@ struct TC {   // coefficient table pointers
   const double *W, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;
   int sym;      // bdiff[i][j] == bdiff[j][i] bitwise (binary diffusion fits are symmetric)
   const double *nasaT, *bdiffT, *vc1T, *vc2T;   // species-minor copies (Thermo::dnasaT ...), coop kernel
+  const double *vcP, *bdR;                      // packed copies (Thermo::dvcP, dbdR; bdR only when sym)
 };
 
 // NASA7 polynomials of species i at T: cp/R and h/(R T); coefficient k at a[k * st] (st = 1: the
@@ -481,8 +482,10 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       double s2[NCB];
 #pragma unroll
       for (int c = 0; c < NCB; ++c) s2[c] = 0.0;
+#pragma unroll 4
       for (int j = 0; j < S; ++j) {
-        const double v2 = t.vc2T[j * S + i], v1 = t.vc1T[j * S + i];
+        const double2 vp = reinterpret_cast<const double2*>(t.vcP)[j * S + i];   // {vc1, vc2}: one 16-B load
+        const double v1 = vp.x, v2 = vp.y;
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
           const double tmp = 1.0 + (sv[c][q] * sR[grp * NCB + c][j]) * v2;
@@ -537,6 +540,50 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
   double rpT[NCB], rdv[NCB][SPL];
 #pragma unroll
   for (int c = 0; c < NCB; ++c) rpT[c] = 1.0 / (Tc[c] * sT[c]);
+  if (SPL == 1 && t.bdR) {
+    // symmetric fits, one species per lane: each unordered pair is evaluated once. At rotation step d lane i
+    // evaluates 1 / D of the pair (i, i + d mod S) and receives from lane i - d that of (i - d, i): d = 1 .. S / 2
+    // covers every pair of an odd S once; for an even S the pair (i, i + S / 2) of the last step is evaluated by
+    // both its lanes and each keeps its own value. Half the fit evaluations, reciprocals and coefficient loads of
+    // the row loop below; the row sums are accumulated in rotation order (agrees to rounding).
+    const int i = l;
+    double s1[NCB], s2[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) { s1[c] = 0.0; s2[c] = 0.0; }
+    const int D = S / 2;
+    const int gb = threadIdx.x - l;   // the group's lane 0
+#pragma unroll 2
+    for (int d = 1; d <= D; ++d) {
+      const int jp = i + d < S ? i + d : i + d - S, jm = i - d >= 0 ? i - d : i - d + S;
+      const bool own = i < S;
+      const double2* bd = reinterpret_cast<const double2*>(t.bdR + ((long)(d - 1) * S + (own ? i : 0)) * 6);
+      const double2 b01 = bd[0], b23 = bd[1], b4p = bd[2];
+      const double wp = t.W[own ? jp : 0], wm = t.W[own ? jm : 0];
+      const bool both = 2 * d != S;   // the received value is a different pair's
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const double tmp = b01.x * poly[c][0] + b01.y * poly[c][1] + b23.x * poly[c][2] + b23.y * poly[c][3] +
+                           b4p.x * poly[c][4];
+        const double inv = rpT[c] * rcp_nr(tmp);
+        const double inr = __shfl(inv, gb + (own ? jm : 0), 64);
+        if (own) {
+          const double xp = sX[grp * NCB + c][jp], xm = sX[grp * NCB + c][jm];
+          s1[c] += xp * inv;
+          s2[c] += xp * wp * inv;
+          if (both) { s1[c] += xm * inr; s2[c] += xm * wm * inr; }
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      double rd = 0.0;
+      if (i < S && !(X[c][0] + 1e-10 > 1.)) {
+        const double q2 = s2[c] * (X[c][0] / (Wm[c] - X[c][0] * t.W[i]));
+        rd = 1 / (s1[c] + q2) * rdp[c];
+      }
+      rdv[c][0] = rd;
+    }
+  } else
 #pragma unroll
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
@@ -631,6 +678,25 @@ void thermo_upload(Ctx& x) {
   t.dbdiffT.upload(bT, x.stream);
   t.dvc1T.upload(v1, x.stream);
   t.dvc2T.upload(v2, x.stream);
+  std::vector<double> vp(2 * S * S), br;
+  for (int j = 0; j < S; ++j)
+    for (int i = 0; i < S; ++i) { vp[(j * S + i) * 2] = t.vc1[i * S + j]; vp[(j * S + i) * 2 + 1] = t.vc2[i * S + j]; }
+  t.dvcP.upload(vp, x.stream);
+  bool sym = true;
+  for (int i = 0; i < S && sym; ++i)
+    for (int j = 0; j < S && sym; ++j)
+      for (int k = 0; k < 5; ++k)
+        if (t.bdiff[(i * S + j) * 5 + k] != t.bdiff[(j * S + i) * 5 + k]) { sym = false; break; }
+  if (sym && S > 1) {
+    const int D = S / 2;
+    br.assign((size_t)D * S * 6, 0.0);
+    for (int d = 1; d <= D; ++d)
+      for (int i = 0; i < S; ++i)
+        for (int k = 0; k < 5; ++k) br[((size_t)(d - 1) * S + i) * 6 + k] = t.bdiff[(i * S + (i + d) % S) * 5 + k];
+    t.dbdR.upload(br, x.stream);
+  } else {
+    t.dbdR.release();
+  }
   DFMI_HIP(hipStreamSynchronize(x.stream));   // the staging vectors above go out of scope
 }
 
@@ -642,7 +708,8 @@ void thermo_energy_gradient(Ctx& x) {
   bool any = false;
   for (int p = 0; p < x.P; ++p) any = any || pt[p] == GRADIENT_ENERGY;
   if (!any) return;   // the field stays zero
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T};
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
+       th.dvcP, nullptr};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                  \
   hipLaunchKernelGGL(k_energy_gradient<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t, x.st("he"), \
@@ -669,7 +736,8 @@ void thermo_correct(Ctx& x, bool from_T) {
     for (int j = 0; j < th.S && sym; ++j)
       for (int k = 0; k < 5; ++k)
         if (th.bdiff[(i * th.S + j) * 5 + k] != th.bdiff[(j * th.S + i) * 5 + k]) { sym = 0; break; }
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T};
+  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
+       th.dvcP, sym && th.dbdR.n ? th.dbdR.p : nullptr};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                   \
   do {                                                                                                            \
