@@ -410,6 +410,32 @@ __global__ void k_lim_w_face(MeshView m, int b01, double twoByk, const double* _
   }
   wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
 }
+// the same on a hex box in blockMesh order, one thread per cell over its owned (+x, +y, +z) faces (no owner /
+// neighbour index loads, the owner's value read once); bitwise k_lim_w_face
+__global__ void k_lim_w_cell(MeshView m, int b01, double twoByk, const double* __restrict__ phi,
+                             const double* __restrict__ v, const double* __restrict__ g, double* __restrict__ wout) {
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
+  if (c >= m.C) return;
+  const int nx = m.hx, ny = m.hy, nxy = m.hx * m.hy;
+  const int t = c / nx, i = c - t * nx, k = t / ny, j = t - k * ny;
+  const int hxp = i < nx - 1, hyp = j < ny - 1, hzp = k < m.hz - 1;
+  const long C = m.C, Fs = m.F;
+  const double vo = v[c];
+  auto face = [&](long f, int n) {
+    const double ph = phi[f], vn = v[n];
+    double lim = 0.0;
+    if (!(b01 && out01(ph, vo, vn))) {
+      const double dv[3] = {m.md[f], m.md[Fs + f], m.md[2 * Fs + f]};
+      const int cu = ph > 0 ? c : n;
+      const double gu[3] = {g[cu], g[C + cu], g[2 * C + cu]};
+      lim = ll_limiter(twoByk, ph, vo, vn, gu, dv);
+    }
+    wout[f] = lim * m.w[f] + (1 - lim) * pos0(ph);
+  };
+  if (hxp) face(c, c + 1);
+  if (hyp) face(hxp * C + c, c + nx);
+  if (hzp) face((hxp + hyp) * C + c, c + nxy);
+}
 // boundary slots; bg = the neighbour-side gradient on processor slots ([3][B], halo), cyclic: partner cell
 __global__ void k_lim_w_slot(MeshView m, const int8_t* __restrict__ ty, int b01, double twoByk,
                              const double* __restrict__ bphi, const double* __restrict__ v, const double* __restrict__ bv,
@@ -531,6 +557,35 @@ __global__ void k_cubic_face(MeshView m, const double* __restrict__ vf, const do
 #pragma unroll
   for (int q = 0; q < 9; ++q) { gP[q] = g[q * C + o]; gN[q] = g[q * C + n]; }
   cf[f] = cubic_corr(m.w[f], S, m.magSf[f], m.dc[f], vP, vN, gP, gN);
+}
+// the same on a hex box in blockMesh order (MeshView::hx), one thread per cell over its owned (+x, +y, +z) faces:
+// the owner's value and gradient are loaded once for its three faces instead of once per face (face-parallel: 24
+// gathered doubles per face); bitwise k_cubic_face (the same cubic_corr on the same operands)
+__global__ void k_cubic_cell(MeshView m, const double* __restrict__ vf, const double* __restrict__ g,
+                             double* __restrict__ cf) {
+  const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
+  if (c >= m.C) return;
+  const int nx = m.hx, ny = m.hy, nxy = m.hx * m.hy;
+  const int t = c / nx, i = c - t * nx, k = t / ny, j = t - k * ny;
+  const int hxp = i < nx - 1, hyp = j < ny - 1, hzp = k < m.hz - 1;
+  const long C = m.C, Fs = m.F;
+  double vP[3], gP[9];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) vP[q] = vf[q * C + c];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) gP[q] = g[q * C + c];
+  auto face = [&](long f, int n) {
+    const double S[3] = {m.Sf[f], m.Sf[Fs + f], m.Sf[2 * Fs + f]};
+    double vN[3], gN[9];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) vN[q] = vf[q * C + n];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) gN[q] = g[q * C + n];
+    cf[f] = cubic_corr(m.w[f], S, m.magSf[f], m.dc[f], vP, vN, gP, gN);
+  };
+  if (hxp) face(c, c + 1);
+  if (hyp) face(hxp * C + c, c + nx);
+  if (hzp) face((hxp + hyp) * C + c, c + nxy);
 }
 __global__ void k_cubic_slot(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ vf,
                              const double* __restrict__ bvf, const double* __restrict__ g, const double* __restrict__ bg,
@@ -2149,7 +2204,8 @@ static void e_scheme_terms(Ctx& x) {
     const int b01 = lim ? (x.sch.K == SCH_LL01) : 1;
     const double twoByk = 2.0 / std::max(x.sch.k_K, 1e-15);
     if (lim) {
-      LAUNCH(k_lim_w_face, x.Fs, m, b01, twoByk, x.f("phi"), x.f("K"), g, w);
+      if (face_hex(x)) LAUNCH(k_lim_w_cell, x.C, m, b01, twoByk, x.f("phi"), x.f("K"), g, w);
+      else LAUNCH(k_lim_w_face, x.Fs, m, b01, twoByk, x.f("phi"), x.f("K"), g, w);
       LAUNCH(k_lim_w_slot, x.B, m, x.st("K"), b01, twoByk, x.f("boundary_phi"), x.f("K"), x.f("boundary_K"), g, bg, bw);
     } else {
       LAUNCH(k_upwind_w_face, x.Fs, m, x.f("phi"), w);
@@ -2165,7 +2221,8 @@ static void e_scheme_terms(Ctx& x) {
     else if (face_rows(x)) LAUNCH((k_grad_cells<3, 6>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
     else LAUNCH((k_grad_cells<3, 0>), x.C, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g);
     halo_fields(x, {"gradHD"});
-    LAUNCH(k_cubic_face, x.Fs, m, x.f("hDiffCorrFlux"), g, cf);
+    if (face_hex(x)) LAUNCH(k_cubic_cell, x.C, m, x.f("hDiffCorrFlux"), g, cf);
+    else LAUNCH(k_cubic_face, x.Fs, m, x.f("hDiffCorrFlux"), g, cf);
     LAUNCH(k_cubic_slot, x.B, m, x.st("calculated"), x.f("hDiffCorrFlux"), x.f("boundary_hDiffCorrFlux"), g,
            x.f("boundary_gradHD"), bcf);
   }
