@@ -111,7 +111,8 @@ struct Sys {
 // per system: ELL values, dS = diag + sum internalCoeffs, rhs = source + non-coupled boundaryCoeffs
 // (fvMatrix::addBoundaryDiag / addBoundarySource(source, false)), slot order as the sequential code
 // vshared: the systems share one operator (U's components: one LDU, and the coupled-slot coefficients of
-// translational cyclic / processor patches do not depend on the component), so only system 0 writes val
+// translational cyclic / processor patches do not depend on the component), so only system 0 writes val;
+// 2: no values at all (a PCG that reads the operator face-wise and reuses the V-cycle built earlier)
 __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, const int* __restrict__ sys_map, int W,
                             const int* __restrict__ esrc, long Ce, double* __restrict__ val, double* __restrict__ dS,
                             double* __restrict__ rhs, int vshared = 0, const int* __restrict__ eopos = nullptr) {
@@ -123,7 +124,7 @@ __global__ void k_ell_build(MeshView m, const int8_t* __restrict__ ty, Sys q, co
   const double* ic = q.ic + ms * q.bstride;
   const double* bc = q.bc + ms * q.bstride;
   double* vs = val + (long)s * W * C;
-  const bool wv = !(vshared && s > 0);
+  const bool wv = vshared == 0 || (vshared == 1 && s == 0);
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < m.C; c += gridDim.x * blockDim.x) {
     const int pc = eopos ? eopos[c] : c;   // the row of c (even-odd layout) or c
     const int cl = ecls_of(m, c);
@@ -1775,11 +1776,17 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   dim3 g(nblk), bl(TPB);
   Launch L{x, nblk, 1};
   const bool amg = cfg.precond == 1;
-  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, 0); }
-  { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
-  DFMI_HIP(hipGetLastError());
   // the symmetric p operator read face-wise on a hex box (FaceOp, one rank; pcg.face_form = 0: the ELL values)
   const bool face = x.hex[0] > 0 && x.fslot && x.nranks == 1 && !halo_active(x) && !small_solve(x) && x.on("pcg.face_form");
+  // a later corrector of the same step (amg.reuse): the V-cycle keeps the operators the first corrector built --
+  // a fixed SPD preconditioner of a matrix that changed by the density update only, so PCG still converges to
+  // this system's own tolerance; the fp32 rounding and Galerkin sums of one solve are saved
+  const bool reuse = amg && x.amg.ready && x.amg.reuse_ok && x.on("amg.reuse") && x.nranks == 1;
+  // face-wise PCG with the reused V-cycle: nothing reads the ELL values, so they are not written
+  const int novals = face && reuse ? 2 : 0;
+  { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, novals); }
+  { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
+  DFMI_HIP(hipGetLastError());
   FaceOp<double> fo{};
   if (face) fo = FaceOp<double>{1, x.hex[0], x.hex[1], x.hex[2], C, upper, bc, x.ell.csStart.p, x.ell.csSlot.p,
                                 x.ell.scol.p};
@@ -1787,10 +1794,7 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     if (!x.amg.ready) amg_setup(x);
     x.amg.face = face && amg_l0_fusable(x) && x.amg.l0_sweeps == 1;
     x.amg.dfo = fo;
-    // a later corrector of the same step (amg.reuse): the V-cycle keeps the operators the first corrector built --
-    // a fixed SPD preconditioner of a matrix that changed by the density update only, so PCG still converges to
-    // this system's own tolerance; the fp32 rounding and Galerkin sums of one solve are saved
-    if (!(x.amg.reuse_ok && x.on("amg.reuse") && x.nranks == 1)) amg_galerkin(x, val, v.dS);
+    if (!reuse) amg_galerkin(x, val, v.dS);
     if (x.amg.halo_l0) {   // the level-0 diagonal across processor faces, once per solve
       halo_vecs(x, {v.dS}, 1, Ce);
       x.amg.dS_full = v.dS;
