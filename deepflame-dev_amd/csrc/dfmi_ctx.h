@@ -105,7 +105,7 @@ struct SolveStats { int iters = 0; double res0 = 0, res = 0; };
 struct Thermo {
   int S = 0;
   std::vector<double> W, nasa, visc, cond, bdiff, vc1, vc2;
-  DevBuf<double> dW, dnasa, dvisc, dcond, dbdiff, dvc1, dvc2;
+  DevBuf<double> dW, drW, dnasa, dvisc, dcond, dbdiff, dvc1, dvc2;   // drW = 1 / W
   // species-minor copies for the cooperative S > 16 kernel (lanes own consecutive species i, so a
   // coefficient load over a group is one contiguous run): nasa [15][S], bdiff [j][5][i], vc [j][i]
   DevBuf<double> dnasaT, dbdiffT, dvc1T, dvc2T;

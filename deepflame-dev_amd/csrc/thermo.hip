@@ -20,30 +20,47 @@ constexpr double R_GAS = 8314.46261815324;
 constexpr double SQRT8 = 2.8284271247461903;
 
 struct TC {   // coefficient table pointers
-  const double *W, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;
+  const double *W, *rW, *nasa, *visc, *cond, *bdiff, *vc1, *vc2;   // rW = 1 / W
   int sym;      // bdiff[i][j] == bdiff[j][i] bitwise (binary diffusion fits are symmetric)
   const double *nasaT, *bdiffT, *vc1T, *vc2T;   // species-minor copies (Thermo::dnasaT ...), coop kernel
   const double *vcP, *bdR;                      // packed copies (Thermo::dvcP, dbdR; bdR only when sym)
 };
 
-// NASA7 polynomials of species i at T: cp/R and h/(R T); coefficient k at a[k * st] (st = 1: the
-// species-major table, st = S: the species-minor copy)
-__device__ __forceinline__ void nasa_cp_h(const double* a, double T, double& cpR, double& hRT, int st = 1) {
-  const int o = ((T > a[0]) ? 1 : 8) * st;
+// 1/x from the hardware reciprocal estimate refined by two Newton steps (correctly rounded in all but rare
+// last-bit cases; x is a positive normal number here): a short dependency chain in place of the IEEE division
+// sequence (~10 instructions)
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// powers of T shared by the S species' NASA7 evaluations at one temperature: the divisions by 3, 5 and T once
+// per temperature instead of once per species (the result agrees with the per-species divisions to rounding)
+struct TPow { double T, T2, T3, T4, H1, H2, H3, H4, RT; };
+__device__ __forceinline__ TPow tpow(double T) {
   const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;
-  const double a0 = a[o], a1 = a[o + st], a2 = a[o + 2 * st], a3 = a[o + 3 * st], a4 = a[o + 4 * st], a5 = a[o + 5 * st];
-  cpR = a0 + a1 * T + a2 * T2 + a3 * T3 + a4 * T4;
-  hRT = a0 + a1 * T / 2 + a2 * T2 / 3 + a3 * T3 / 4 + a4 * T4 / 5 + a5 / T;
+  return TPow{T, T2, T3, T4, T * 0.5, T2 * (1.0 / 3.0), T3 * 0.25, T4 * (1.0 / 5.0), rcp_nr(T)};
+}
+// NASA7 polynomials of species i at T: cp/R and h/(R T)
+__device__ __forceinline__ void nasa_cp_h(const double* a, const TPow& q, double& cpR, double& hRT) {
+  const int o = (q.T > a[0]) ? 1 : 8;
+  const double a0 = a[o], a1 = a[o + 1], a2 = a[o + 2], a3 = a[o + 3], a4 = a[o + 4], a5 = a[o + 5];
+  cpR = a0 + a1 * q.T + a2 * q.T2 + a3 * q.T3 + a4 * q.T4;
+  hRT = a0 + a1 * q.H1 + a2 * q.H2 + a3 * q.H3 + a4 * q.H4 + a5 * q.RT;
 }
 
 // mixture h and cp at T, ryw[i] = R Y_i / W_i
 template <int S>
 __device__ __forceinline__ void hcp_mix(const TC& t, double T, const double* ryw, double& h, double& cp) {
+  const TPow q = tpow(T);
   h = 0.; cp = 0.;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     double c, hh;
-    nasa_cp_h(t.nasa + i * 15, T, c, hh);
+    nasa_cp_h(t.nasa + i * 15, q, c, hh);
     h += hh * T * ryw[i];
     cp += c * ryw[i];
   }
@@ -51,8 +68,10 @@ __device__ __forceinline__ void hcp_mix(const TC& t, double T, const double* ryw
 
 // state (T or he), p, Y -> T, he, psi, rho, mu, alpha, rhoD[S], hai[S]; mirrors oracle thermo_point
 // (same formulas; divisions hoisted out of the O(S^2) loops -- reciprocals of the species
-// viscosities, one reciprocal per binary-diffusion pair when the fit table is symmetric -- so the
-// result agrees with the sequential evaluation to rounding, not bitwise)
+// viscosities, one reciprocal per binary-diffusion pair when the fit table is symmetric -- and the
+// per-species divisions as products with 1/W, T powers shared per temperature (tpow) and Newton-refined
+// reciprocals (rcp_nr), so the result agrees with the sequential evaluation to rounding, not bitwise;
+// the Newton step and its stopping test keep their divisions, so the iteration count is the oracle's)
 template <int S>
 __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, double& he, double p, const double* y,
                                              double& psi, double& rho, double& mu, double& alpha, double* rhoD,
@@ -63,11 +82,11 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   double X[S], rw[S], ryw[S];
   double sum = 0.;
 #pragma unroll
-  for (int i = 0; i < S; ++i) { rw[i] = R_GAS / t.W[i]; ryw[i] = rw[i] * y[i]; sum += y[i] / t.W[i]; }
+  for (int i = 0; i < S; ++i) { rw[i] = R_GAS * t.rW[i]; ryw[i] = rw[i] * y[i]; sum += y[i] * t.rW[i]; }
   double Wm = 0.;
   const double rsum = 1.0 / sum;
 #pragma unroll
-  for (int i = 0; i < S; ++i) { X[i] = y[i] / t.W[i] * rsum; Wm += X[i] * t.W[i]; }
+  for (int i = 0; i < S; ++i) { X[i] = y[i] * t.rW[i] * rsum; Wm += X[i] * t.W[i]; }
   double cpm;
   if (fixT) {
     hcp_mix<S>(t, T, ryw, he, cpm);
@@ -97,7 +116,7 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
 #pragma unroll
     for (int j = 0; j < 5; ++j) dp += t.visc[i * 5 + j] * poly[j];
     sv[i] = dp;
-    rsv[i] = 1.0 / dp;
+    rsv[i] = rcp_nr(dp);
     xs[i] = X[i] * (1.0 / SQRT8);
   }
   double mumix = 0.;
@@ -109,7 +128,7 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
       const double tmp = 1.0 + (sv[i] * rsv[j]) * t.vc2[i * S + j];
       s2 += xs[j] * t.vc1[i * S + j] * (tmp * tmp);
     }
-    mumix += X[i] * (sv[i] * sv[i]) / s2;
+    mumix += X[i] * (sv[i] * sv[i]) * rcp_nr(s2);
   }
   const double sT = sqrt(T);
   mu = mumix * sT;
@@ -121,7 +140,7 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
     for (int j = 0; j < 5; ++j) dp += t.cond[i * 5 + j] * poly[j];
     const double lam = dp * sT;
     sc += X[i] * lam;
-    sic += X[i] / lam;
+    sic += X[i] * rcp_nr(lam);
   }
   alpha = 0.5 * (sc + 1.0 / sic) / cpm;
   // mixture-averaged diffusion: s1_i = sum_j X_j / D_ij, s2_i = sum_j X_j W_j / D_ij (j != i, ascending j)
@@ -137,7 +156,7 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
         double tmp = 0.;
 #pragma unroll
         for (int k = 0; k < 5; ++k) tmp += t.bdiff[(i * S + j) * 5 + k] * poly[k];
-        const double inv = 1.0 / (tmp * powT);
+        const double inv = rcp_nr(tmp * powT);
         s1[i] += X[j] * inv; s2[i] += X[j] * t.W[j] * inv;
         s1[j] += X[i] * inv; s2[j] += X[i] * t.W[i] * inv;
       }
@@ -157,13 +176,14 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     if (X[i] + 1e-10 > 1.) { rhoD[i] = 0.; continue; }
-    const double q2 = s2[i] * (X[i] / (Wm - X[i] * t.W[i]));
-    rhoD[i] = 1 / (s1[i] + q2) * rdp;
+    const double q2 = s2[i] * (X[i] * rcp_nr(Wm - X[i] * t.W[i]));
+    rhoD[i] = rcp_nr(s1[i] + q2) * rdp;
   }
+  const TPow qT = tpow(T);
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     double c, hh;
-    nasa_cp_h(t.nasa + i * 15, T, c, hh);
+    nasa_cp_h(t.nasa + i * 15, qT, c, hh);
     hai[i] = hh * T * rw[i];
   }
 }
@@ -272,16 +292,6 @@ __device__ __forceinline__ double gsum(double v) {
   return v;
 }
 
-// 1/x from the hardware reciprocal estimate refined by two Newton steps (correctly rounded in all
-// but rare last-bit cases; x is a positive normal number here): a short dependency chain in place of
-// the IEEE division sequence, which left the pair loops latency-bound
-__device__ __forceinline__ double rcp_nr(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);
-}
 
 // slots == nullptr: cells (index = cell, stride n); otherwise boundary slots with per-slot types
 template <int TG, int NCB>
@@ -658,6 +668,12 @@ __global__ void k_energy_gradient_rt(MeshView m, int S, TC t, const int8_t* __re
 void thermo_upload(Ctx& x) {
   Thermo& t = x.thermo;
   t.dW.upload(t.W, x.stream);
+  {
+    std::vector<double> rw(t.W.size());
+    for (size_t i = 0; i < rw.size(); ++i) rw[i] = 1.0 / t.W[i];
+    t.drW.upload(rw, x.stream);
+    DFMI_HIP(hipStreamSynchronize(x.stream));
+  }
   t.dnasa.upload(t.nasa, x.stream);
   t.dvisc.upload(t.visc, x.stream);
   t.dcond.upload(t.cond, x.stream);
@@ -708,7 +724,7 @@ void thermo_energy_gradient(Ctx& x) {
   bool any = false;
   for (int p = 0; p < x.P; ++p) any = any || pt[p] == GRADIENT_ENERGY;
   if (!any) return;   // the field stays zero
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
+  TC t{th.dW, th.drW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, 0, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
        th.dvcP, nullptr};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                  \
@@ -736,7 +752,7 @@ void thermo_correct(Ctx& x, bool from_T) {
     for (int j = 0; j < th.S && sym; ++j)
       for (int k = 0; k < 5; ++k)
         if (th.bdiff[(i * th.S + j) * 5 + k] != th.bdiff[(j * th.S + i) * 5 + k]) { sym = 0; break; }
-  TC t{th.dW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
+  TC t{th.dW, th.drW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
        th.dvcP, sym && th.dbdR.n ? th.dbdR.p : nullptr};
   MeshView m = x.view();
 #define CALL(NS)                                                                                                   \
