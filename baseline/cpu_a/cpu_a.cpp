@@ -34,6 +34,7 @@
 #define DFMI_HD   // the generated kinetics run on the host here
 #define DFMI_SCHED_FENCE()   // scheduling barrier of the device build only
 #define DFMI_CONTRACT() do {} while (0)   // FMA contraction of the device build only
+#define DFMI_RCP(x) (1.0 / (x))           // the device build's refined hardware reciprocal
 #pragma GCC diagnostic push
 #pragma GCC diagnostic ignored "-Wunused-variable"
 #include "../../deepflame-dev_amd/csrc/chem_gen_burke9.inc"

@@ -573,6 +573,16 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 // between the reactions of the fused rates + Jacobian pass: nothing is scheduled across, so one reaction's
 // temporaries die before the next one's loads are issued (the register peak is J plus one reaction)
 #define DFMI_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// 1 / x for the generated kinetics (fall-off factors, LU pivots): the hardware reciprocal estimate refined by two
+// Newton steps instead of the ~10-instruction IEEE division sequence (x is a nonzero normal number there)
+__device__ __forceinline__ double dfmi_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+#define DFMI_RCP(x) dfmi_rcp(x)
 // products contracted into FMAs inside the generated kinetics (the library builds with -ffp-contract=off for the
 // bitwise FV kernels; the chemistry is checked against SciPy BDF to a tolerance, not bitwise)
 #define DFMI_CONTRACT() _Pragma("clang fp contract(fast)") do {} while (0)
@@ -635,7 +645,7 @@ __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __rest
       asm volatile("" : "+v"(arho));
       if (steps + rejects >= max_steps) { steps = -1; break; }
       if (t + h > dt) h = dt - t;
-      const double hg = h * g, rh = 1.0 / h;
+      const double hg = h * g, rh = dfmi_rcp(h);
       double f0[SA], A[SA * SA];
 #pragma unroll
       for (int e = 0; e < SA * SA; ++e) A[e] = 0.0;
@@ -664,7 +674,7 @@ __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __rest
         for (int a = 0; a < SA; ++a) {
           const int i = G::ACT[a];
           yn[a] = y[i] + k1[a] + m2 * k2[a] + m3 * k3[a];
-          const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) / (arho * G::RW[i] + rtol * fmax(fabs(y[i]), fabs(yn[a])));
+          const double e = (e1 * k1[a] + e2 * k2[a] + e3 * k3[a]) * dfmi_rcp(arho * G::RW[i] + rtol * fmax(fabs(y[i]), fabs(yn[a])));
           err += e * e;   // weighted RMS error norm (KPP / CVODE) over all S species (inactive terms are 0)
         }
         err = sqrt(err / S);
