@@ -644,7 +644,7 @@ __device__ __forceinline__ void dev2T(double sc, const double* v, double* o) {
 }
 
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
                          const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
                          double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
@@ -710,7 +710,7 @@ __global__ void __launch_bounds__(TPB) k_u_grad(MeshView m, const int8_t* __rest
 // UEqn matrix (UEqn.H:3-20): ddt(rho,U) + div(phi,U) - laplacian(mu,U) - div(mu dev2 T(gradU)),
 // plus source_solve = source - grad(p) and rAU (dfUEqn.cu:721-738).
 template <int WT>
-__global__ void __launch_bounds__(TPB) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
     const double* __restrict__ rho, const double* __restrict__ rho_old, const double* __restrict__ U_old,
     const double* __restrict__ bU, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ mu, const double* __restrict__ bmu, const double* __restrict__ p,
@@ -1390,7 +1390,7 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
 // boundaryCoeffs in slot order -- bitwise what k_ell_build makes from the LDU arrays, without writing
 // and re-reading lower/upper/internalCoeffs/boundaryCoeffs.
 template <int S, int WT>
-__global__ void __launch_bounds__(TPB) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
