@@ -194,14 +194,17 @@ void do_U(Ctx& x) {
 }
 // YEqn up to its assembled rows: the chemistry source, the preparation terms and the rows (no host
 // synchronisation inside, so dfmi_time_step can issue it on the side stream beside the UEqn)
-void do_Y_front(Ctx& x) {
+// weights = false: the div(phi,Yi_h) weights are formed elsewhere (do_U_Y_fork) and `rows_after` (if set) is the
+// event the rows wait for on this stream
+void do_Y_front(Ctx& x, bool weights = true, hipEvent_t rows_after = nullptr) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
   YWs _yw(x);
   // chemistry->solve(deltaT) before YEqn (YEqn.H); the thermo density of that call is rho before this
   // step's rhoEqn, i.e. rho_old (dfChemistryModel.C:87,771; the GPU reference passes d_rho_old, dfYEqn.cu:449)
   if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt, "rho_old");
   else if (x.chem.mode == 2) dnn_solve(x, "rho_old");   // chemistrySolver_GPU.Inference (YEqn_GPU.H)
-  y_prep(x);
+  y_prep(x, weights);
+  if (rows_after) DFMI_HIP(hipStreamWaitEvent(x.stream, rows_after, 0));
   // production path: the assembly writes the solver's ELL rows directly (no LDU round trip)
   double *val, *dS, *rhs;
   bicg_layout(x, x.S - 1, &val, &dS, &rhs);
@@ -232,17 +235,24 @@ bool step_overlap(const Ctx& x) {
   static const bool on = [] { const char* e = std::getenv("DFMI_STEP_OVERLAP"); return !(e && std::atoi(e) == 0); }();
   return on && x.nranks == 1 && !halo_active(x) && x.ktimer.targets.empty();
 }
-// the side stream forks from the main one and runs the YEqn front; ev_join marks its end
+// the side stream forks from the main one and runs the YEqn front; ev_join marks its end. The side stream is the
+// longer of the two (chemistry, preparation, rows against the UEqn), so the div(phi,Yi_h) weights (they read phi,
+// Y, he only) run on the main stream ahead of the UEqn and the side stream waits for them just before the rows
+// (the step timeline had the main stream idle for ~1 ms at the join)
 void do_U_Y_fork(Ctx& x) {
   if (!x.stream2) {
     DFMI_HIP(hipStreamCreateWithFlags(&x.stream2, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e})
+    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e, &x.ev_cw})
       DFMI_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
   DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_fork, 0));
+  // the weights' event is recorded below, after the side stream's launches that do not need it are issued
+  // (hipStreamWaitEvent waits for the event's most recent record at call time, so it is recorded first)
+  conv_weights(x);
+  DFMI_HIP(hipEventRecord(x.ev_cw, x.stream));
   OnStream _os(x, x.stream2);
-  do_Y_front(x);
+  do_Y_front(x, false, x.ev_cw);
   DFMI_HIP(hipEventRecord(x.ev_join, x.stream2));
 }
 void do_U_Y(Ctx& x) {

@@ -365,7 +365,7 @@ struct Ctx {
   SolverWs& sws() { return ws_is_y ? ws_y : ws; }
   // side stream of the time step (dfmi_time_step: chemistry + YEqn preparation beside the UEqn) and its events
   hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr, ev_cw = nullptr;
   // final solver state of the last solve of each equation, copied asynchronously at the end of the
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
@@ -476,7 +476,7 @@ void u_post_solve(Ctx& x);
 void u_hbya(Ctx& x);
 void p_assemble(Ctx& x);
 void p_post_solve(Ctx& x);
-void y_prep(Ctx& x);
+void y_prep(Ctx& x, bool weights = true);   // weights = false: the caller formed the div(phi,Yi_h) weights
 void y_assemble(Ctx& x);
 void y_assemble_ell(Ctx& x, int W, long Ce, double* val, double* dS, double* rhs);
 void y_post_solve(Ctx& x);

@@ -2228,8 +2228,8 @@ static void e_scheme_terms(Ctx& x) {
   }
 }
 
-void y_prep(Ctx& x) {
-  conv_weights(x);   // div(phi,Yi_h) weights of this step (before Y changes)
+void y_prep(Ctx& x, bool weights) {
+  if (weights) conv_weights(x);   // div(phi,Yi_h) weights of this step (before Y changes)
   MeshView m = x.view();
   double* gout = x.fields.count("dbg_gradY") ? x.f("dbg_gradY") : nullptr;
 // (k_y_prep: the CSR walk measured faster than the gather rows -- 667 vs 848 us on the 2M box; its

@@ -151,6 +151,7 @@ Ctx::~Ctx() {
   if (ev_join) (void)hipEventDestroy(ev_join);
   if (ev_u) (void)hipEventDestroy(ev_u);
   if (ev_e) (void)hipEventDestroy(ev_e);
+  if (ev_cw) (void)hipEventDestroy(ev_cw);
 }
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }
