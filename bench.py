@@ -111,8 +111,10 @@ ROOF_KERNELS = SOLVER_KERNELS + ASSEMBLY_KERNELS + ("k_thermo_cells",)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    # the chemistry's per-cell step sizes and the solvers' poll cadence settle over the first few steps (the first
+    # chemistry solves issue 2-6x the steady FLOPs, profiles/r05_pmc_flops.json): 5 untimed steps reach the steady state
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", "--cells-per-dir", dest="n", type=int, default=128, help="cells per direction (128 -> 2M cells)")
     ap.add_argument("--mech", default="burke9", choices=sorted(MECHS))
     ap.add_argument("--ncorr", type=int, default=2)
