@@ -337,6 +337,23 @@ __global__ void __launch_bounds__(TPB) k_bcg_xp(long C, long Ce, Red red_t, Sys 
   block_partials<2>(acc, partial, s);
 }
 
+// convergence record of a solve into host-coherent memory (Poller, below), by one wave (lane = threadIdx.x & 63):
+// lane s reads system s (vector loads, vector stores)
+__device__ __forceinline__ void poll_post(const double* __restrict__ scal, int nsys, PollRec* rec, long long seq) {
+  const int lane = threadIdx.x & 63;
+  int act = 0, it = 0;
+  for (int s = lane; s < nsys; s += 64) {
+    act |= scal[s * NSCAL + 6] != 0.0;
+    it = max(it, (int)scal[s * NSCAL + 7]);
+  }
+  for (int o = 32; o > 0; o >>= 1) { act |= __shfl_xor(act, o, 64); it = max(it, __shfl_xor(it, o, 64)); }
+  if (lane == 0) {
+    PollRec* r = rec + (seq & 1);
+    r->stopped = act ? 0 : 1;
+    r->iters = it;
+    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 // ============================================================== even-odd (red-black) reduced BiCGStab
 // On a coupling graph that 2-colours (every entry of a row couples the other colour: hex meshes, walled or
 // periodic with even cyclic extents) the Jacobi-scaled system splits as
@@ -545,9 +562,12 @@ __global__ void __launch_bounds__(TPB) k_eo_d(long C, long Ce, int ne, int no, i
 }
 
 // colour-1 rows, k_bcg_xp's update on the reduced vectors (x_o in xw's colour-1 half)
+// rec != nullptr: wave 0 of block (0, 0) also posts convergence record `seq` (Poller::plan) before anything else --
+// the systems' flags and counts it reads were final after k_eo_a, exactly what a k_poll_post after this kernel reads
 __global__ void __launch_bounds__(TPB) k_eo_xp(long Ce, int ne, int no, Red red_t, double* scal, BV b,
-                                               double* partial) {
+                                               double* partial, PollRec* rec = nullptr, long long seq = 0) {
   const int s = blockIdx.y;
+  if (rec && blockIdx.x == 0 && s == 0 && threadIdx.x < 64) poll_post(scal, gridDim.y, rec, seq);
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
   double tv[4];
@@ -1100,19 +1120,7 @@ bool small_solve(const Ctx& x) {
 // solve (~4.7 us each: 0.3 ms per p-solve, ~1.2 ms per step, profiles/r05_timeline_poll.json), and each
 // snapshot was a device-to-host copy plus an event (~10 us of the stream); the posted record is one small launch.
 __global__ void k_poll_post(const double* __restrict__ scal, int nsys, PollRec* rec, long long seq) {
-  const int lane = threadIdx.x;   // one wave; lane s reads system s (vector loads, vector stores)
-  int act = 0, it = 0;
-  for (int s = lane; s < nsys; s += 64) {
-    act |= scal[s * NSCAL + 6] != 0.0;
-    it = max(it, (int)scal[s * NSCAL + 7]);
-  }
-  for (int o = 32; o > 0; o >>= 1) { act |= __shfl_xor(act, o, 64); it = max(it, __shfl_xor(it, o, 64)); }
-  if (lane == 0) {
-    PollRec* r = rec + (seq & 1);
-    r->stopped = act ? 0 : 1;
-    r->iters = it;
-    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  poll_post(scal, nsys, rec, seq);
 }
 
 struct Poller {
@@ -1142,15 +1150,19 @@ struct Poller {
       }
     }
   }
-  // after iteration `it` (0-based) has been enqueued: post a record when the cadence says so; true when an
-  // earlier record shows every system stopped (its iteration count becomes the next solve's `expect`)
-  bool after(int it) {
+  long long next = 0;      // the record the current iteration posts (0: none)
+  // before iteration `it`'s (0-based) last kernel is enqueued: the sequence number of the record this iteration
+  // posts when the cadence says so, else 0 (a caller may have that kernel post it: k_eo_xp)
+  long long plan(int it) {
     const int n = it + 1;
     const bool snap = expect > 0 ? (n >= expect - 1 || n % 4 == 0) : (n % 2 == 0);
-    if (!snap) return false;
-    const long long seq = ++x.sws().poll_seq;
-    hipLaunchKernelGGL(k_poll_post, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.sws().poll.d, seq);
-    DFMI_HIP(hipGetLastError());
+    next = snap ? ++x.sws().poll_seq : 0;
+    return next;
+  }
+  // after the iteration was enqueued (with its record, if plan() asked for one): true when an earlier record
+  // shows every system stopped (its iteration count becomes the next solve's `expect`)
+  bool check() {
+    if (!next) return false;
     bool done = false;
     if (pending > 0) {
       const PollRec& r = wait(pending);
@@ -1159,8 +1171,16 @@ struct Poller {
         x.solve_expect[key] = r.iters;
       }
     }
-    pending = seq;
+    pending = next;
     return done;
+  }
+  // the same with the record posted by its own one-wave launch
+  bool after(int it) {
+    const long long seq = plan(it);
+    if (!seq) return false;
+    hipLaunchKernelGGL(k_poll_post, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.sws().poll.d, seq);
+    DFMI_HIP(hipGetLastError());
+    return check();
   }
 };
 
@@ -1685,10 +1705,12 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
         hipLaunchKernelGGL(k_eo_d<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pT);
       });
       const Red rT = L.after(pT, 4, 0, hb);
-      { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_eo_xp, gh, bl, 0, x.stream, Ce, ne, no, rT, WS.scal.p, b, pR); }
+      const long long pseq = poll.plan(it);   // the update kernel posts this iteration's record (no extra launch)
+      { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_eo_xp, gh, bl, 0, x.stream, Ce, ne, no, rT, WS.scal.p, b, pR,
+                                                      pseq ? WS.poll.d : (PollRec*)nullptr, pseq); }
       DFMI_HIP(hipGetLastError());
       red = L.after(pR, 2, 0, hb);
-      if (poll.after(it)) break;
+      if (poll.check()) break;
     }
     hx({b.xw});
     dispatch_W(W, [&](auto wt) {
