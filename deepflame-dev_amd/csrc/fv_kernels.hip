@@ -1585,7 +1585,7 @@ __device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, i
 // (2 waves per SIMD: 16k cells per XCD x 53 species x 3 arrays = 20 MB against its 4 MB), so each neighbour
 // value is fetched again by each of the cells that read it; a range of species per launch shrinks that set.
 template <int CH, int WT>
-__global__ void __launch_bounds__(TPB) k_y_prep_gen(MeshView m, int s_lo, int s_hi, int pass,
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) k_y_prep_gen(MeshView m, int s_lo, int s_hi, int pass,
     const int8_t* __restrict__ tyY,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ hai, const double* __restrict__ bhai,
