@@ -346,15 +346,15 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int q = 0; q < SPL; ++q) {
       const int i = q * TG + l;
       y[q] = (i < S) ? (live[c] ? sX[grp * NCB + c][i] : (i == 0 ? 1.0 : 0.0)) : 0.0;
-      if (i < S) sum += y[q] / t.W[i];
+      if (i < S) sum += y[q] * t.rW[i];
     }
     const double rsum = 1.0 / gsum<TG>(sum);
     double wm = 0.0;
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
       const int i = q * TG + l;
-      X[c][q] = i < S ? y[q] / t.W[i] * rsum : 0.0;
-      ryw[c][q] = i < S ? R_GAS / t.W[i] * y[q] : 0.0;
+      X[c][q] = i < S ? y[q] * t.rW[i] * rsum : 0.0;
+      ryw[c][q] = i < S ? R_GAS * t.rW[i] * y[q] : 0.0;
       if (i < S) wm += X[c][q] * t.W[i];
     }
     Wm[c] = gsum<TG>(wm);
@@ -376,7 +376,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       hh[c] = 0.0; cc[c] = 0.0;
       const double T1 = TT[c], T2 = T1 * T1, T3 = T2 * T1, T4 = T3 * T1;
       P1[c] = T1; P2[c] = T2; P3[c] = T3; P4[c] = T4;
-      Q1[c] = T1 * 0.5; Q2[c] = T2 / 3; Q3[c] = T3 * 0.25; Q4[c] = T4 / 5; RT[c] = 1.0 / T1;
+      Q1[c] = T1 * 0.5; Q2[c] = T2 * (1.0 / 3.0); Q3[c] = T3 * 0.25; Q4[c] = T4 * (1.0 / 5.0); RT[c] = rcp_nr(T1);
     }
 #pragma unroll
     for (int q = 0; q < SPL; ++q) {
@@ -453,13 +453,13 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int c = 0; c < NCB; ++c) ha[c][q] = 0.0;
     if (i >= S) continue;
     const double* a = t.nasaT + i;
-    const double tm = a[0], rw = R_GAS / t.W[i];
+    const double tm = a[0], rw = R_GAS * t.rW[i];
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
       const double T1 = Tc[c], T2 = T1 * T1, T3 = T2 * T1, T4 = T3 * T1;
       const int o = (T1 > tm) ? 1 : 8;
-      const double h1 = a[o * S] + a[(o + 1) * S] * (T1 * 0.5) + a[(o + 2) * S] * (T2 / 3) + a[(o + 3) * S] * (T3 * 0.25) +
-                        a[(o + 4) * S] * (T4 / 5) + a[(o + 5) * S] * (1.0 / T1);
+      const double h1 = a[o * S] + a[(o + 1) * S] * (T1 * 0.5) + a[(o + 2) * S] * (T2 * (1.0 / 3.0)) +
+                        a[(o + 3) * S] * (T3 * 0.25) + a[(o + 4) * S] * (T4 * (1.0 / 5.0)) + a[(o + 5) * S] * rcp_nr(T1);
       ha[c][q] = h1 * T1 * rw;
     }
   }
@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
 #pragma unroll
         for (int k = 0; k < 5; ++k) dp += vc[k] * poly[c][k];
         sv[c][q] = dp;
-        if (i < S) { sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8); sR[grp * NCB + c][i] = 1.0 / dp; }
+        if (i < S) { sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8); sR[grp * NCB + c][i] = rcp_nr(dp); }
       }
     }
     __syncthreads();
@@ -503,7 +503,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
         }
       }
 #pragma unroll
-      for (int c = 0; c < NCB; ++c) mpart[c] += X[c][q] * (sv[c][q] * sv[c][q]) / s2[c];
+      for (int c = 0; c < NCB; ++c) mpart[c] += X[c][q] * (sv[c][q] * sv[c][q]) * rcp_nr(s2[c]);
     }
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
         for (int k = 0; k < 5; ++k) dp += kc[k] * poly[c][k];
         const double lam = dp * sT[c];
         sc[c] += X[c][q] * lam;
-        sic[c] += X[c][q] / lam;
+        sic[c] += X[c][q] * rcp_nr(lam);
       }
     }
 #pragma unroll
@@ -588,8 +588,8 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int c = 0; c < NCB; ++c) {
       double rd = 0.0;
       if (i < S && !(X[c][0] + 1e-10 > 1.)) {
-        const double q2 = s2[c] * (X[c][0] / (Wm[c] - X[c][0] * t.W[i]));
-        rd = 1 / (s1[c] + q2) * rdp[c];
+        const double q2 = s2[c] * (X[c][0] * rcp_nr(Wm[c] - X[c][0] * t.W[i]));
+        rd = rcp_nr(s1[c] + q2) * rdp[c];
       }
       rdv[c][0] = rd;
     }
@@ -618,8 +618,8 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int c = 0; c < NCB; ++c) {
       double rd = 0.0;
       if (!(X[c][q] + 1e-10 > 1.)) {
-        const double q2 = s2[c] * (X[c][q] / (Wm[c] - X[c][q] * t.W[i]));
-        rd = 1 / (s1[c] + q2) * rdp[c];
+        const double q2 = s2[c] * (X[c][q] * rcp_nr(Wm[c] - X[c][q] * t.W[i]));
+        rd = rcp_nr(s1[c] + q2) * rdp[c];
       }
       rdv[c][q] = rd;
     }
