@@ -285,13 +285,55 @@ __global__ void k_energy_gradient(MeshView m, TC t, const int8_t* __restrict__ t
 // rounding: the tests hold it to 1e-12).
 constexpr int TCB = 256, SMAX = 64;
 
-template <int TG>
-__device__ __forceinline__ double gsum(double v) {
-#pragma unroll
-  for (int o = 1; o < TG; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
 
+// Sum over the group, every lane ending with the same bits. One wave (TG = 64): lane pairings that are
+// involutions, each step v + v(partner) (IEEE addition commutes, so both lanes of a pair agree): quad swaps,
+// the half-row and row mirrors (DPP), then gfx950's row and half-wave swaps (v_permlane16/32_swap: both
+// outputs hold the even / odd row, the lower / upper half, so the sum is formed in the same order
+// everywhere) -- no LDS round trips (the ds_bpermute butterfly of __shfl_xor).
+template <int TG>
+__device__ __forceinline__ double gsum(double v) {
+  if constexpr (TG == 64) {
+    v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);   // row_half_mirror
+    v += dpp_mov<0x140>(v);   // row_mirror
+    {
+      const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+      const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+      v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+    }
+    {
+      const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+      const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+      v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+    }
+    return v;
+  } else {
+#pragma unroll
+    for (int o = 1; o < TG; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+}
+
+
+// a group's own LDS rows written and read back by its own lanes: a wave-level ordering when the group is one wave
+template <int TG>
+__device__ __forceinline__ void group_sync() {
+  if constexpr (TG == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
 
 // slots == nullptr: cells (index = cell, stride n); otherwise boundary slots with per-slot types
 template <int TG, int NCB>
@@ -310,6 +352,9 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
   __shared__ double sX[CPB][SMAX + 1], sR[CPB][SMAX + 1];
   __shared__ int sLive[CPB];
   const int grp = threadIdx.x / TG, l = threadIdx.x % TG;
+  const int DS = (S / 2) * S;
+  const double2* vcP = reinterpret_cast<const double2*>(t.vcP);
+  const double2* bdp = reinterpret_cast<const double2*>(t.bdR);
   const int blk = ty ? (int)blockIdx.x : xcd_block();
   const long base = (long)blk * CPB;
   for (int e = threadIdx.x; e < CPB * S; e += TCB) {
@@ -480,7 +525,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
         if (i < S) { sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8); sR[grp * NCB + c][i] = rcp_nr(dp); }
       }
     }
-    __syncthreads();
+    group_sync<TG>();
     // Wilke rows
     double mpart[NCB];
 #pragma unroll
@@ -494,7 +539,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       for (int c = 0; c < NCB; ++c) s2[c] = 0.0;
 #pragma unroll 4
       for (int j = 0; j < S; ++j) {
-        const double2 vp = reinterpret_cast<const double2*>(t.vcP)[j * S + i];   // {vc1, vc2}: one 16-B load
+        const double2 vp = vcP[j * S + i];   // {vc1, vc2}: one 16-B load
         const double v1 = vp.x, v2 = vp.y;
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
@@ -538,7 +583,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       if (live[c] && l == 0) alpha[idx[c]] = al;
     }
   }
-  __syncthreads();   // mole fractions (unscaled) for the diffusion rows
+  group_sync<TG>();   // mole fractions (unscaled) for the diffusion rows
 #pragma unroll
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
@@ -546,7 +591,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int c = 0; c < NCB; ++c)
       if (i < S) sX[grp * NCB + c][i] = X[c][q];
   }
-  __syncthreads();
+  group_sync<TG>();
   double rpT[NCB], rdv[NCB][SPL];
 #pragma unroll
   for (int c = 0; c < NCB; ++c) rpT[c] = 1.0 / (Tc[c] * sT[c]);
@@ -566,8 +611,8 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int d = 1; d <= D; ++d) {
       const int jp = i + d < S ? i + d : i + d - S, jm = i - d >= 0 ? i - d : i - d + S;
       const bool own = i < S;
-      const double2* bd = reinterpret_cast<const double2*>(t.bdR + ((long)(d - 1) * S + (own ? i : 0)) * 6);
-      const double2 b01 = bd[0], b23 = bd[1], b4p = bd[2];
+      const int e = (d - 1) * S + (own ? i : 0);
+      const double2 b01 = bdp[e], b23 = bdp[DS + e], b4p = bdp[2 * DS + e];
       const double wp = t.W[own ? jp : 0], wm = t.W[own ? jm : 0];
       const bool both = 2 * d != S;   // the received value is a different pair's
 #pragma unroll
@@ -705,10 +750,13 @@ void thermo_upload(Ctx& x) {
         if (t.bdiff[(i * S + j) * 5 + k] != t.bdiff[(j * S + i) * 5 + k]) { sym = false; break; }
   if (sym && S > 1) {
     const int D = S / 2;
-    br.assign((size_t)D * S * 6, 0.0);
+    // three planes of D * S pairs {b0, b1}, {b2, b3}, {b4, 0}: lane i's pair (i, i + d) at (d - 1) * S + i
+    const size_t DS = (size_t)D * S;
+    br.assign(DS * 6, 0.0);
     for (int d = 1; d <= D; ++d)
       for (int i = 0; i < S; ++i)
-        for (int k = 0; k < 5; ++k) br[((size_t)(d - 1) * S + i) * 6 + k] = t.bdiff[(i * S + (i + d) % S) * 5 + k];
+        for (int k = 0; k < 5; ++k)
+          br[((k / 2) * DS + (size_t)(d - 1) * S + i) * 2 + k % 2] = t.bdiff[(i * S + (i + d) % S) * 5 + k];
     t.dbdR.upload(br, x.stream);
   } else {
     t.dbdR.release();
