@@ -209,9 +209,33 @@ template <class T, class FN> __device__ __forceinline__ void face_row(const Face
 // ---- fixed-order reductions of per-block partials (solvers: linsolve.hip; the PCG stop test the AMG's
 // first V-cycle kernel repeats, amg.hip). Blocks of RED_TPB threads.
 constexpr int RED_TPB = 256, RED_NW = RED_TPB / 64;
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum over the wave, every lane ending with the same bits: lane pairings that are involutions, each step
+// v + v(partner) (IEEE addition commutes, so both lanes of a pair agree): quad swaps, the half-row and row
+// mirrors (DPP), then gfx950's row and half-wave swaps (v_permlane16/32_swap: both outputs hold the even /
+// odd row, the lower / upper half, so the sum is formed in the same order everywhere). No LDS round trips
+// (a __shfl butterfly is six dependent ds_bpermute pairs). Call with every lane of the wave active.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  {
+    const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
+  {
+    const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
+  }
   return v;
 }
 

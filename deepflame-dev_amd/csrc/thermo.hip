@@ -285,35 +285,11 @@ __global__ void k_energy_gradient(MeshView m, TC t, const int8_t* __restrict__ t
 // rounding: the tests hold it to 1e-12).
 constexpr int TCB = 256, SMAX = 64;
 
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// Sum over the group, every lane ending with the same bits. One wave (TG = 64): lane pairings that are
-// involutions, each step v + v(partner) (IEEE addition commutes, so both lanes of a pair agree): quad swaps,
-// the half-row and row mirrors (DPP), then gfx950's row and half-wave swaps (v_permlane16/32_swap: both
-// outputs hold the even / odd row, the lower / upper half, so the sum is formed in the same order
-// everywhere) -- no LDS round trips (the ds_bpermute butterfly of __shfl_xor).
+// Sum over the group, every lane ending with the same bits (one wave: wave_sum, dfmi_common.h)
 template <int TG>
 __device__ __forceinline__ double gsum(double v) {
   if constexpr (TG == 64) {
-    v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
-    v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
-    v += dpp_mov<0x141>(v);   // row_half_mirror
-    v += dpp_mov<0x140>(v);   // row_mirror
-    {
-      const auto l = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
-      const auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
-      v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
-    }
-    {
-      const auto l = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
-      const auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
-      v = __hiloint2double(h[0], l[0]) + __hiloint2double(h[1], l[1]);
-    }
+    v = wave_sum(v);
     return v;
   } else {
 #pragma unroll
