@@ -387,8 +387,17 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     hc[c] = live[c] ? he[idx[c]] : 0.0;
     pc[c] = live[c] ? p[idx[c]] : 101325.0;
   }
-  // mixture h and cp of the cells flagged in `on` at temperatures TT (NASA coefficients loaded once
-  // per species for all NCB cells, both ranges; each cell picks its own)
+  // the lane's NASA coefficients, both ranges, loaded once for the Newton loop, the final h / cp and h_i
+  double nhi[SPL][6], nlo[SPL][6], ntm[SPL];
+#pragma unroll
+  for (int q = 0; q < SPL; ++q) {
+    const int i = q * TG + l;
+    const double* a = t.nasaT + (i < S ? i : 0);
+    ntm[q] = a[0];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { nhi[q][k] = a[(1 + k) * S]; nlo[q][k] = a[(8 + k) * S]; }
+  }
+  // mixture h and cp of the cells flagged in `on` at temperatures TT (each cell picks its range)
   auto hcp = [&](const double (&TT)[NCB], const bool (&on)[NCB], double (&h)[NCB], double (&cp)[NCB]) {
     double hh[NCB], cc[NCB];
     double P1[NCB], P2[NCB], P3[NCB], P4[NCB], Q1[NCB], Q2[NCB], Q3[NCB], Q4[NCB], RT[NCB];
@@ -403,11 +412,9 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     for (int q = 0; q < SPL; ++q) {
       const int i = q * TG + l;
       if (i < S) {
-        const double* a = t.nasaT + i;
-        const double tm = a[0];
-        double hi[6], lo[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) { hi[k] = a[(1 + k) * S]; lo[k] = a[(8 + k) * S]; }
+        const double tm = ntm[q];
+        const double (&hi)[6] = nhi[q];
+        const double (&lo)[6] = nlo[q];
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
           const double T1 = TT[c];
@@ -473,14 +480,16 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
 #pragma unroll
     for (int c = 0; c < NCB; ++c) ha[c][q] = 0.0;
     if (i >= S) continue;
-    const double* a = t.nasaT + i;
-    const double tm = a[0], rw = R_GAS * t.rW[i];
+    const double tm = ntm[q], rw = R_GAS * t.rW[i];
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
       const double T1 = Tc[c], T2 = T1 * T1, T3 = T2 * T1, T4 = T3 * T1;
-      const int o = (T1 > tm) ? 1 : 8;
-      const double h1 = a[o * S] + a[(o + 1) * S] * (T1 * 0.5) + a[(o + 2) * S] * (T2 * (1.0 / 3.0)) +
-                        a[(o + 3) * S] * (T3 * 0.25) + a[(o + 4) * S] * (T4 * (1.0 / 5.0)) + a[(o + 5) * S] * rcp_nr(T1);
+      const bool up = T1 > tm;
+      double a[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) a[k] = up ? nhi[q][k] : nlo[q][k];
+      const double h1 = a[0] + a[1] * (T1 * 0.5) + a[2] * (T2 * (1.0 / 3.0)) +
+                        a[3] * (T3 * 0.25) + a[4] * (T4 * (1.0 / 5.0)) + a[5] * rcp_nr(T1);
       ha[c][q] = h1 * T1 * rw;
     }
   }
