@@ -604,18 +604,19 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       for (int c = 0; c < NCB; ++c) {
         const double tmp = b01.x * poly[c][0] + b01.y * poly[c][1] + b23.x * poly[c][2] + b23.y * poly[c][3] +
                            b4p.x * poly[c][4];
-        const double inv = rpT[c] * rcp_nr(tmp);
+        const double inv = rcp_nr(tmp);   // T^1.5 / D_ij: the common factor 1 / T^1.5 applied to the row sums
         const double inr = __shfl(inv, gb + (own ? jm : 0), 64);
-        if (own) {
-          const double xp = sX[grp * NCB + c][jp], xm = sX[grp * NCB + c][jm];
-          s1[c] += xp * inv;
-          s2[c] += xp * wp * inv;
-          if (both) { s1[c] += xm * inr; s2[c] += xm * wm * inr; }
-        }
+        // lanes past S accumulate in-bounds garbage (their rows and their 1/D are never used): no branch
+        const double xp = sX[grp * NCB + c][jp], xm = sX[grp * NCB + c][jm];
+        s1[c] += xp * inv;
+        s2[c] += xp * wp * inv;
+        if (both) { s1[c] += xm * inr; s2[c] += xm * wm * inr; }
       }
     }
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
+      s1[c] *= rpT[c];
+      s2[c] *= rpT[c];
       double rd = 0.0;
       if (i < S && !(X[c][0] + 1e-10 > 1.)) {
         const double q2 = s2[c] * (X[c][0] * rcp_nr(Wm[c] - X[c][0] * t.W[i]));
