@@ -507,7 +507,8 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
 #pragma unroll
         for (int k = 0; k < 5; ++k) dp += vc[k] * poly[c][k];
         sv[c][q] = dp;
-        if (i < S) { sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8); sR[grp * NCB + c][i] = rcp_nr(dp); }
+        sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8);   // lanes past S: unused entries of the row
+        sR[grp * NCB + c][i] = rcp_nr(dp);
       }
     }
     group_sync<TG>();
@@ -574,7 +575,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     const int i = q * TG + l;
 #pragma unroll
     for (int c = 0; c < NCB; ++c)
-      if (i < S) sX[grp * NCB + c][i] = X[c][q];
+      sX[grp * NCB + c][i] = X[c][q];
   }
   group_sync<TG>();
   double rpT[NCB], rdv[NCB][SPL];
@@ -660,7 +661,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
     const int i = q * TG + l;
 #pragma unroll
     for (int c = 0; c < NCB; ++c)
-      if (i < S) { sX[grp * NCB + c][i] = rdv[c][q]; sR[grp * NCB + c][i] = ha[c][q]; }
+      sX[grp * NCB + c][i] = rdv[c][q], sR[grp * NCB + c][i] = ha[c][q];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < CPB * S; e += TCB) {
