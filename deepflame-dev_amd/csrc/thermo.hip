@@ -326,6 +326,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
   // per-cell rows (+1: groups on distinct banks); a group only touches its own NCB rows except in the
   // block-wide transposes that load Y and store rhoD/hai with cell-contiguous (coalesced) accesses
   __shared__ double sX[CPB][SMAX + 1], sR[CPB][SMAX + 1];
+  __shared__ double2 sP[CPB][SMAX];   // Wilke rows: {x_j / sqrt 8, 1 / sv_j}, one 16-B broadcast read per pair
   __shared__ int sLive[CPB];
   const int grp = threadIdx.x / TG, l = threadIdx.x % TG;
   const int DS = (S / 2) * S;
@@ -507,8 +508,7 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
 #pragma unroll
         for (int k = 0; k < 5; ++k) dp += vc[k] * poly[c][k];
         sv[c][q] = dp;
-        sX[grp * NCB + c][i] = X[c][q] * (1.0 / SQRT8);   // lanes past S: unused entries of the row
-        sR[grp * NCB + c][i] = rcp_nr(dp);
+        sP[grp * NCB + c][i] = make_double2(X[c][q] * (1.0 / SQRT8), rcp_nr(dp));   // lanes past S: unused entries
       }
     }
     group_sync<TG>();
@@ -529,8 +529,9 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
         const double v1 = vp.x, v2 = vp.y;
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
-          const double tmp = 1.0 + (sv[c][q] * sR[grp * NCB + c][j]) * v2;
-          s2[c] += sX[grp * NCB + c][j] * v1 * (tmp * tmp);
+          const double2 xr = sP[grp * NCB + c][j];
+          const double tmp = 1.0 + (sv[c][q] * xr.y) * v2;
+          s2[c] += xr.x * v1 * (tmp * tmp);
         }
       }
 #pragma unroll
