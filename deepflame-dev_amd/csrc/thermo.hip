@@ -575,8 +575,10 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
   for (int q = 0; q < SPL; ++q) {
     const int i = q * TG + l;
 #pragma unroll
-    for (int c = 0; c < NCB; ++c)
+    for (int c = 0; c < NCB; ++c) {
       sX[grp * NCB + c][i] = X[c][q];
+      sP[grp * NCB + c][i] = make_double2(X[c][q], X[c][q] * t.W[i < S ? i : 0]);   // {x_j, x_j W_j}
+    }
   }
   group_sync<TG>();
   double rpT[NCB], rdv[NCB][SPL];
@@ -600,7 +602,6 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
       const bool own = i < S;
       const int e = (d - 1) * S + (own ? i : 0);
       const double2 b01 = bdp[e], b23 = bdp[DS + e], b4p = bdp[2 * DS + e];
-      const double wp = t.W[own ? jp : 0], wm = t.W[own ? jm : 0];
       const bool both = 2 * d != S;   // the received value is a different pair's
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
@@ -609,10 +610,10 @@ __global__ void __launch_bounds__(TCB) k_thermo_coop(int n, int S, TC t, int fix
         const double inv = rcp_nr(tmp);   // T^1.5 / D_ij: the common factor 1 / T^1.5 applied to the row sums
         const double inr = __shfl(inv, gb + (own ? jm : 0), 64);
         // lanes past S accumulate in-bounds garbage (their rows and their 1/D are never used): no branch
-        const double xp = sX[grp * NCB + c][jp], xm = sX[grp * NCB + c][jm];
-        s1[c] += xp * inv;
-        s2[c] += xp * wp * inv;
-        if (both) { s1[c] += xm * inr; s2[c] += xm * wm * inr; }
+        const double2 xp = sP[grp * NCB + c][jp], xm = sP[grp * NCB + c][jm];
+        s1[c] += xp.x * inv;
+        s2[c] += xp.y * inv;
+        if (both) { s1[c] += xm.x * inr; s2[c] += xm.y * inr; }
       }
     }
 #pragma unroll
