@@ -156,6 +156,7 @@ void allocate_fields(Ctx& x) {
   alloc(x, "boundary_Y_ref", B, S);
   alloc(x, "boundary_K_ref", B, 1);
   alloc(x, "chem_stats", C, 3);
+  alloc(x, "Qdot", C, 1);   // heat release -sum_i hc_i RR_i (dfChemistryModel.C:771)
   const long ns = std::max(S, 3);
   auto wk = [&](const std::string& n, long len) { x.work[n].assign(std::max(len, 1L), 0.0); };
   wk("out_lower", (long)S * F); wk("out_upper", (long)S * F); wk("out_diag", (long)S * C);
@@ -564,6 +565,20 @@ unsigned long long fnv(unsigned long long h, const void* p, size_t n) {
   return h;
 }
 
+// hc_i = Hf298_i / W_i (dfChemistryModel.C:335-338), the expression of thermo.hip heat_of_formation_per_mass
+std::vector<double> hf298_per_mass(const Ctx& x) {
+  std::vector<double> hc(x.S);
+  const double T = 298.15, T2 = T * T, T3 = T2 * T, T4 = T3 * T, rT = 1.0 / T;
+  for (int i = 0; i < x.S; ++i) {
+    const double* row = x.nasa.data() + 15 * i;
+    const double* a = T <= row[0] ? row + 8 : row + 1;
+    const double ct0 = a[0], ct1 = a[1] * T, ct2 = a[2] * T2, ct3 = a[3] * T3, ct4 = a[4] * T4;
+    const double h_RT = ct0 + 0.5 * ct1 + (1.0 / 3.0) * ct2 + 0.25 * ct3 + 0.2 * ct4 + a[5] * rT;
+    hc[i] = h_RT * RU * T / x.W[i];
+  }
+  return hc;
+}
+
 template <class G>
 int chem_cells(Ctx& x, double dt, const double* rho_rr) {
   constexpr int S = G::S, SA = G::SA;   // active species: the integrated state (chem.hip k_chem_gen)
@@ -574,8 +589,9 @@ int chem_cells(Ctx& x, double dt, const double* rho_rr) {
   constexpr double e1 = 0.5, e2 = -0.29079558716805469821718236208017e1, e3 = 0.22354069897811569627360909276199;
   const long n = x.C;
   const double *Tf = x.f("T"), *pf = x.f("p"), *Yf = x.f("Y");
-  double *RR = x.f("RR"), *stats = x.f("chem_stats");
+  double *RR = x.f("RR"), *stats = x.f("chem_stats"), *Qdot = x.f("Qdot");
   const double rtol = x.rtol, atol = x.atol, Tmin = x.Tmin;
+  const std::vector<double> hc = hf298_per_mass(x);
   const int max_steps = x.max_steps;
   int fail = 0;
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : fail)
@@ -639,10 +655,14 @@ int chem_cells(Ctx& x, double dt, const double* rho_rr) {
       }
       if (steps >= 0) hnext = h;
     }
+    double q = 0.0;
     for (int i = 0; i < S; ++i) {
       const double Yn = y[i] * G::W[i] / rho;
-      RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho_rr[c] / dt : 0.0;
+      const double rr = T >= Tmin ? (Yn - Y0[i]) * rho_rr[c] / dt : 0.0;
+      RR[(long)i * n + c] = rr;
+      q -= hc[i] * rr;
     }
+    Qdot[c] = q;
     stats[c] = steps;
     stats[n + c] = rejects;
     if (hnext > 0.0) stats[2 * n + c] = hnext;
@@ -1202,6 +1222,9 @@ int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps) {
 
 int dfmi_dnn_set_model(dfmi_ctx*, int, int, const int*, const float*, const double*, const double*, const double*,
                        const double*, double, double) {
+  return guard([&] { throw Error("dfmi (CPU-A): DNN chemistry is a GPU-path feature"); });
+}
+int dfmi_dnn_load_model(dfmi_ctx*, const char*, double, double) {
   return guard([&] { throw Error("dfmi (CPU-A): DNN chemistry is a GPU-path feature"); });
 }
 int dfmi_dnn_infer(dfmi_ctx*, int*) { return guard([&] { throw Error("dfmi (CPU-A): DNN chemistry is a GPU-path feature"); }); }

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <numeric>
 
 struct dfmi_ctx { dfmi::Ctx x; };
@@ -47,6 +48,7 @@ void allocate_fields(Ctx& x) {
   }
   alloc_field(x, "tauU", C, 9, false);
   alloc_field(x, "chem_stats", C, 3, false);   // per cell: accepted / rejected integrator steps, next step size
+  alloc_field(x, "Qdot", C, 1, false);         // heat release -sum_i hc_i RR_i [W/m^3] (dfChemistryModel.C:771)
   alloc_field(x, "boundary_tauU", B, 9, true);
   alloc_field(x, "boundary_heGradient", B, 1, true);   // gradientEnergy patches (dfEEqn.cu:266-287)
   // mixed conditions: p's waveTransmissive valueFraction (set at each pEqn assembly) and gamma; the
@@ -247,8 +249,9 @@ void do_U_Y_fork(Ctx& x) {
   }
   DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
   DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_fork, 0));
-  // the weights' event is recorded below, after the side stream's launches that do not need it are issued
-  // (hipStreamWaitEvent waits for the event's most recent record at call time, so it is recorded first)
+  // the weights' event is recorded on the main stream right after the weights, before the side stream's
+  // hipStreamWaitEvent on it is issued (inside do_Y_front: a wait binds to the event's most recent record at call
+  // time, so the record must come first); the side stream's chemistry and preparation do not wait for it
   conv_weights(x);
   DFMI_HIP(hipEventRecord(x.ev_cw, x.stream));
   OnStream _os(x, x.stream2);
@@ -660,6 +663,12 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
   return guard([&] {
     Ctx& x = ctx->x;
     require_ready(x);
+    // a step that throws records no end mark: restart the timer's ring so no reported interval spans two steps
+    struct TimerReset {
+      StepTimer& t;
+      bool done = false;
+      ~TimerReset() { if (!done) t.used = 0; }
+    } treset{x.steptimer};
     if (x.steptimer.on && x.steptimer.used == 0) x.steptimer.mark(x.stream);
     x.dnn.prepared = false;         // never reuse a compaction of an earlier (failed) step
     copy_old(x);                    // preTimeStep
@@ -681,6 +690,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
     if (x.chem.mode == 1) chem_check(x);   // the p solves' polls have already passed the chemistry
     if (x.steptimer.on) x.steptimer.mark(x.stream);
+    treset.done = true;
   });
 }
 
@@ -698,10 +708,13 @@ int dfmi_step_times(dfmi_ctx* ctx, double* ms, int n, int* got) {
     Ctx& x = ctx->x;
     DFMI_HIP(hipStreamSynchronize(x.stream));
     const StepTimer& t = x.steptimer;
-    const int have = t.used > 1 ? (int)t.used - 1 : 0;
+    // intervals between consecutive marks still in the ring: the last min(used, CAP) - 1 of them
+    const size_t kept = std::min(t.used, StepTimer::CAP);
+    const int have = kept > 1 ? (int)kept - 1 : 0;
+    const size_t m0 = t.used - kept;
     for (int i = 0; i < have && i < n; ++i) {
       float v = 0;
-      DFMI_HIP(hipEventElapsedTime(&v, t.ev[i], t.ev[i + 1]));
+      DFMI_HIP(hipEventElapsedTime(&v, t.at(m0 + i), t.at(m0 + i + 1)));
       ms[i] = v;
     }
     if (got) *got = have;
@@ -900,6 +913,51 @@ int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* di
   });
 }
 
+int dfmi_dnn_load_model(dfmi_ctx* ctx, const char* path, double T_react, double dt_infer) {
+  std::vector<char> raw;
+  int rc = guard([&] {
+    DFMI_CHECK(path, "null path");
+    std::ifstream in(path, std::ios::binary);
+    DFMI_CHECK(in.good(), std::string("cannot open DF-ODENet model file ") + path);
+    raw.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+  });
+  if (rc) return rc;
+  int nmod = 0, nl = 0;
+  std::vector<int> dims;
+  std::vector<double> xmu, xstd, ymu, ystd;
+  std::vector<float> params;
+  rc = guard([&] {
+    size_t o = 0;
+    auto take = [&](void* dst, size_t n) {
+      DFMI_CHECK(o + n <= raw.size(), std::string("truncated DF-ODENet model file ") + path);
+      std::memcpy(dst, raw.data() + o, n);
+      o += n;
+    };
+    char magic[8];
+    take(magic, 8);
+    DFMI_CHECK(std::memcmp(magic, "DFMIDNN1", 8) == 0, std::string(path) + ": not a packed DF-ODENet file (DFMIDNN1)");
+    take(&nmod, 4);
+    take(&nl, 4);
+    DFMI_CHECK(nmod >= 1 && nmod <= 63 && nl >= 1 && nl <= 8, std::string(path) + ": bad module / layer counts");
+    dims.resize(nl + 1);
+    take(dims.data(), 4 * dims.size());
+    size_t np = 0;
+    for (int l = 0; l < nl; ++l) {
+      DFMI_CHECK(dims[l] > 0 && dims[l] <= 65536 && dims[l + 1] > 0 && dims[l + 1] <= 65536, std::string(path) + ": bad widths");
+      np += (size_t)dims[l] * dims[l + 1] + dims[l + 1];
+    }
+    xmu.resize(dims[0]); xstd.resize(dims[0]); ymu.resize(nmod); ystd.resize(nmod);
+    take(xmu.data(), 8 * xmu.size()); take(xstd.data(), 8 * xstd.size());
+    take(ymu.data(), 8 * ymu.size()); take(ystd.data(), 8 * ystd.size());
+    params.resize(np * nmod);
+    take(params.data(), 4 * params.size());
+    DFMI_CHECK(o == raw.size(), std::string(path) + ": trailing bytes after the parameters");
+  });
+  if (rc) return rc;
+  return dfmi_dnn_set_model(ctx, nmod, nl, dims.data(), params.data(), xmu.data(), xstd.data(), ymu.data(), ystd.data(),
+                            T_react, dt_infer);
+}
+
 int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting) {
   return guard([&] {
     Ctx& x = ctx->x;
@@ -984,7 +1042,15 @@ int dfmi_set_option(dfmi_ctx* ctx, const char* key, double value) {
     Ctx& x = ctx->x;
     (void)x.opt(key);   // throws for an unknown key
     const std::string k(key);
-    const bool structural = k.rfind("amg.", 0) == 0 || k == "solver.even_odd" || k == "solver.row_classes";
+    // keys read when the AMG hierarchy (amg_setup) or the solver rows (build_ell) are built; every other key is
+    // read at each call (amg.reuse per p solve, pcg.* / fv.* / chem.* / dnn.* per launch)
+    static const char* structural_keys[] = {"amg.omega", "amg.overcorrection", "amg.coarsest_sweeps",
+                                            "amg.coarsest_size", "amg.presweeps", "amg.pairwise_passes_l0",
+                                            "amg.pairwise_passes", "amg.precision", "amg.padded", "amg.tail",
+                                            "amg.halo_l0", "amg.global_coarse", "solver.even_odd", "solver.small",
+                                            "solver.row_classes"};
+    bool structural = false;
+    for (const char* s : structural_keys) structural |= k == s;
     DFMI_CHECK(!structural || (!x.amg.ready && !x.ell.ready),
                "dfmi_set_option: '" + k + "' shapes the solver structures; set it before the first solve");
     x.opts[k] = value;

@@ -475,7 +475,8 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
                                                 const double* __restrict__ rhof, const double* __restrict__ Yf,
                                                 double dt, double rtol, double atol, double Tmin, int max_steps,
                                                 int method, double* __restrict__ RR, double* __restrict__ stats,
-                                                int* __restrict__ fail, int tiled) {
+                                                int* __restrict__ fail, int tiled, const double* __restrict__ hc,
+                                                double* __restrict__ Qdot) {
   extern __shared__ double lds[];
   Lane<S> L;
   L.lane = threadIdx.x;
@@ -555,11 +556,15 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
     }
     if (steps >= 0) hnext = h;
   }
+  double q = 0.0;   // Qdot = -sum_i hc_i RR_i in species order (dfChemistryModel.C:771)
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double Yn = y[i] * m.W[i] / rho;
-    RR[(long)i * n + c] = T >= Tmin ? (Yn - Y0[i]) * rho_rr / dt : 0.0;
+    const double rr = T >= Tmin ? (Yn - Y0[i]) * rho_rr / dt : 0.0;
+    RR[(long)i * n + c] = rr;
+    q -= hc[i] * rr;
   }
+  Qdot[c] = q;
   stats[c] = steps;
   stats[n + c] = rejects;
   if (hnext > 0.0) stats[2 * n + c] = hnext;
@@ -608,7 +613,8 @@ template <class G>
 __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __restrict__ perm,
     const double* __restrict__ Tf, const double* __restrict__ pf, const double* __restrict__ rhof,
     const double* __restrict__ Yf, double dt, double rtol, double atol, double Tmin, int max_steps,
-    double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail, int tiled) {
+    double* __restrict__ RR, double* __restrict__ stats, int* __restrict__ fail, int tiled, const double* __restrict__ hc,
+    double* __restrict__ Qdot) {
   constexpr int S = G::S, SA = G::SA;
   constexpr double g = 0.43586652150845899941601945119356;
   constexpr double c21 = -0.10156171083877702091975600115545e1, c31 = 0.40759956452537699824805835358067e1,
@@ -696,11 +702,15 @@ __global__ void __launch_bounds__(LANES, 1) k_chem_gen(long n, const int* __rest
     if (steps >= 0) hnext = h;
   }
   const double rho_rr = rhof[c];   // Y0 and rho_rr re-read here rather than held through the integration
+  double q = 0.0;   // Qdot = -sum_i hc_i RR_i in species order (dfChemistryModel.C:771)
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double Yn = y[i] * G::W[i] / rho;
-    RR[(long)i * n + c] = T >= Tmin ? (Yn - Yf[(long)i * n + c]) * rho_rr / dt : 0.0;
+    const double rr = T >= Tmin ? (Yn - Yf[(long)i * n + c]) * rho_rr / dt : 0.0;
+    RR[(long)i * n + c] = rr;
+    q -= hc[i] * rr;
   }
+  Qdot[c] = q;
   stats[c] = steps;
   stats[n + c] = rejects;
   if (hnext > 0.0) stats[2 * n + c] = hnext;
@@ -783,7 +793,8 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   if (h.generated) {
     KScope _ks(x, "k_chem");
 #define GEN(G) hipLaunchKernelGGL((k_chem_gen<G>), g, dim3(LANES), 0, x.stream, (long)x.C, perm, x.f("T"), x.f("p"),  \
-                                  rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats, h.fail.p, tiled)
+                                  rho_rr, x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, x.f("RR"), stats, h.fail.p, tiled,   \
+                                  x.thermo.dhc.p, x.f("Qdot"))
     if (h.generated == 1) GEN(ChemGen_burke9); else GEN(ChemGen_es80);
 #undef GEN
     DFMI_HIP(hipGetLastError());
@@ -794,7 +805,8 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   do {                                                                                                              \
     KScope _ks(x, "k_chem");                                                                                        \
     hipLaunchKernelGGL(k_chem<NS>, g, dim3(LANES), lds, x.stream, (long)x.C, perm, m, x.f("T"), x.f("p"), rho_rr,      \
-                       x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats, h.fail.p, tiled); \
+                       x.f("Y"), dt, h.rtol, h.atol, h.Tmin, h.max_steps, h.method, x.f("RR"), stats, h.fail.p, tiled,   \
+                       x.thermo.dhc.p, x.f("Qdot"));                                                          \
   } while (0)
   switch (x.S) {
     case 4: CALL(4); break; case 5: CALL(5); break; case 6: CALL(6); break; case 7: CALL(7); break;

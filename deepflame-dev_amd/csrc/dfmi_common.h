@@ -7,6 +7,12 @@
 #include <string>
 #include <vector>
 
+// The library is written for MI355X alone: wave_sum's v_permlane16/32_swap, the MFMA tiles of dnn.hip and the
+// LDS-DMA staging exist on gfx950 only. A device pass for any other target stops here with a clear message.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "dfmi targets gfx950 (MI355X) only: build with --offload-arch=gfx950 (Makefile ARCH)"
+#endif
+
 namespace dfmi {
 
 // Block -> cell range for the per-cell (gather) kernels: the dispatcher deals consecutive blocks

@@ -106,6 +106,8 @@ struct Thermo {
   int S = 0;
   std::vector<double> W, nasa, visc, cond, bdiff, vc1, vc2;
   DevBuf<double> dW, drW, dnasa, dvisc, dcond, dbdiff, dvc1, dvc2;   // drW = 1 / W
+  std::vector<double> hc;        // Hf298_i / W_i [J/kg]: the heat-release weights (dfChemistryModel.C:335-338)
+  DevBuf<double> dhc;
   // species-minor copies for the cooperative S > 16 kernel (lanes own consecutive species i, so a
   // coefficient load over a group is one contiguous run): nasa [15][S], bdiff [j][5][i], vc [j][i]
   DevBuf<double> dnasaT, dbdiffT, dvc1T, dvc2T;
@@ -182,19 +184,26 @@ struct KernelTimer {
 // Per-step timing (dfmi_step_timer / dfmi_step_times): while armed, dfmi_time_step records an event on the
 // context stream before its first step and after every step (no synchronisation), so the bench reads each
 // step's duration -- end of step i to end of step i-1 -- and reports their median beside the bracketed mean.
+// The events form a ring of CAP marks, so an armed timer holds a bounded number of events however many steps
+// run; dfmi_step_times reports the last CAP - 1 intervals. A step that fails resets the ring (its end mark is
+// never recorded, and an interval spanning two steps must not be reported).
 struct StepTimer {
+  static constexpr size_t CAP = 1024;
   bool on = false;
-  std::vector<hipEvent_t> ev;         // ev[0]: before the first armed step; ev[i]: after step i
-  size_t used = 0;
+  std::vector<hipEvent_t> ev;         // mark m at ev[m % CAP]: m = 0 before the first armed step, m = i after step i
+  size_t used = 0;                    // marks recorded since arming (or since the last failed step)
   ~StepTimer() { for (auto e : ev) (void)hipEventDestroy(e); }
   void mark(hipStream_t s) {
-    if (used == ev.size()) {
+    const size_t slot = used % CAP;
+    if (slot == ev.size()) {
       hipEvent_t e;
       DFMI_HIP(hipEventCreate(&e));
       ev.push_back(e);
     }
-    DFMI_HIP(hipEventRecord(ev[used++], s));
+    DFMI_HIP(hipEventRecord(ev[slot], s));
+    ++used;
   }
+  hipEvent_t at(size_t m) const { return ev[m % CAP]; }
 };
 
 // Communication accounting per exchange point (dfmi_comm_timer / dfmi_comm_report): every transport call
@@ -492,6 +501,7 @@ void thermo_psip0(Ctx& x);
 void thermo_correct_psip_rho(Ctx& x);
 // thermo.hip
 void thermo_upload(Ctx& x);
+std::vector<double> heat_of_formation_per_mass(int S, const double* W, const double* nasa);   // hc_i (Qdot weights)
 void thermo_correct(Ctx& x, bool from_T);
 // boundary_heGradient on gradientEnergy slots of he (0 elsewhere)
 void thermo_energy_gradient(Ctx& x);

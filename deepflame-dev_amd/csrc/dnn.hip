@@ -720,7 +720,8 @@ __global__ void __launch_bounds__(64 * OG) k_dnn_output(int n, int C, int S, int
                              const float* __restrict__ P, long sP, const float* __restrict__ b,
                              const double* __restrict__ Ymu, const double* __restrict__ Ystd,
                              const double* __restrict__ Y, const double* __restrict__ rho,
-                             const double* __restrict__ p, double dt, double* __restrict__ RR) {
+                             const double* __restrict__ p, double dt, double* __restrict__ RR,
+                             const double* __restrict__ hc, double* __restrict__ Qdot) {
   __shared__ double syn[64][64], ssum[64];   // [species][cell]; nmod <= 63
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + cl;
@@ -746,8 +747,17 @@ __global__ void __launch_bounds__(64 * OG) k_dnn_output(int n, int C, int S, int
     const double rc = rho[c], pc = p[c] / 101325.0, sum = ssum[cl];
     for (int m = g; m < nmod; m += OG) {
       const double y = syn[m][cl] / sum;
-      RR[(long)m * C + c] = (y - Y[(long)m * C + c]) * rc * pc / dt;
+      const double rr = (y - Y[(long)m * C + c]) * rc * pc / dt;
+      RR[(long)m * C + c] = rr;
+      syn[m][cl] = rr;   // only this thread reads syn[m][cl]; it now holds RR for the heat release below
     }
+  }
+  __syncthreads();
+  // Qdot = -sum_i hc_i RR_i in species order (pytorchFunctions.H:233-238; the inert species' RR is 0 here)
+  if (g == 0 && live && hc) {   // hc == nullptr: no thermo table uploaded (a surrogate-only context)
+    double q = 0.0;
+    for (int m = 0; m < nmod; ++m) q -= hc[m] * syn[m][cl];
+    Qdot[c] = q;
   }
 }
 
@@ -833,6 +843,7 @@ void dnn_solve(Ctx& x, const char* rho_field) {
   d.prepared = false;
   double* RR = x.f("RR");
   hipLaunchKernelGGL(k_zero, dim3(blocks_for((long)S * C, 256)), dim3(256), 0, x.stream, (long)S * C, RR);
+  hipLaunchKernelGGL(k_zero, dim3(blocks_for((long)C, 256)), dim3(256), 0, x.stream, (long)C, x.f("Qdot"));
   // the count was copied behind an event at the step start; the solver polls since then have passed it
   DFMI_HIP(hipEventSynchronize(d.nr_ev));
   const int nr = d.nr_host.p[0];
@@ -908,7 +919,8 @@ void dnn_solve(Ctx& x, const char* rho_field) {
     }
     KScope _ks(x, "k_dnn_output");
     hipLaunchKernelGGL(k_dnn_output, dim3(blocks_for(n, 64)), dim3(64 * OG), 0, x.stream, n, C, S, nq, d.nmod, idx,
-                       d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f(rho_field), x.f("p"), d.dt, RR);
+                       d.part.p, sP, d.b[L - 1].p, d.ymu.p, d.ystd.p, x.f("Y"), x.f(rho_field), x.f("p"), d.dt, RR,
+                       x.thermo.dhc.n == (size_t)S ? (const double*)x.thermo.dhc.p : nullptr, x.f("Qdot"));
     DFMI_HIP(hipGetLastError());
   }
 }

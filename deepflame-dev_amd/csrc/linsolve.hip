@@ -1804,8 +1804,10 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
   // a fixed SPD preconditioner of a matrix that changed by the density update only, so PCG still converges to
   // this system's own tolerance; the fp32 rounding and Galerkin sums of one solve are saved
   const bool reuse = amg && x.amg.ready && x.amg.reuse_ok && x.on("amg.reuse") && x.nranks == 1;
-  // face-wise PCG with the reused V-cycle: nothing reads the ELL values, so they are not written
-  const int novals = face && reuse ? 2 : 0;
+  // face-wise PCG with the reused V-cycle: nothing reads the ELL values, so they are not written -- only when
+  // the V-cycle's level 0 is the face-wise fp32 copy too (the fp64 V-cycle's level 0 reads the ELL values of
+  // THIS solve beside its diagonal, so they must be current)
+  const int novals = face && reuse && amg_l0_fusable(x) ? 2 : 0;
   { KScope _ks(x, "k_ell_build"); hipLaunchKernelGGL(k_ell_build, g, bl, 0, x.stream, m, ty, q, (const int*)nullptr, W, x.ell.src.p, Ce, val, v.dS, v.rhs, novals); }
   { KScope _ks(x, "k_copy_x"); hipLaunchKernelGGL(k_copy_x, g, bl, 0, x.stream, C, Ce, q, (const int*)nullptr, v.xw); }
   DFMI_HIP(hipGetLastError());

@@ -699,6 +699,23 @@ __global__ void k_energy_gradient_rt(MeshView m, int S, TC t, const int8_t* __re
 
 }  // namespace
 
+// hc_i = Hf298SS_i / W_i [J/kg] (dfChemistryModel.C:335-338): Cantera's NasaPoly2::reportHf298 -- the NASA7 range
+// holding 298.15 K (the low one when 298.15 <= T_mid), h/RT by NasaPoly1::updateProperties' expression
+// (ct_k = a_k T^k; h/RT = ct0 + ct1/2 + ct2/3 + ct3/4 + ct4/5 + a5/T), times GasConstant * 298.15.
+// oracle/chem_oracle.py:hf298_per_mass restates the same expression in the same order.
+std::vector<double> heat_of_formation_per_mass(int S, const double* W, const double* nasa) {
+  std::vector<double> hc(S);
+  const double T = 298.15, T2 = T * T, T3 = T2 * T, T4 = T3 * T, rT = 1.0 / T;
+  for (int i = 0; i < S; ++i) {
+    const double* row = nasa + 15 * i;
+    const double* a = T <= row[0] ? row + 8 : row + 1;
+    const double ct0 = a[0], ct1 = a[1] * T, ct2 = a[2] * T2, ct3 = a[3] * T3, ct4 = a[4] * T4;
+    const double h_RT = ct0 + 0.5 * ct1 + (1.0 / 3.0) * ct2 + 0.25 * ct3 + 0.2 * ct4 + a[5] * rT;
+    hc[i] = h_RT * R_GAS * T / W[i];
+  }
+  return hc;
+}
+
 void thermo_upload(Ctx& x) {
   Thermo& t = x.thermo;
   t.dW.upload(t.W, x.stream);
@@ -709,6 +726,8 @@ void thermo_upload(Ctx& x) {
     DFMI_HIP(hipStreamSynchronize(x.stream));
   }
   t.dnasa.upload(t.nasa, x.stream);
+  t.hc = heat_of_formation_per_mass(t.S, t.W.data(), t.nasa.data());
+  t.dhc.upload(t.hc, x.stream);
   t.dvisc.upload(t.visc, x.stream);
   t.dcond.upload(t.cond, x.stream);
   t.dbdiff.upload(t.bdiff, x.stream);

@@ -88,6 +88,7 @@ SIGNATURES = {
     "dfmi_chem_info": [_P, _IP],
     "dfmi_dnn_set_model": [_P, C.c_int, C.c_int, _IP, C.POINTER(C.c_float), _DP, _DP, _DP, _DP, C.c_double,
                            C.c_double],
+    "dfmi_dnn_load_model": [_P, C.c_char_p, C.c_double, C.c_double],
     "dfmi_dnn_infer": [_P, _IP],
     "dfmi_dnn_stats": [_P, _IP, _DP],
 }
@@ -354,13 +355,17 @@ class Context:
 
     def dnn_set_model(self, dims, params, x_mu, x_std, y_mu, y_std, T_react=610.0, dt_infer=1e-6):
         """params: list over modules of [(W [out,in], b [out]) per layer] (numpy float32)."""
+        from .dnn_checkpoint import pack_params
         d = _i32(dims)
-        flat = np.concatenate([np.concatenate([np.ravel(W), np.ravel(b)]) for mod in params for (W, b) in mod])
-        flat = np.ascontiguousarray(flat, dtype=np.float32)
+        flat = pack_params(params)
         self._keep_dnn = flat
         arr = [_f64(a) for a in (x_mu, x_std, y_mu, y_std)]
         self._call("dfmi_dnn_set_model", self.h, len(params), len(dims) - 1, _ip(d),
                    flat.ctypes.data_as(C.POINTER(C.c_float)), *[_dp(a) for a in arr], float(T_react), float(dt_infer))
+
+    def dnn_load_model(self, path, T_react=610.0, dt_infer=1e-6):
+        """a packed model file (dfmi/dnn_checkpoint.py write_packed) through dfmi_dnn_load_model"""
+        self._call("dfmi_dnn_load_model", self.h, str(path).encode(), float(T_react), float(dt_infer))
 
     def dnn_infer(self):
         n = C.c_int()

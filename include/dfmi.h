@@ -261,6 +261,11 @@ int dfmi_chem_info(dfmi_ctx* ctx, int* generated);
 int dfmi_dnn_set_model(dfmi_ctx* ctx, int n_modules, int n_layers, const int* dims, const float* params,
                        const double* x_mu, const double* x_std, const double* y_mu, const double* y_std,
                        double T_react, double dt_infer);
+/* the same model from a packed file (magic "DFMIDNN1", n_modules, n_layers, dims, the four normalisation vectors,
+ * the params above; written by deepflame-dev_amd/dfmi/dnn_checkpoint.py from a checkpoint in inference.py's
+ * state_dict layout) -- the file-path entry the reference's setConstantValue has (torch::jit::load of
+ * new_Temporary_Chemical_<i>.pt, dfChemistrySolver.cu:112-126), without executing a TorchScript program */
+int dfmi_dnn_load_model(dfmi_ctx* ctx, const char* path, double T_react, double dt_infer);
 /* run the surrogate on the current T, p, Y -> field "RR" (0 for non-reacting cells), scaled by field
  * "rho" (inside dfmi_time_step: "rho_old", as the reference passes d_rho_old, dfYEqn.cu:449) */
 int dfmi_dnn_infer(dfmi_ctx* ctx, int* n_reacting);

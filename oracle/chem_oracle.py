@@ -33,6 +33,35 @@ def g_RT(nasa, T):
     return out
 
 
+def hf298_per_mass(nasa, W):
+    """hc_i = Hf298SS_i / W_i [J/kg], dfChemistryModel.C:335-338. Cantera's NasaPoly2::reportHf298 takes the
+    NASA7 range holding 298.15 K (the low range when 298.15 <= T_mid) and NasaPoly1::updateProperties'
+    h/RT = ct0 + ct1/2 + ct2/3 + ct3/4 + ct4/5 + a5/T with ct_k = a_k T^k, times GasConstant * 298.15; the same
+    expression in the same order as the library's heat_of_formation_per_mass (thermo.hip), scalar Python floats."""
+    T = 298.15
+    T2 = T * T
+    T3 = T2 * T
+    T4 = T3 * T
+    rT = 1.0 / T
+    out = np.zeros(len(W))
+    for i, row in enumerate(np.asarray(nasa, dtype=np.float64)):
+        a = [float(v) for v in (row[8:15] if T <= row[0] else row[1:8])]
+        ct0, ct1, ct2, ct3, ct4 = a[0], a[1] * T, a[2] * T2, a[3] * T3, a[4] * T4
+        h_RT = ct0 + 0.5 * ct1 + (1.0 / 3.0) * ct2 + 0.25 * ct3 + 0.2 * ct4 + a[5] * rT
+        out[i] = h_RT * RU * T / float(W[i])
+    return out
+
+
+def heat_release(hc, RR):
+    """Qdot per cell = -sum_i hc_i RR_i, accumulated species by species from 0 (dfChemistryModel.C:753,771;
+    the DF-ODENet path pytorchFunctions.H:233-238). RR [S, n] -> Qdot [n]."""
+    RR = np.asarray(RR, dtype=np.float64)
+    q = np.zeros(RR.shape[1])
+    for i in range(RR.shape[0]):
+        q = q - float(hc[i]) * RR[i]
+    return q
+
+
 class Kinetics:
     def __init__(self, mech, nasa, W):
         self.m = mech
@@ -116,6 +145,10 @@ class Kinetics:
         if not sol.success:
             raise RuntimeError(sol.message)
         return sol.y[:, -1] * self.W / rho
+
+    def heat_release(self, RR):
+        """Qdot = -sum_i hc_i RR_i of reaction rates RR [S, n] (dfChemistryModel.C:771)."""
+        return heat_release(hf298_per_mass(self.nasa, self.W), RR)
 
     def reaction_rates(self, T, p, rho, Y, dt, **kw):
         """RR [S, n] = (Y(dt) - Y) rho / dt for each cell (columns of Y), dfChemistryModel::solveSingle

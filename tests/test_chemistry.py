@@ -92,3 +92,36 @@ def test_pack_layout():
     idata, irs, dd = m.pack()
     assert idata.shape == (23, 8) and irs.shape == (23, 6) and dd.shape == (23, ND0 + 9)
     assert (idata[:, 2] == (m.reac >= 0).sum(axis=1)).all()
+
+
+def test_heat_of_formation_weights_pinned():
+    """hc_i = Hf298_i / W_i (the Qdot weights, dfChemistryModel.C:335-338) from the mechanisms' NASA7 rows
+    against tabulated standard enthalpies of formation at 298.15 K (JANAF / ATcT, kJ/mol): elements in their
+    reference state are 0 and the radicals and water carry their formation enthalpies."""
+    from chem_oracle import hf298_per_mass
+    ref = {"H2": 0.0, "O2": 0.0, "N2": 0.0, "H2O": -241.826, "H": 217.998, "O": 249.18, "OH": 37.3,
+           "H2O2": -136.1, "HO2": 12.0}
+    for name in MECHS:
+        _, ym, _ = _kin(name)
+        hc = hf298_per_mass(ym["nasa"], ym["W"])
+        for i, sp in enumerate(ym["species"]):
+            if sp in ref:
+                kj_mol = hc[i] * ym["W"][i] / 1e6   # J/kg * kg/kmol = J/kmol -> kJ/mol
+                assert abs(kj_mol - ref[sp]) < 2.5, (name, sp, kj_mol)
+
+
+def test_heat_release_sums_species_in_order():
+    """Qdot = -sum_i hc_i RR_i (dfChemistryModel.C:771): a closed reactor conserves mass (sum RR = 0), and the
+    H2/O2 -> H2O conversion releases heat (Qdot > 0) on a hot cell."""
+    from chem_oracle import heat_release, hf298_per_mass
+    m, ym, kin = _kin(MECHS[0])
+    T, rho, Y = _states(ym, 4, seed=3)
+    T[:] = 1500.0
+    RR = kin.reaction_rates(T, None, rho, Y, 1e-6)
+    q = kin.heat_release(RR)
+    hc = hf298_per_mass(ym["nasa"], ym["W"])
+    manual = np.array([-sum(hc[i] * RR[i, c] for i in range(m.S)) for c in range(4)])
+    assert np.allclose(q, manual, rtol=1e-13, atol=0)
+    assert np.abs(RR.sum(axis=0)).max() < 1e-6 * np.abs(RR).max()
+    assert (q > 0).all()
+    assert np.array_equal(heat_release(hc, np.zeros((m.S, 3))), np.zeros(3))

@@ -100,6 +100,12 @@ def test_dnn_matches_torch_fp32():
     assert np.median(err) < 2e-3, np.median(err)
     assert err.max() < 2e-2, err.max()
     _check_half_semantics(RR, mods, T, p, rho, Y, XMU, XSTD, YMU, YSTD)
+    # heat release of the surrogate's source (pytorchFunctions.H:233-238) vs the oracle's sum over that RR
+    from chem_oracle import heat_release, hf298_per_mass
+    q = ctx.get_field("Qdot", (C,))
+    qref = heat_release(hf298_per_mass(t.nasa, t.W), RR)
+    assert np.array_equal(q, qref), np.abs(q - qref).max() / np.abs(qref).max()
+    assert np.all(q[T < 610.0] == 0.0) and np.abs(q).max() > 0
 
 
 def _half_reference(mods, T, p, rho, Y, xmu, xstd, ymu, ystd, dt=1e-6, Tr=610.0):
@@ -262,3 +268,49 @@ def test_dnn_wide_layer_kernels_bitwise_at_scale(monkeypatch):
         ctx.close()
     assert np.isfinite(out["0"]).all()
     assert np.array_equal(out["1"], out["0"]), np.abs(out["1"] - out["0"]).max()
+
+
+def test_dnn_packed_model_file_equals_set_model(tmp_path):
+    """dfmi_dnn_load_model (a packed file written from a reference-layout checkpoint, dfmi/dnn_checkpoint.py)
+    installs exactly the model dfmi_dnn_set_model does: the same RR and Qdot bit for bit"""
+    import torch
+    from dfmi.mesh import hex_box
+    from dfmi.mech import read_thermo_table, read_yaml_mechanism
+    from dfmi.lib import Context
+    from dfmi import case
+    from dfmi.dnn_checkpoint import from_state_dict, write_packed
+    ym = read_yaml_mechanism(os.path.join(GOLDEN, "Burke2012_s9r23.yaml"))
+    t = read_thermo_table(os.path.join(GOLDEN, "thermo_Burke2012_s9r23.txt"), ym["species"])
+    m = hex_box(16, 8, 8)
+    C = m.n_cells
+    mods = _weights()
+    sd = {"data_in_mean": torch.tensor(XMU), "data_in_std": torch.tensor(XSTD),
+          "data_target_mean": torch.tensor(YMU), "data_target_std": torch.tensor(YSTD)}
+    for i, layers in enumerate(mods):
+        sd[f"net{i}"] = {f"net.linear_layer_{k}.{n}": torch.from_numpy(a)
+                         for k, (W, b) in enumerate(layers) for n, a in (("weight", W), ("bias", b))}
+    path = tmp_path / "h2.dfmidnn"
+    write_packed(str(path), from_state_dict(sd))
+    rng = np.random.default_rng(4)
+    yu, yb = case.h2_air_compositions(ym["species"])
+    prog = rng.random(C)
+    Y = (1 - prog) * yu[:, None] + prog * yb[:, None]
+    Y /= Y.sum(axis=0)
+    T = 300.0 + 2200.0 * rng.random(C)
+    p = np.full(C, 101325.0)
+    rho = p * (1.0 / (Y / t.W[:, None]).sum(axis=0)) / (8314.46261815324 * T)
+    out = []
+    for how in ("set", "file"):
+        ctx = Context(0)
+        case.setup_context(ctx, m, t, ym["species"].index("N2"), 1e-6)
+        if how == "set":
+            ctx.dnn_set_model(DIMS, mods, XMU, XSTD, YMU, YSTD)
+        else:
+            ctx.dnn_load_model(path)
+        for n, v in (("T", T), ("p", p), ("rho", rho), ("Y", Y)):
+            ctx.set_field(n, v)
+        assert ctx.dnn_infer() == int((T >= 610.0).sum())
+        out.append((ctx.get_field("RR", (9, C)), ctx.get_field("Qdot", (C,))))
+        ctx.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.abs(out[0][0]).max() > 0

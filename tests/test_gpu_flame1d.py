@@ -93,6 +93,16 @@ def test_flame1d_front_chemistry_matches_oracle():
     ref = Kinetics(mech, ym["nasa"], ym["W"]).reaction_rates(T[idx], p[idx], rho[idx], Y[:, idx], dt)
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     assert (np.abs(rr - ref) / scale).max() < 1e-4
+    # heat release over the whole flame (dfChemistryModel.C:771): the oracle's sum of the GPU's RR, and the
+    # front's Qdot against the oracle's BDF source
+    from chem_oracle import heat_release, hf298_per_mass
+    RR = ctx.get_field("RR", (t.S, m.n_cells))
+    q = ctx.get_field("Qdot", (m.n_cells,))
+    hc = hf298_per_mass(t.nasa, t.W)
+    qref = heat_release(hc, RR)
+    assert rel_err(q, qref) <= 1e-12, rel_err(q, qref)
+    assert q.max() > 0.0                                  # heat is released in the reaction zone
+    assert (np.abs(heat_release(hc, ref) - q[idx]) / np.abs(q).max()).max() < 1e-4
 
 
 def test_flame1d_runs_bounded():

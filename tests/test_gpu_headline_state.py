@@ -64,6 +64,13 @@ def test_tgv64_tile_with_chemistry_matches_oracle():
     scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-3 * np.abs(ref).max())
     assert np.abs(RR).max() > 0
     assert (np.abs(RR[:, sel] - ref) / scale).max() < 2e-3
+    # heat release Qdot = -sum_i hc_i RR_i of that source (dfChemistryModel.C:771) vs the oracle's sum
+    from chem_oracle import heat_release, hf298_per_mass
+    q = ctx.get_field("Qdot", (C,))
+    qref = heat_release(hf298_per_mass(t.nasa, t.W), RR)
+    assert rel_err(q, qref) <= 1e-12, rel_err(q, qref)
+    assert q.max() > 0
+    assert (np.abs(heat_release(hf298_per_mass(t.nasa, t.W), ref) - q[sel]) / np.abs(qref).max()).max() < 2e-3
     # one outer iteration with the chemistry inside the step vs the oracle fed the same source
     case.push_state(ctx, st)
     ctx.set_field("chem_stats", np.zeros((3, C)))
@@ -74,6 +81,7 @@ def test_tgv64_tile_with_chemistry_matches_oracle():
     st2 = dict(st)
     ctx.time_step(2)
     assert np.array_equal(ctx.get_field("RR", (t.S, C)), RR)   # the step integrated exactly that source
+    assert np.array_equal(ctx.get_field("Qdot", (C,)), q)       # ... and reported its heat release
     st2["RR"] = RR
     print("GPU step done, oracle step", flush=True)
     o = O.Oracle(m, t, {k: v.copy() for k, v in st2.items()}, pt, inert, 1.0 / dt)
