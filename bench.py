@@ -729,6 +729,27 @@ def main():
                "value": m.n_cells * world * args.alt_steps / ea}
         for term, sch in schemes.items():
             ctx.set_scheme(term, sch)
+    # ---- several ranks: the other setting of the overlapped solver halos (option halo.overlap, read per solve),
+    # timed beside the headline the same way, so one multi-GPU run decides DESIGN.md 7's rule from its own numbers
+    ovl = None
+    if world > 1 and args.alt_steps > 0:
+        cur = ctx.get_option("halo.overlap")
+        ctx.set_option("halo.overlap", 0.0 if cur else 1.0)
+        ctx.time_step(args.ncorr)
+        ctx.sync()
+        dist.barrier()
+        ta = time.perf_counter()
+        for _ in range(args.alt_steps):
+            ctx.time_step(args.ncorr)
+        ctx.sync()
+        eo_ = time.perf_counter() - ta
+        tt = torch.tensor([eo_], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        eo_ = float(tt.item())
+        ctx.set_option("halo.overlap", cur)
+        ovl = {"halo_overlap": 0 if cur else 1, "headline_halo_overlap": int(cur), "steps": args.alt_steps,
+               "ms_per_step": eo_ / args.alt_steps * 1e3, "value": m.n_cells * world * args.alt_steps / eo_,
+               "speedup_vs_headline": (el / args.steps) / (eo_ / args.alt_steps)}
 
     ncls = ctx.row_classes()
     hexd = ctx.hex_dims()
@@ -816,6 +837,19 @@ def main():
                              if fl else "no PMC FLOP counts for this workload",
                              "hbm_achieved_GBs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS})
     hbm = {k: v for k, v in roofs.items() if v["bound"] == "hbm"}
+    # the north star's face-flux assembly item as one number (achieved = sum of the assembly kernels'
+    # algorithmic bytes / (sum of their kernel time x 8 TB/s)), with the PMC traffic of the same kernels beside it
+    asm = [k for k in ASSEMBLY_KERNELS if k in roofs]
+    asm_bytes = sum(roofs[k]["algorithmic_bytes"] * roofs[k]["launches"] for k in asm)
+    asm_ms = sum(roofs[k]["total_ms"] for k in asm)
+    asm_traffic = (sum(roofs[k]["traffic"] * roofs[k]["launches"] for k in asm) / asm_bytes
+                   if asm and all(roofs[k]["traffic"] for k in asm) else None)
+    assembly_roofline = ({"kernels": asm, "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                          "achieved": asm_bytes / (asm_ms / 1e3) / 1e9, "frac": asm_bytes / (asm_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                          "algorithmic_bytes_per_step": asm_bytes / max(args.roof_steps, 1),
+                          "kernel_ms_per_step": asm_ms / max(args.roof_steps, 1),
+                          "traffic_over_algorithmic": asm_traffic,
+                          "per_kernel_frac": {k: roofs[k]["frac"] for k in asm}} if asm and asm_ms > 0 else None)
     primary = args.kernel if args.kernel != "auto" else (max(hbm, key=lambda k: hbm[k]["total_ms"]) if hbm else None)
     out = {
         "metric": "cell-updates/s (dfLowMachFoam outer iter)",
@@ -893,9 +927,12 @@ def main():
                                    "frac": gemm_flops / (gemm_ms / 1e3) / 1e12 / 2500.0},
                  "inferences_per_s_gemm_time": n_react * args.roof_steps / (gemm_ms / 1e3)}
                 if args.chem == "dnn" and gemm_ms > 0 else None),
+        "assembly_roofline": assembly_roofline,
         "finite": finite,
         "other_schemes": alt,
     }
+    if ovl is not None:
+        out["other_halo_overlap"] = ovl
     if comm is not None:
         out["comm"] = comm
     if world == 1 and out["roofline"] is not None:   # the headline kernel against a measured copy peak as well

@@ -227,15 +227,17 @@ void do_Y(Ctx& x) {
 }
 
 // The chemistry and the YEqn preparation/assembly read nothing the UEqn writes (T, p, Y, rho_old, phi, the
-// thermo's transport from the last correctThermo) and the UEqn nothing they write, so on one rank they run on
-// the side stream while the UEqn assembles and solves on the main one: the VALU-bound chemistry beside the
-// memory-bound UEqn. Both are issued before the UEqn's convergence polls block the host. Several ranks keep
-// one stream (every RCCL operation of a rank stays ordered on one communicator). DFMI_STEP_OVERLAP=0: off.
+// thermo's transport from the last correctThermo) and the UEqn nothing they write, so they run on the side stream
+// while the UEqn assembles and solves on the main one: the VALU-bound chemistry beside the memory-bound UEqn. Both
+// are issued before the UEqn's convergence polls block the host. With several ranks the side stream's field halos
+// (the YEqn preparation's sumYDiffError / hDiffCorrFlux, the EEqn scheme terms' gradients) go through the halo's
+// second channel -- its own RCCL communicator and buffers (halo.hip) -- so the two streams' exchanges never
+// interleave on one communicator; the chemistry needs no halo at all. DFMI_STEP_OVERLAP=0: off.
 // While per-kernel timers are armed (dfmi_kernel_timer: the bench's roofline pass) the step runs on one
 // stream, so every timed kernel has the GPU to itself and its HIP-event time is its own.
 bool step_overlap(const Ctx& x) {
   static const bool on = [] { const char* e = std::getenv("DFMI_STEP_OVERLAP"); return !(e && std::atoi(e) == 0); }();
-  return on && x.nranks == 1 && !halo_active(x) && x.ktimer.targets.empty();
+  return on && x.ktimer.targets.empty();
 }
 // the side stream forks from the main one and runs the YEqn front; ev_join marks its end. The side stream is the
 // longer of the two (chemistry, preparation, rows against the UEqn), so the div(phi,Yi_h) weights (they read phi,
@@ -1093,8 +1095,9 @@ void set_comm(Ctx& x, int nranks, int rank, const int* neighb) {
   x.nranks = nranks;
   x.rank = rank;
   x.peer.assign(neighb, neighb + x.P);
-  const char* e = std::getenv("DFMI_HALO_OVERLAP");   // overlapped solver halos (default off)
-  x.halo_overlap = e && std::atoi(e) != 0;
+  // overlapped solver halos: the option halo.overlap (read per solve); the environment sets its default here
+  const char* e = std::getenv("DFMI_HALO_OVERLAP");
+  if (e && !x.opts.count("halo.overlap")) x.opts["halo.overlap"] = std::atoi(e) != 0 ? 1.0 : 0.0;
 }
 // the exchange lists need the boundary topology: built now, or at the end of
 // dfmi_init_constant_fields_boundary (every rank reaches both points in the same order)

@@ -266,6 +266,8 @@ inline const OptDef* option_defs(int& n) {
     {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
     {"chem.binning", 2},              // cells launched in cost-binned order: 1 over the mesh, 2 inside 4096-cell tiles
     {"dnn.tuned_gemm", 1},            // DF-ODENet layers by the shape-tuned kernels (0: k_mlp_gemm for every layer)
+    {"halo.overlap", 0},              // several ranks: solver halo exchanges on a comm stream while the interior rows run
+                                      // (read per solve; DFMI_HALO_OVERLAP sets the default when the communicator is set)
   };
   n = (int)(sizeof(d) / sizeof(d[0]));
   return d;
@@ -358,7 +360,6 @@ struct Ctx {
       return v;
     }
   } ell;
-  bool halo_overlap = false;     // DFMI_HALO_OVERLAP=1: solver halo exchanges overlap the interior rows
   Amg amg;                       // pressure preconditioner hierarchy (amg.hip)
   Chem chem;
   Dnn dnn;
@@ -546,6 +547,8 @@ struct HaloItem {
   long cstride, dstride;
   bool to_slots;
   bool split = false;   // the source vector is stored in the even-odd row order (Ell::eo): send value[eo_pos[cell]]
+  int colour = -1;      // split vectors: -1 every processor face; k: only the faces whose sending cell has colour k
+                        // (the next half-row pass reads no other halo entries; halo.hip Plan)
 };
 bool halo_active(const Ctx& x);
 void halo_update(Ctx& x, const HaloItem* items, int n);

@@ -435,35 +435,41 @@ __global__ void __launch_bounds__(TPB) k_eo_init_o(long C, long Ce, int ne, int 
 
 // prologue: res0 (it 0: the full initial residual), res = ||D r||, rho, convergence;
 // colour-0 rows: w = H_eo p (p's colour-0 half)
+// defer (several ranks, it > 0): ||D r|| rides the next all-gather (k_eo_c's) instead of its own, so the stop test
+// moves there; this launch only takes rho (k_eo_xp's) and forms w
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_eo_a(long C, long Ce, int ne, int W_, ColView col,
                                               const double* __restrict__ val, int it, int max_iter, double tol,
-                                              double abs_tol, Red redI, Red redR, double* scal, BV b) {
+                                              double abs_tol, Red redI, Red redR, double* scal, BV b, int defer = 0) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (it > 0 && st[6] == 0.0) return;   // stopped earlier (uniform per block)
-  double res0, n2, rho;
-  if (it == 0) {
-    double e[1], o[3];
-    red_sum<1>(redI, s, e);
-    red_sum<3>(redR, s, o);
-    res0 = sqrt(e[0] + o[0]); n2 = o[1]; rho = o[2];
+  if (defer) {
+    if (leader()) st[0] = st[8];
   } else {
-    double o[2];
-    red_sum<2>(redR, s, o);
-    n2 = o[0]; rho = st[8]; res0 = st[4];
+    double res0, n2, rho;
+    if (it == 0) {
+      double e[1], o[3];
+      red_sum<1>(redI, s, e);
+      red_sum<3>(redR, s, o);
+      res0 = sqrt(e[0] + o[0]); n2 = o[1]; rho = o[2];
+    } else {
+      double o[2];
+      red_sum<2>(redR, s, o);
+      n2 = o[0]; rho = st[8]; res0 = st[4];
+    }
+    const double res = sqrt(n2);
+    const bool keep = it == 0 && (res0 <= abs_tol || res0 == 0.0);
+    const bool stop = keep || res <= tol * res0 || res <= abs_tol || it >= max_iter ||
+                      (it > 0 && (rho == 0.0 || st[3] == 0.0));
+    if (leader()) {
+      if (it == 0) { st[4] = res0; st[9] = keep ? 1.0 : 0.0; }
+      st[0] = rho;
+      st[5] = res; st[7] = it;
+      st[6] = stop ? 0.0 : 1.0;
+    }
+    if (stop) return;
   }
-  const double res = sqrt(n2);
-  const bool keep = it == 0 && (res0 <= abs_tol || res0 == 0.0);
-  const bool stop = keep || res <= tol * res0 || res <= abs_tol || it >= max_iter ||
-                    (it > 0 && (rho == 0.0 || st[3] == 0.0));
-  if (leader()) {
-    if (it == 0) { st[4] = res0; st[9] = keep ? 1.0 : 0.0; }
-    st[0] = rho;
-    st[5] = res; st[7] = it;
-    st[6] = stop ? 0.0 : 1.0;
-  }
-  if (stop) return;
   const int W = WT > 0 ? WT : W_;
   const double* vs = val + (long)(b.vshared ? 0 : s) * W * C;
   double* ps = b.p + s * Ce;
@@ -504,14 +510,29 @@ __global__ void __launch_bounds__(TPB) k_eo_b(long C, long Ce, int ne, int no, i
 }
 
 // prologue: alpha = rho / (r0.v); colour-0 rows: w2 = H_eo s, s = r - alpha v formed at the neighbours
+// defer (k_eo_a's): redV also carries ||D r||^2 of the last update -- the stop test of this iteration runs here
 template <int WT>
 __global__ void __launch_bounds__(TPB) k_eo_c(long C, long Ce, int ne, int W_, ColView col,
-                                              const double* __restrict__ val, Red redV, double* scal, BV b) {
+                                              const double* __restrict__ val, Red redV, double* scal, BV b,
+                                              int defer = 0, int it = 0, double tol = 0.0, double abs_tol = 0.0) {
   const int s = blockIdx.y;
   double* st = scal + s * NSCAL;
   if (st[6] == 0.0) return;
-  double rv[1];
-  red_sum<1>(redV, s, rv);
+  double rv[2];
+  if (defer) {
+    red_sum<2>(redV, s, rv);
+    const double res = sqrt(rv[1]);
+    const bool stop = res <= tol * st[4] || res <= abs_tol || st[0] == 0.0 || st[3] == 0.0;
+    if (leader()) {
+      st[5] = res; st[7] = it;
+      if (stop) st[6] = 0.0;
+    }
+    if (stop) return;
+  } else {
+    double r1[1];
+    red_sum<1>(redV, s, r1);
+    rv[0] = r1[0];
+  }
   const double alpha = rv[0] != 0.0 ? st[0] / rv[0] : 0.0;
   if (leader()) st[2] = alpha;
   const int W = WT > 0 ? WT : W_;
@@ -527,6 +548,16 @@ __global__ void __launch_bounds__(TPB) k_eo_c(long C, long Ce, int ne, int W_, C
     for_cols<WT>(col, s_ct, rb, C, W, i, [&](int k, int j) { o += vs[k * C + i] * (rs[j] - alpha * ws[j]); });
     ts[i] = o / b.dS[s * Ce + i];
   });
+}
+
+// several ranks: this rank's (r0.v, ||D r||^2) per system from k_eo_b's and k_eo_xp's block partials, for one
+// all-gather
+__global__ void k_red_vr(const double* pV, const double* pR, int nblk, double* out) {
+  const int s = blockIdx.x;
+  double a[1], c[1];
+  red_sum<1>(Red{pV, nblk, 1, (long)nblk}, s, a);
+  red_sum<1>(Red{pR, nblk, 2, 2L * nblk}, s, c);
+  if (threadIdx.x == 0) { out[2 * s] = a[0]; out[2 * s + 1] = c[0]; }
 }
 
 // colour-1 rows: t = S s = s - H_oe w2; partials (t.s, t.t, r0.t, r0.s)
@@ -706,6 +737,89 @@ __global__ void __launch_bounds__(TPB) k_cg_x(long C, Red red, double* scal, dou
   for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     x[c] = x[c] + alpha * pnew[c];
     const double rr = v.r[c] - alpha * v.q[c];
+    v.r[c] = rr;
+    if (JAC) {
+      const double zz = rr / v.dS[c];
+      v.z[c] = zz;
+      acc[0] += rr * zz;
+    }
+    acc[1] += rr * rr;
+  }
+  block_partials<2>(acc, partial, 0);
+}
+
+// ---- several ranks: single-reduction PCG (Chronopoulos & Gear 1989). Every dot product of an iteration --
+// gamma = r.z, delta = w.z with w = A z, and ||r||^2 -- goes out in ONE all-gather, where the standard
+// recurrence needs two (p.q before alpha, then r.z and r.r after the preconditioner): with p = z + beta p and
+// s = w + beta s (= A p, by recurrence), alpha = gamma / (delta - beta gamma / alpha_prev). The SpMV is applied
+// to z, so the halo carries z alone (the standard form exchanges z and p_old). Vectors: p in pa, s in pb, w in q.
+// scal: 0 gamma, 2 alpha, 4 res0, 5 res, 6 active, 7 iters (as the standard form); 10/11 and 12/13 gamma and alpha
+// of even / odd iterations (read by the next iteration's update).
+
+// w = A z over the row set; partial z.w
+template <int WT>
+__global__ void __launch_bounds__(TPB) k_cgcg_w(long C, int W_, ColView col, const double* __restrict__ val,
+                                                const double* scal, int it, CV v, double* partial, RowSet rs) {
+  if (it > 0 && scal[6] == 0.0) return;   // stopped (the update kernel of this iteration decided it)
+  const int W = WT > 0 ? WT : W_;
+  __shared__ int s_ct[CT_MAX];
+  col.stage(s_ct);
+  double acc[1] = {0.0};
+  for_rows(C, rs, [&](int c) {
+    const double y = ell_mv<WT>(W, C, col, s_ct, val, v.dS[c], v.z, c);
+    v.q[c] = y;
+    acc[0] += v.z[c] * y;
+  });
+  block_partials<1>(acc, partial, 0, rs);
+}
+
+// this rank's (||r||^2, r.z, z.w) from the three kernels' block partials, for the one all-gather
+__global__ void __launch_bounds__(TPB) k_cgcg_local(Red rr, Red rz, Red zw, const double* scal, int it, double* out) {
+  if (it > 0 && scal[6] == 0.0) return;
+  double a[1], b[1], c[1];
+  red_sum<1>(rr, 0, a);
+  red_sum<1>(rz, 0, b);
+  red_sum<1>(zw, 0, c);
+  if (threadIdx.x == 0) { out[0] = a[0]; out[1] = b[0]; out[2] = c[0]; }
+}
+
+// prologue: the gathered (||r||^2, gamma, delta) -> stop test (k_cg_spmv's), beta, alpha; body: p = z + beta p,
+// s = w + beta s, x += alpha p, r -= alpha s; partials (r.z [Jacobi: z = r / dS here], r.r)
+template <bool JAC>
+__global__ void __launch_bounds__(TPB) k_cgcg_update(long C, int it, int max_iter, double tol, double abs_tol, Red red,
+                                                     double* scal, double* __restrict__ x, CV v, double* partial) {
+  if (it > 0 && scal[6] == 0.0) return;
+  double o[3];
+  {
+    double t[1];
+    red_sum<1>(red, 0, t); o[0] = t[0];
+    Red r1 = red; r1.p += 1; red_sum<1>(r1, 0, t); o[1] = t[0];
+    Red r2 = red; r2.p += 2; red_sum<1>(r2, 0, t); o[2] = t[0];
+  }
+  const double res = sqrt(o[0]), gamma = o[1], delta = o[2];
+  const double res0 = it == 0 ? res : scal[4];
+  // gamma and alpha of the previous iteration: slots 10/11 or 12/13 by iteration parity, so no block reads a slot
+  // the leader of this launch writes
+  const double gp = it == 0 ? 0.0 : scal[10 + 2 * ((it - 1) & 1)], ap = it == 0 ? 0.0 : scal[11 + 2 * ((it - 1) & 1)];
+  const bool stop = res <= tol * res0 || res <= abs_tol || it >= max_iter || (it > 0 && (gp == 0.0 || ap == 0.0));
+  const double beta = it == 0 ? 0.0 : gamma / gp;
+  const double den = it == 0 ? delta : delta - beta * gamma / ap;
+  const double alpha = den != 0.0 ? gamma / den : 0.0;
+  if (leader()) {
+    if (it == 0) scal[4] = res;
+    scal[5] = res; scal[7] = it;
+    scal[6] = stop ? 0.0 : 1.0;
+    scal[0] = gamma; scal[2] = alpha;
+    scal[10 + 2 * (it & 1)] = gamma; scal[11 + 2 * (it & 1)] = alpha;
+  }
+  if (stop) return;
+  double acc[2] = {0.0, 0.0};
+  for (int c = xcd_block() * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    const double pc = v.z[c] + beta * (it == 0 ? 0.0 : v.pa[c]);
+    const double sc = v.q[c] + beta * (it == 0 ? 0.0 : v.pb[c]);
+    v.pa[c] = pc; v.pb[c] = sc;
+    x[c] = x[c] + alpha * pc;
+    const double rr = v.r[c] - alpha * sc;
     v.r[c] = rr;
     if (JAC) {
       const double zz = rr / v.dS[c];
@@ -1075,10 +1189,10 @@ template <class F> void dispatch_W(int W, F&& f) {
   }
 }
 
-void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce, bool split = false) {
+void halo_vecs(Ctx& x, std::initializer_list<double*> vecs, int nsys, long Ce, bool split = false, int colour = -1) {
   if (!halo_active(x)) return;
   std::vector<HaloItem> it;
-  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false, split});
+  for (double* v : vecs) it.push_back({v, v, nsys, Ce, Ce, false, split, colour});
   halo_update(x, it.data(), (int)it.size());
 }
 
@@ -1658,16 +1772,17 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     double* pV = pR + (size_t)nsys * hb * 2;       // r0.v
     double* pT = pV + (size_t)nsys * hb;           // (t.s, t.t, r0.t, r0.s)
     // exchange points (several ranks): every kernel that gathers across a processor face reads the other
-    // colour's rows of the vector it gathers, exchanged just before it
-    auto hx = [&](std::initializer_list<double*> v) { halo_vecs(x, v, nsys, Ce, true); };
-    hx({b.xw});
+    // colour's rows of the vector it gathers, exchanged just before it -- only that colour's faces (k: the colour
+    // the sending side's cells have, i.e. the colour the half-row pass after it reads)
+    auto hx = [&](std::initializer_list<double*> v, int k) { halo_vecs(x, v, nsys, Ce, true, k); };
+    hx({b.xw}, -1);   // both halves: init_e reads x's colour 1, init_o its colour 0
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_init");
       hipLaunchKernelGGL(k_eo_init_e<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, b, pI);
     });
     const Red rI = L.after(pI, 1, 1, hb);
-    hx({b.p});
+    hx({b.p}, 0);
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_bcg_init");
@@ -1676,29 +1791,48 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
     DFMI_HIP(hipGetLastError());
     Red red = L.after(pR3, 3, 0, hb);
     Poller poll(x, WS.scal.p, nsys, std::string(eqn) + (x.ws_is_y ? "/y" : ""));
+    // several ranks: from the second iteration on, ||D r|| of the last update rides the r0.v all-gather and the
+    // stop test runs in k_eo_c (two all-gathers per iteration instead of three); the last allowed iteration keeps
+    // the test in k_eo_a so the solve ends with its residual recorded
+    const bool merged = x.nranks > 1;
     for (int it = 0;; ++it) {
-      hx({b.p});
+      const bool last = it >= cfg.max_iter;
+      const int defer = merged && it > 0 && !last ? 1 : 0;
+      if (merged && it > 0 && last) red = L.after(pR, 2, 0, hb);
+      hx({b.p}, 1);
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_eo");
         hipLaunchKernelGGL(k_eo_a<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, it, cfg.max_iter, cfg.tol,
-                           cfg.abs_tol, rI, red, WS.scal.p, b);
+                           cfg.abs_tol, rI, red, WS.scal.p, b, defer);
       });
-      if (it >= cfg.max_iter) break;
-      hx({b.p});
+      if (last) break;
+      hx({b.p}, 0);   // w in p's colour-0 half
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_eo");
         hipLaunchKernelGGL(k_eo_b<WT>, gh, bl, 0, x.stream, C, Ce, ne, no, W, ec, val, WS.scal.p, b, pV);
       });
-      const Red rV = L.after(pV, 1, 0, hb);
-      hx({b.r, b.v});
+      Red rV;
+      if (defer) {   // (r0.v, ||D r||^2) per system in one all-gather
+        const size_t per = (size_t)nsys * 4;
+        if (WS.red_local.n < 2 * per) WS.red_local.alloc(2 * per);
+        if (WS.red_all.n < 2 * per * x.nranks) WS.red_all.alloc(2 * per * x.nranks);
+        hipLaunchKernelGGL(k_red_vr, dim3(nsys), dim3(TPB), 0, x.stream, pV, pR, hb, WS.red_local.p);
+        DFMI_HIP(hipGetLastError());
+        halo_allgather(x, WS.red_local.p, WS.red_all.p, (long)nsys * 2);
+        rV = Red{WS.red_all.p, x.nranks, (long)nsys * 2, 2};
+      } else {
+        rV = L.after(pV, 1, 0, hb);
+      }
+      hx({b.r, b.v}, 1);
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_eo");
-        hipLaunchKernelGGL(k_eo_c<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, rV, WS.scal.p, b);
+        hipLaunchKernelGGL(k_eo_c<WT>, gh, bl, 0, x.stream, C, Ce, ne, W, ec, val, rV, WS.scal.p, b, defer, it, cfg.tol,
+                           cfg.abs_tol);
       });
-      hx({b.t});
+      hx({b.t}, 0);   // w2 in t's colour-0 half
       dispatch_W(W, [&](auto wt) {
         constexpr int WT = decltype(wt)::value;
         KScope _ks(x, "k_bcg_eo");
@@ -1709,10 +1843,10 @@ SolveStats solve_bicgstab(Ctx& x, const char* eqn, int nsys, const int* sys_map_
       { KScope _ks(x, "k_bcg_xp"); hipLaunchKernelGGL(k_eo_xp, gh, bl, 0, x.stream, Ce, ne, no, rT, WS.scal.p, b, pR,
                                                       pseq ? WS.poll.d : (PollRec*)nullptr, pseq); }
       DFMI_HIP(hipGetLastError());
-      red = L.after(pR, 2, 0, hb);
+      if (!merged) red = L.after(pR, 2, 0, hb);
       if (poll.check()) break;
     }
-    hx({b.xw});
+    hx({b.xw}, 1);
     dispatch_W(W, [&](auto wt) {
       constexpr int WT = decltype(wt)::value;
       KScope _ks(x, "k_eo_final");
@@ -1852,25 +1986,50 @@ SolveStats solve_pcg(Ctx& x, const char* eqn, const double* lower, const double*
     else hipLaunchKernelGGL(k_cg_init<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, v, q2, fo);
   });
   DFMI_HIP(hipGetLastError());
+  if (x.nranks > 1) {
+    // several ranks: the single-reduction form -- per iteration the preconditioner, w = A z with z's halo, and ONE
+    // all-gather of (||r||^2, r.z, z.w), then the update (two all-gathers and the p_old halo in the standard form)
+    if (x.sws().red_local.n < 8) x.sws().red_local.alloc(8);
+    if (x.sws().red_all.n < (size_t)8 * x.nranks) x.sws().red_all.alloc((size_t)8 * x.nranks);
+    double* loc = x.sws().red_local.p;
+    double* all = x.sws().red_all.p;
+    const Red red_g{all, x.nranks, 3, 0};
+    Poller poll(x, WS.scal.p, 1, std::string(eqn) + (amg ? "/amg" : "/jacobi") + "/cg1");
+    for (int it = 0;; ++it) {
+      if (amg) {
+        if (x.amg.halo_l0) halo_vecs(x, {v.r}, 1, Ce);   // the V-cycle's level 0 reads the residual across ranks
+        amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, it == 0 ? nullptr : WS.scal.p + 6);
+      }
+      const int np = spmv_with_halo(x, {v.z}, 1, Ce, nblk, [&](RowSet rs) {
+        dispatch_W(W, [&](auto wt) {
+          constexpr int WT = decltype(wt)::value;
+          KScope _ks(x, "k_cg_spmv");
+          hipLaunchKernelGGL(k_cgcg_w<WT>, g, bl, 0, x.stream, C, W, x.ell.cols(), val, WS.scal.p, it, v, q1, rs);
+        });
+      });
+      hipLaunchKernelGGL(k_cgcg_local, dim3(1), dim3(TPB), 0, x.stream, Red{q2 + 1, nblk, 2, 0},
+                         amg ? Red{q3, nblk, 1, 0} : Red{q2, nblk, 2, 0}, Red{q1, np, 1, 0}, WS.scal.p, it, loc);
+      DFMI_HIP(hipGetLastError());
+      halo_allgather(x, loc, all, 3);
+      {
+        KScope _ks(x, "k_cg_x");
+        if (amg)
+          hipLaunchKernelGGL(k_cgcg_update<false>, g, bl, 0, x.stream, C, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red_g,
+                             WS.scal.p, xsol, v, q2);
+        else
+          hipLaunchKernelGGL(k_cgcg_update<true>, g, bl, 0, x.stream, C, it, cfg.max_iter, cfg.tol, cfg.abs_tol, red_g,
+                             WS.scal.p, xsol, v, q2);
+      }
+      DFMI_HIP(hipGetLastError());
+      if (it >= cfg.max_iter) break;
+      if (poll.after(it)) break;
+    }
+    record_stats(x, eqn, WS.scal.p, 1);
+    return SolveStats{};
+  }
   // (r.z, r.r) readers: Jacobi -> both from q2; AMG -> r.z from the V-cycle's partials in q3
   // act: the solve's active flag (after the first iteration the V-cycle of a stopped solve is skipped)
-  auto reds = [&](Red& rz, Red& rr, const double* act) {
-    if (amg && x.nranks > 1) {
-      // several ranks: both sums (r.r from the update, r.z from the V-cycle) go out in ONE all-gather
-      // of three values per rank instead of two collectives per iteration
-      if (x.sws().red_local.n < 8) x.sws().red_local.alloc(8);
-      if (x.sws().red_all.n < (size_t)8 * x.nranks) x.sws().red_all.alloc((size_t)8 * x.nranks);
-      double* loc = x.sws().red_local.p;
-      hipLaunchKernelGGL(k_red_local<2>, dim3(1), dim3(TPB), 0, x.stream, q2, nblk, loc);
-      if (x.amg.halo_l0) halo_vecs(x, {v.r}, 1, Ce);   // the V-cycle's level 0 reads the residual across ranks
-      amg_apply(x, val, v.dS, x.ell.cols(), v.r, v.z, q3, nblk, act);
-      hipLaunchKernelGGL(k_red_local<1>, dim3(1), dim3(TPB), 0, x.stream, q3, nblk, loc + 2);
-      DFMI_HIP(hipGetLastError());
-      halo_allgather(x, loc, x.sws().red_all.p, 3);
-      rr = Red{x.sws().red_all.p + 1, x.nranks, 3, 0};
-      rz = Red{x.sws().red_all.p + 2, x.nranks, 3, 0};
-      return;
-    }
+  auto reds = [&](Red& rz, Red& rr, const double* act) {   // one rank (several ranks: the form above)
     Red r2 = L.after(q2, 2, 0);
     rr = r2; rr.p += 1;
     if (amg) {
