@@ -255,6 +255,8 @@ void do_U_Y_fork(Ctx& x) {
   // hipStreamWaitEvent on it is issued (inside do_Y_front: a wait binds to the event's most recent record at call
   // time, so the record must come first); the side stream's chemistry and preparation do not wait for it
   conv_weights(x);
+  // (the YEqn preparation on the main stream ahead of the UEqn instead, the side stream holding the chemistry and the
+  // rows only: 14.02 / 14.05 -> 14.52 / 14.40 ms per step, round 6 -- not kept)
   DFMI_HIP(hipEventRecord(x.ev_cw, x.stream));
   OnStream _os(x, x.stream2);
   do_Y_front(x, false, x.ev_cw);

@@ -232,7 +232,8 @@ int channel_of(const Ctx& x, hipStream_t st) {
 void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<double*>& dst, const Plan& pl, int base,
               hipStream_t st) {
   Halo& h = *x.halo;
-  Channel& c = h.ch[channel_of(x, st)];
+  const int chan = channel_of(x, st);
+  Channel& c = h.ch[chan];
   const bool timed = st == x.stream;
   const int K = (int)src.size();
   for (int k0 = 0; k0 < K; k0 += MAXK) {
@@ -252,7 +253,8 @@ void exchange(Ctx& x, const std::vector<const double*>& src, const std::vector<d
       c.roff[i] = (long)kk * pl.pr_off[i]; c.rcnt[i] = (long)kk * pl.pr_cnt[i];
     }
     if (x.comm.on) {
-      auto& e = x.comm.pts[x.comm.tag.empty() ? std::string("halo") : x.comm.tag];
+      // the side stream's exchanges (channel 1) are reported as their own points
+      auto& e = x.comm.pts[(x.comm.tag.empty() ? std::string("halo") : x.comm.tag) + (chan ? " @side" : "")];
       hipEvent_t ea = x.comm.next(), eb = x.comm.next();
       DFMI_HIP(hipEventRecord(ea, st));
       c.tr->sendrecv(x, st, c.sbuf.p, c.rbuf.p, h.peers, c.soff, c.scnt, c.roff, c.rcnt);

@@ -1,16 +1,17 @@
 #!/bin/bash
 # The 2-rank RCCL rehearsal of the multi-GPU bench on the box's one GPU (socket transport, not xGMI): bench.py
 # --gpus 2 launches its own two ranks (DFMI_RCCL_SPLIT_HOSTS=1: each poses as its own host); in-order halos and
-# DFMI_HALO_OVERLAP=1. Each line's `comm` block lists the exchange points -> gpurun_out/r05_rccl2_<name>.json
+# DFMI_HALO_OVERLAP=1. Each line's `comm` block lists the exchange points -> gpurun_out/${TAG}_rccl2_<name>.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+TAG=${TAG:-r06}
 for v in halo:0 ov:1; do
   name="${v%%:*}"; ov="${v#*:}"
   DFMI_HALO_OVERLAP=$ov DFMI_RCCL_SPLIT_HOSTS=1 timeout -k 10 300 python3 bench.py --gpus 2 --n ${N:-128} --steps 3 \
-    --warmup 1 --roof-steps 2 --no-cpu --no-flame --alt-steps 0 > gpurun_out/r05_rccl2_$name.log 2>&1
+    --warmup 1 --roof-steps 2 --no-cpu --no-flame --alt-steps 0 > gpurun_out/${TAG}_rccl2_$name.log 2>&1
   rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  grep '^{' gpurun_out/r05_rccl2_$name.log | tail -1 > gpurun_out/r05_rccl2_$name.json
-  python3 - gpurun_out/r05_rccl2_$name.json <<'PY'
+  grep '^{' gpurun_out/${TAG}_rccl2_$name.log | tail -1 > gpurun_out/${TAG}_rccl2_$name.json
+  python3 - gpurun_out/${TAG}_rccl2_$name.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
 c = d["comm"]

@@ -91,12 +91,17 @@ def main():
     case.init_state(c, m, t.S, fl["T"], fl["p"], fl["U"], fl["Y"])
     del fl
     c.call("pre_time_step")
+    c.comm_timer(True)   # transport calls and bytes per exchange point (the side stream's listed as "@side")
     for _ in range(a.steps):
         c.time_step(2)
     mine = fields(c, m.n_cells)
     mine["gid"] = g
     mine["p_iters"] = int(c.solver_stats("p")[0])
+    comm = c.comm_report()
+    c.comm_timer(False)
     c.close()
+    every_comm = [None] * WORLD
+    dist.all_gather_object(every_comm, {k: {"calls": v["calls"], "bytes": v["bytes"]} for k, v in comm.items()})
     # fields travel through files (a 16M-cell run would push GBs through the object collectives)
     import tempfile
     xdir = [tempfile.mkdtemp(prefix="dfmi_rccl_") if RANK == 0 else None]
@@ -120,6 +125,12 @@ def main():
         res = {"world": WORLD, "decomp": list(decomp), "mesh": [nx, ny, nz], "cells": mg.n_cells,
                "overlap": a.overlap, "steps": a.steps, "tol": a.tol,
                "p_iters_per_rank": [int(o["p_iters"]) for o in allr], "vs_single_domain": {}, "vs_oracle": {}}
+        pts = sorted({k for e in every_comm for k in e})
+        res["comm_per_step"] = {k: {"calls_max": max(e.get(k, {}).get("calls", 0) for e in every_comm) / a.steps,
+                                    "bytes_max": max(e.get(k, {}).get("bytes", 0.0) for e in every_comm) / a.steps}
+                                for k in pts}
+        res["comm_calls_per_step_max"] = max(sum(v["calls"] for v in e.values()) for e in every_comm) / a.steps
+        res["comm_bytes_per_step_max"] = max(sum(v["bytes"] for v in e.values()) for e in every_comm) / a.steps
         orc = None
         if a.steps == 1 and not a.no_oracle:
             import oracle as O

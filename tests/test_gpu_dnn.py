@@ -284,8 +284,8 @@ def test_dnn_packed_model_file_equals_set_model(tmp_path):
     m = hex_box(16, 8, 8)
     C = m.n_cells
     mods = _weights()
-    sd = {"data_in_mean": torch.tensor(XMU), "data_in_std": torch.tensor(XSTD),
-          "data_target_mean": torch.tensor(YMU), "data_target_std": torch.tensor(YSTD)}
+    f64 = lambda v: torch.tensor(v, dtype=torch.float64)   # the normalisation stays double, as set_model takes it
+    sd = {"data_in_mean": f64(XMU), "data_in_std": f64(XSTD), "data_target_mean": f64(YMU), "data_target_std": f64(YSTD)}
     for i, layers in enumerate(mods):
         sd[f"net{i}"] = {f"net.linear_layer_{k}.{n}": torch.from_numpy(a)
                          for k, (W, b) in enumerate(layers) for n, a in (("weight", W), ("bias", b))}

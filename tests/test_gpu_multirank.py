@@ -35,7 +35,7 @@ def _setup(m, t, ym, dt, comm=None, schemes=None):
 
 
 def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True, renumber=None, overlap=False,
-         schemes=None, perturb=False, env=None):
+         schemes=None, perturb=False, env=None, timers=True):
     from dfmi.mesh import hex_box, global_cell_ids
     from dfmi.mech import read_thermo_table, read_yaml_mechanism
     from dfmi import case
@@ -87,12 +87,20 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
             c = _setup(m, t, ym, dt, comm={"hub": hub, "nranks": nr, "rank": r}, schemes=schemes)
             case.init_state(c, m, t.S, f["T"][g], f["p"][g], f["U"][:, g], f["Y"][:, g])
             c.call("pre_time_step")
-            c.kernel_timer("k_bcg_eo")   # whether the even-odd BiCGStab ran (the ranks' colourings agree)
+            if timers:
+                c.kernel_timer("k_bcg_eo")   # whether the even-odd BiCGStab ran (the ranks' colourings agree)
+            else:
+                c.comm_timer(True)           # no kernel timers: the time step keeps its side stream
             for _ in range(n_steps):
                 c.time_step(2)
             o = {n: c.get_field(n, (m.n_cells,)) for n in ("T", "p", "rho", "he")}
-            o["eo"] = c.kernel_time("k_bcg_eo")[1]
-            c.kernel_timer("")
+            if timers:
+                o["eo"] = c.kernel_time("k_bcg_eo")[1]
+                c.kernel_timer("")
+            else:
+                o["comm"] = c.comm_report()
+                o["proc_faces"] = int(m.proc_rows_cols()[0].size)
+                c.comm_timer(False)
             o["U"] = c.get_field("U", (3, m.n_cells))
             o["Y"] = c.get_field("Y", (t.S, m.n_cells))
             o["stats"] = {e: c.solver_stats(e) for e in ("U", "Y", "E", "p")}
@@ -139,7 +147,10 @@ def _run(nx, ny, nz, decomp, n_steps=1, gradings=(1.0, 1.3, 1.0), periodic=True,
     for r in range(1, nr):
         assert out[r]["stats"]["p"][0] == out[0]["stats"]["p"][0]
     glob["p_iters"] = out[0]["stats"]["p"][0]
-    glob["eo_launches"] = [out[r]["eo"] for r in range(nr)]
+    glob["eo_launches"] = [out[r].get("eo") for r in range(nr)]
+    glob["comm"] = [out[r].get("comm") for r in range(nr)]
+    glob["proc_faces"] = [out[r].get("proc_faces") for r in range(nr)]
+    glob["stats"] = [out[r]["stats"] for r in range(nr)]
     if orc is not None:
         ref["oracle"] = {n: orc[n] for n in ("T", "p", "rho", "he", "U", "Y")}
     return ref, glob
@@ -350,3 +361,25 @@ def test_halo_coupled_level0_needs_fewer_pcg_iterations():
     for n in ("T", "p", "rho", "he", "U", "Y"):
         assert rel_err(hal[n], ref[n]) < 1e-9, n
         assert rel_err(bj[n], ref[n]) < 1e-9, n
+
+
+def test_decomposed_side_stream_one_colour_halos_single_reduction_pcg():
+    """Round 6's multi-rank step: the side stream (chemistry, YEqn front, EEqn scheme terms) runs at N > 1 with
+    its field halos on the halo's second channel (reported as "... @side" points); the even-odd BiCGStab
+    exchanges carry one colour's faces (fewer bytes per call than a full exchange of the same vectors); the PCG
+    takes ONE all-gather per iteration (single-reduction form). Against the oracle's exact solves to 1e-9."""
+    ref, glob = _run(12, 8, 8, (2, 2, 2), timers=False)
+    for n in ("T", "p", "rho", "he", "U", "Y"):
+        e = rel_err(glob[n], ref["oracle"][n])
+        assert e < 1e-9, ("oracle", n, e)
+    for r, comm in enumerate(glob["comm"]):
+        side = [k for k in comm if k.endswith("@side")]
+        assert any(k.startswith("fields sumYDiffError hDiffCorrFlux") for k in side), sorted(comm)
+        assert not any(k.startswith("bicgstab") or k.startswith("pcg") for k in side), side
+        H = glob["proc_faces"][r]
+        e = comm["bicgstab E"]
+        assert e["bytes"] / e["calls"] < 0.75 * 8.0 * H, (e, H)   # mostly half-face (one-colour) messages
+        # PCG: per iteration one all-gather (+ the setup's); the standard form takes two
+        its = glob["stats"][r]["p"][0]
+        ag = comm.get("allgather pcg p", {}).get("calls", 0)
+        assert 0 < ag <= 3 * (its + 3), (ag, its)

@@ -376,10 +376,11 @@ def test_small_solves_match_batched_path(prec, monkeypatch):
     from dfmi import case, lib
     monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.precision", 64 if prec == "f64" else 32)
     monkeypatch.setitem(lib.DEFAULT_OPTIONS, "amg.coarsest_size", 64)      # a multi-level hierarchy on this mesh
-    ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
     res = {}
     for small in ("1", "0"):
-        ctx.set_option("solver.small", int(small))
+        # solver.small decides the solver rows' layout when they are built (the first solve): one context per arm
+        monkeypatch.setitem(lib.DEFAULT_OPTIONS, "solver.small", int(small))
+        ctx, m, t, st, pt, inert, dt = _case(nx=16, ny=12, nz=8, mech="burke9")
         out = {}
         for tight in (True, False):
             case.push_state(ctx, st)
