@@ -11,6 +11,13 @@
 //
 // Compiled with -ffp-contract=off: the arithmetic sequence is the oracle's, op for op.
 #include "dfmi_ctx.h"
+// Occupancy caps of the kernels that share the GPU with the side stream's chemistry: at least n
+// waves' worth of registers per SIMD. -DDFMI_NO_CAPS builds the uncapped A/B variant (scripts/pmc_caps_ab.sh).
+#ifdef DFMI_NO_CAPS
+#define DFMI_WAVES(n)
+#else
+#define DFMI_WAVES(n) __attribute__((amdgpu_waves_per_eu(n, 8)))
+#endif
 #include <cstdlib>
 
 namespace dfmi {
@@ -644,7 +651,7 @@ __device__ __forceinline__ void dev2T(double sc, const double* v, double* o) {
 }
 
 template <int WT>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
+__global__ void __launch_bounds__(TPB) DFMI_WAVES(6) k_u_grad(MeshView m, const int8_t* __restrict__ ty, const double* __restrict__ U,
                          const double* __restrict__ bU, const double* __restrict__ mu, const double* __restrict__ bmu,
                          double* __restrict__ T, double* __restrict__ bT, double* __restrict__ gout) {
   const int c = cell_of(m, xcd_block() * blockDim.x + threadIdx.x);
@@ -709,8 +716,11 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6, 8))
 
 // UEqn matrix (UEqn.H:3-20): ddt(rho,U) + div(phi,U) - laplacian(mu,U) - div(mu dev2 T(gradU)),
 // plus source_solve = source - grad(p) and rAU (dfUEqn.cu:721-738).
-template <int WT>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
+// SPLIT (option fv.uasm_split): the explicit tensor divergence in a second walk over the cell's faces (the cell's
+// and the neighbour's nine tensor components are then never live beside the matrix accumulators) -- every
+// accumulator's sum over the faces in the same order, bitwise the single walk.
+template <int WT, bool SPLIT = false>
+__global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
     const double* __restrict__ rho, const double* __restrict__ rho_old, const double* __restrict__ U_old,
     const double* __restrict__ bU, const double* __restrict__ phi, const double* __restrict__ bphi,
     const double* __restrict__ mu, const double* __restrict__ bmu, const double* __restrict__ p,
@@ -723,21 +733,10 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
   double dT[3] = {0.0, 0.0, 0.0}, gp[3] = {0.0, 0.0, 0.0};
-  // the cell's own tensor, mu and p stay in registers; each face gathers only the other cell's values
-  // (interp_f keeps its owner-first argument order, so the arithmetic is unchanged)
-  double Tc[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
   const double muc = mu[c], pcc = p[c];
-  each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const double w = m.w[f], ph = phi[f];
-    const double L1 = -(wU ? wU[f] : w) * ph;   // div(phi,U): linear, or limitedLinearV weights
-    const double U1 = L1 + ph;
-    const double mun = mu[o2];
-    const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
-    if (own) { d1 -= L1; lower[f] = L1 + (-UL); upper[f] = U1 + (-UL); }
-    else d1 -= U1;
-    dL -= UL;
+  // the tensor divergence of one face (the cell's own tensor in Tc; the other cell's gathered per face;
+  // interp_f keeps its owner-first argument order, so the arithmetic is unchanged)
+  auto tensor_face = [&](const double (&Tc)[9], int f, int o2, bool own, double w) {
     const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     double Tn[9];
 #pragma unroll
@@ -748,11 +747,38 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))
       const double v = sf0 * fi(0 + j) + sf1 * fi(3 + j) + sf2 * fi(6 + j);
       if (own) dT[j] += v; else dT[j] -= v;
     }
+  };
+  auto matrix_face = [&](int f, int o2, bool own, double w) {
+    const double ph = phi[f];
+    const double L1 = -(wU ? wU[f] : w) * ph;   // div(phi,U): linear, or limitedLinearV weights
+    const double U1 = L1 + ph;
+    const double mun = mu[o2];
+    const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
+    if (own) { d1 -= L1; lower[f] = L1 + (-UL); upper[f] = U1 + (-UL); }
+    else d1 -= U1;
+    dL -= UL;
     const double pn = p[o2];
     const double pf = own ? interp_f(w, pcc, pn) : interp_f(w, pn, pcc);
+    const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     const double g0 = sf0 * pf, g1 = sf1 * pf, g2 = sf2 * pf;
     if (own) { gp[0] += g0; gp[1] += g1; gp[2] += g2; } else { gp[0] -= g0; gp[1] -= g1; gp[2] -= g2; }
-  });
+  };
+  if constexpr (SPLIT) {
+    each_face<WT>(m, c, [&](int f, int o2, bool own) { matrix_face(f, o2, own, m.w[f]); });
+    double Tc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
+    each_face<WT>(m, c, [&](int f, int o2, bool own) { tensor_face(Tc, f, o2, own, m.w[f]); });
+  } else {
+    double Tc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
+    each_face<WT>(m, c, [&](int f, int o2, bool own) {
+      const double w = m.w[f];
+      matrix_face(f, o2, own, w);
+      tensor_face(Tc, f, o2, own, w);
+    });
+  }
   // boundary contributions: explicit tensor divergence and the pressure gradient
   each_slot(m, tyU, c, [&](int b, int t) {
     double tt[9];
@@ -1389,8 +1415,11 @@ __global__ void __launch_bounds__(TPB) k_y_assemble(MeshView m, const int8_t* __
 // faces, coupled slots), dS = diag + sum internalCoeffs and rhs = source + non-coupled
 // boundaryCoeffs in slot order -- bitwise what k_ell_build makes from the LDU arrays, without writing
 // and re-reading lower/upper/internalCoeffs/boundaryCoeffs.
+// (the species in two groups, each group its own walk over the cell's faces and slots, bitwise the same: 94 VGPRs and
+// no spill under the side-stream cap, but 660 against 590-610 us per launch and 13.88-13.94 against 13.70-13.76 ms
+// per step, round 6 -- not kept)
 template <int S, int WT>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
+__global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m, const int8_t* __restrict__ tyY, int inert,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ RR, const double* __restrict__ rho,
     const double* __restrict__ rho_old, const double* __restrict__ phi, const double* __restrict__ bphi,
@@ -1401,66 +1430,78 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(5, 8))
   if (c >= m.C) return;
   const int pc = m.eopos ? m.eopos[c] : c;   // the solver row of c (even-odd layout)
   const long C = m.C, B = m.B;
-  double d1 = 0.0, d2 = 0.0;
-  double dL[S], rc[S];
+  auto group = [&](const int g0) {
+    constexpr int G = S;
+    double d1 = 0.0, d2 = 0.0;
+    double dL[G], rc[G];
 #pragma unroll
-  for (int s = 0; s < S; ++s) { dL[s] = 0.0; rc[s] = rhoD[s * C + c]; }
-  int k = 0;
-  each_face<WT>(m, c, [&](int f, int o2, bool own) {
-    const double ph = phi[f], pu = phiUc[f];
-    const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
-    const double L1 = -wu * ph, U1 = L1 + ph;
-    const double L2 = -wu * pu, U2 = L2 + pu;
-    if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
-    const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
-    const double Ls = L1 + L2, Us = U1 + U2;
+    for (int j = 0; j < G; ++j) { const int s = g0 + j; dL[j] = 0.0; rc[j] = s < S ? rhoD[s * C + c] : 0.0; }
+    int k = 0;
+    each_face<WT>(m, c, [&](int f, int o2, bool own) {
+      const double ph = phi[f], pu = phiUc[f];
+      const double wu = wY ? wY[f] : (ph >= 0 ? 1.0 : 0.0);
+      const double L1 = -wu * ph, U1 = L1 + ph;
+      const double L2 = -wu * pu, U2 = L2 + pu;
+      if (own) { d1 -= L1; d2 -= L2; } else { d1 -= U1; d2 -= U2; }
+      const double w = m.w[f], dcf = m.dc[f], ms = m.magSf[f];
+      const double Ls = L1 + L2, Us = U1 + U2;
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
+      for (int j = 0; j < G; ++j) {
+        const int s = g0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const double rn = rhoD[s * C + o2];
+        const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
+        dL[j] -= UL;
+        val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
+      }
+      ++k;
+    });
+    const double vol = m.V[c];
+    const double dd = m.rdt * rho[c] * vol + (d1 + d2);
+    const double ro = m.rdt * rho_old[c];
+    double dg[G], sr[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int s = g0 + j;
+      if (s >= S) break;
+      dg[j] = dd - dL[j];
+      sr[j] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
+    }
+    each_slot(m, tyY, c, [&](int b, int t) {
+      const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
+      const bool cp = bc_coupled(t);
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int s = g0 + j;
+        if (s >= S) break;
+        if (s == inert) continue;
+        const int ss = s < inert ? s : s - 1;
+        const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
+        const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
+        const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
+        const double pG = gam * m.bmagSf[b];
+        const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
+        const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
+        dg[j] += icv;
+        if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
+        else sr[j] += bcv;
+      }
+      if (cp) ++k;
+    });
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int s = g0 + j;
+      if (s >= S) break;
       if (s == inert) continue;
       const int ss = s < inert ? s : s - 1;
-      const double rn = rhoD[s * C + o2];
-      const double UL = dcf * ((own ? interp_f(w, rc[s], rn) : interp_f(w, rn, rc[s])) * ms);
-      dL[s] -= UL;
-      val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
+      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
+      dS[ss * Ce + pc] = dg[j];
+      rhs[ss * Ce + pc] = sr[j];
     }
-    ++k;
-  });
-  const double vol = m.V[c];
-  const double dd = m.rdt * rho[c] * vol + (d1 + d2);
-  const double ro = m.rdt * rho_old[c];
-  double dg[S], sr[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    dg[s] = dd - dL[s];
-    sr[s] = ro * Y[s * C + c] * vol + vol * RR[s * C + c];
-  }
-  each_slot(m, tyY, c, [&](int b, int t) {
-    const double wu = bwY ? bwY[b] : (bphi[b] >= 0 ? 1.0 : 0.0);
-    const bool cp = bc_coupled(t);
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      if (s == inert) continue;
-      const int ss = s < inert ? s : s - 1;
-      const BCoef qc = bcoef_f(t, bY[s * B + b], wu, m.bdc[b], mxY, b, B, s);
-      const BCoef ql = bcoef_f(t, bY[s * B + b], m.bw[b], m.bdc[b], mxY, b, B, s);
-      const double gam = cp ? interp_b(m.bw[b], rhoD[s * C + c], nbrv(m, rhoD + s * C, brhoD + s * B, b)) : brhoD[s * B + b];
-      const double pG = gam * m.bmagSf[b];
-      const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
-      const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
-      dg[s] += icv;
-      if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
-      else sr[s] += bcv;
-    }
-    if (cp) ++k;
-  });
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    if (s == inert) continue;
-    const int ss = s < inert ? s : s - 1;
-    for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
-    dS[ss * Ce + pc] = dg[s];
-    rhs[ss * Ce + pc] = sr[s];
-  }
+  };
+  group(0);
 }
 
 
@@ -1585,7 +1626,7 @@ __device__ __forceinline__ void y_chunk_bgrad(const MeshView& m, int t, int b, i
 // (2 waves per SIMD: 16k cells per XCD x 53 species x 3 arrays = 20 MB against its 4 MB), so each neighbour
 // value is fetched again by each of the cells that read it; a range of species per launch shrinks that set.
 template <int CH, int WT>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) k_y_prep_gen(MeshView m, int s_lo, int s_hi, int pass,
+__global__ void __launch_bounds__(TPB) DFMI_WAVES(4) k_y_prep_gen(MeshView m, int s_lo, int s_hi, int pass,
     const int8_t* __restrict__ tyY,
     const double* __restrict__ Y, const double* __restrict__ bY, const double* __restrict__ rhoD,
     const double* __restrict__ brhoD, const double* __restrict__ hai, const double* __restrict__ bhai,
@@ -2050,10 +2091,16 @@ void u_assemble(Ctx& x) {
     LAUNCH(k_llv_w_face, x.Fs, x.view(), twoByk, x.f("phi"), x.f("U"), gout, w);
     LAUNCH(k_llv_w_slot, x.B, x.view(), x.st("U"), twoByk, x.f("boundary_phi"), x.f("U"), gout, bw);
   }
-  LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
-         x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
-         x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
-         A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
+  if (face_hex(x) && x.on("fv.uasm_split"))   // the tensor divergence in its own face walk (option fv.uasm_split)
+    LAUNCH_AS("k_u_assemble", (k_u_assemble<-1, true>), x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"),
+              x.f("U_old"), x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
+              x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
+              A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
+  else
+    LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
+             x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
+             x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
+             A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
   k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
   halo_fields(x, {"rAU"});
 }

@@ -50,7 +50,8 @@ int dfmi_set_constant_values(dfmi_ctx* ctx, int num_cells, int num_total_cells, 
 int dfmi_set_cyclic_info(dfmi_ctx* ctx, const int* cyclic_neighbor);
 /* dfMatrixDataBase::setCommInfo + ncclInit (dfMatrixDataBase.cu:92-101, dfNcclBase.cu:23-65):
  * nccl_unique_id is the 128-byte RCCL id (rank 0 creates it, the caller broadcasts it),
- * neighb_proc_no[num_patches] the peer rank of each processor patch (-1 otherwise) */
+ * neighb_proc_no[num_patches] the peer rank of each processor patch (-1 otherwise). Collective: every rank calls
+ * it; it also splits a second communicator (ncclCommSplit) for the time step's side stream. */
 int dfmi_set_comm_info(dfmi_ctx* ctx, const void* nccl_unique_id, int nranks, int rank,
                        const int* neighb_proc_no);
 /* rank-0 helper: create a fresh RCCL unique id (128 bytes) */

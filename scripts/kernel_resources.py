@@ -7,7 +7,7 @@ import sys
 import tempfile
 
 B = "/opt/rocm/lib/llvm/bin"
-obj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "deepflame-dev_amd", "csrc", "build", sys.argv[1])
+obj = sys.argv[1] if os.path.sep in sys.argv[1] else os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "deepflame-dev_amd", "csrc", "build", sys.argv[1])
 pat = re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
 with tempfile.TemporaryDirectory() as d:
     fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "dev.co")
