@@ -262,7 +262,6 @@ inline const OptDef* option_defs(int& n) {
     {"fv.csr_walk", 0},               // assembly faces walked from the CSR lists instead of the gather rows
     {"fv.species_generic", 0},        // the species-chunked YEqn kernels at any species count (S > 16 always)
     {"fv.yprep_brick", 1},            // k_y_prep staging 16x4x4 bricks in LDS (hex walk)
-    {"fv.uasm_split", 0},             // hex walk: k_u_assemble walks the faces twice (matrix, then tensor divergence)
     {"chem.method", 0},               // 0: ROS3 Rosenbrock, 1: linearly-implicit Euler extrapolation
     {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
     {"chem.binning", 2},              // cells launched in cost-binned order: 1 over the mesh, 2 inside 4096-cell tiles

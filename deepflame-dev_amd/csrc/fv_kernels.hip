@@ -18,6 +18,14 @@
 #else
 #define DFMI_WAVES(n) __attribute__((amdgpu_waves_per_eu(n, 8)))
 #endif
+// Stores of the assembly kernels' outputs (matrix rows, LDU coefficients): -DDFMI_ST_DROP issues them as sc1
+// stores, which write through and drop the line from the XCD's L2 (MI355X_MICROARCH.md: plain / nt stores keep
+// it), leaving the L2 to the neighbour planes the face gathers re-read. A/B build (scripts/ab_arms.sh).
+#ifdef DFMI_ST_DROP
+__device__ __forceinline__ void st_out(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#else
+__device__ __forceinline__ void st_out(double* p, double v) { *p = v; }
+#endif
 #include <cstdlib>
 
 namespace dfmi {
@@ -716,10 +724,7 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(6) k_u_grad(MeshView m, const 
 
 // UEqn matrix (UEqn.H:3-20): ddt(rho,U) + div(phi,U) - laplacian(mu,U) - div(mu dev2 T(gradU)),
 // plus source_solve = source - grad(p) and rAU (dfUEqn.cu:721-738).
-// SPLIT (option fv.uasm_split): the explicit tensor divergence in a second walk over the cell's faces (the cell's
-// and the neighbour's nine tensor components are then never live beside the matrix accumulators) -- every
-// accumulator's sum over the faces in the same order, bitwise the single walk.
-template <int WT, bool SPLIT = false>
+template <int WT>
 __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, const int8_t* __restrict__ tyU, const int8_t* __restrict__ tyP,
     const double* __restrict__ rho, const double* __restrict__ rho_old, const double* __restrict__ U_old,
     const double* __restrict__ bU, const double* __restrict__ phi, const double* __restrict__ bphi,
@@ -733,10 +738,21 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, co
   const long C = m.C, F = m.F, B = m.B;
   double d1 = 0.0, dL = 0.0;
   double dT[3] = {0.0, 0.0, 0.0}, gp[3] = {0.0, 0.0, 0.0};
+  // the cell's own tensor, mu and p stay in registers; each face gathers only the other cell's values
+  // (interp_f keeps its owner-first argument order, so the arithmetic is unchanged)
+  double Tc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
   const double muc = mu[c], pcc = p[c];
-  // the tensor divergence of one face (the cell's own tensor in Tc; the other cell's gathered per face;
-  // interp_f keeps its owner-first argument order, so the arithmetic is unchanged)
-  auto tensor_face = [&](const double (&Tc)[9], int f, int o2, bool own, double w) {
+  each_face<WT>(m, c, [&](int f, int o2, bool own) {
+    const double w = m.w[f], ph = phi[f];
+    const double L1 = -(wU ? wU[f] : w) * ph;   // div(phi,U): linear, or limitedLinearV weights
+    const double U1 = L1 + ph;
+    const double mun = mu[o2];
+    const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
+    if (own) { d1 -= L1; st_out(&lower[f], L1 + (-UL)); st_out(&upper[f], U1 + (-UL)); }
+    else d1 -= U1;
+    dL -= UL;
     const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     double Tn[9];
 #pragma unroll
@@ -747,38 +763,11 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, co
       const double v = sf0 * fi(0 + j) + sf1 * fi(3 + j) + sf2 * fi(6 + j);
       if (own) dT[j] += v; else dT[j] -= v;
     }
-  };
-  auto matrix_face = [&](int f, int o2, bool own, double w) {
-    const double ph = phi[f];
-    const double L1 = -(wU ? wU[f] : w) * ph;   // div(phi,U): linear, or limitedLinearV weights
-    const double U1 = L1 + ph;
-    const double mun = mu[o2];
-    const double UL = m.dc[f] * ((own ? interp_f(w, muc, mun) : interp_f(w, mun, muc)) * m.magSf[f]);
-    if (own) { d1 -= L1; lower[f] = L1 + (-UL); upper[f] = U1 + (-UL); }
-    else d1 -= U1;
-    dL -= UL;
     const double pn = p[o2];
     const double pf = own ? interp_f(w, pcc, pn) : interp_f(w, pn, pcc);
-    const double sf0 = m.Sf[f], sf1 = m.Sf[F + f], sf2 = m.Sf[2 * F + f];
     const double g0 = sf0 * pf, g1 = sf1 * pf, g2 = sf2 * pf;
     if (own) { gp[0] += g0; gp[1] += g1; gp[2] += g2; } else { gp[0] -= g0; gp[1] -= g1; gp[2] -= g2; }
-  };
-  if constexpr (SPLIT) {
-    each_face<WT>(m, c, [&](int f, int o2, bool own) { matrix_face(f, o2, own, m.w[f]); });
-    double Tc[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
-    each_face<WT>(m, c, [&](int f, int o2, bool own) { tensor_face(Tc, f, o2, own, m.w[f]); });
-  } else {
-    double Tc[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) Tc[k] = T[k * C + c];
-    each_face<WT>(m, c, [&](int f, int o2, bool own) {
-      const double w = m.w[f];
-      matrix_face(f, o2, own, w);
-      tensor_face(Tc, f, o2, own, w);
-    });
-  }
+  });
   // boundary contributions: explicit tensor divergence and the pressure gradient
   each_slot(m, tyU, c, [&](int b, int t) {
     double tt[9];
@@ -800,12 +789,12 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, co
   });
   const double vol = m.V[c];
   const double dg = (m.rdt * rho[c] * vol + d1) + (-dL);
-  diag[c] = dg;
+  st_out(&diag[c], dg);
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const double s = m.rdt * rho_old[c] * U_old[k * C + c] * vol + dT[k];
-    src[k * C + c] = s;
-    srcs[k * C + c] = s - gp[k];
+    st_out(&src[k * C + c], s);
+    st_out(&srcs[k * C + c], s - gp[k]);
   }
   double r = dg;
   each_slot(m, tyU, c, [&](int b, int t) {
@@ -817,12 +806,12 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_u_assemble(MeshView m, co
       const BCoef q = bcoef_f(t, bU[k * B + b], m.bw[b], m.bdc[b], mxU, b, B, k);
       const BCoef qc = bwU ? bcoef_f(t, bU[k * B + b], bwU[b], m.bdc[b], mxU, b, B, k) : q;   // convection weights
       icv[k] = bphi[b] * qc.vic + (-(pG * q.gic));
-      ic[k * B + b] = icv[k];
+      st_out(&ic[k * B + b], icv[k]);
       bc[k * B + b] = -bphi[b] * qc.vbc + (-(-pG * q.gbc));
     }
     r += (icv[0] + icv[1] + icv[2]) / 3;
   });
-  rAU[c] = 1 / (r / vol);
+  st_out(&rAU[c], 1 / (r / vol));
 }
 
 // K = 0.5*magSqr(U) on cells (boundary K is done per slot below)
@@ -1454,7 +1443,7 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
         const double rn = rhoD[s * C + o2];
         const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
         dL[j] -= UL;
-        val[((long)ss * W + k) * C + pc] = own ? Us - UL : Ls - UL;
+        st_out(&val[((long)ss * W + k) * C + pc], own ? Us - UL : Ls - UL);
       }
       ++k;
     });
@@ -1485,7 +1474,7 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
         const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
         const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
         dg[j] += icv;
-        if (cp) val[((long)ss * W + k) * C + pc] = -bcv;
+        if (cp) st_out(&val[((long)ss * W + k) * C + pc], -bcv);
         else sr[j] += bcv;
       }
       if (cp) ++k;
@@ -1496,9 +1485,9 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
       if (s >= S) break;
       if (s == inert) continue;
       const int ss = s < inert ? s : s - 1;
-      for (int kk = k; kk < W; ++kk) val[((long)ss * W + kk) * C + pc] = 0.0;
-      dS[ss * Ce + pc] = dg[j];
-      rhs[ss * Ce + pc] = sr[j];
+      for (int kk = k; kk < W; ++kk) st_out(&val[((long)ss * W + kk) * C + pc], 0.0);
+      st_out(&dS[ss * Ce + pc], dg[j]);
+      st_out(&rhs[ss * Ce + pc], sr[j]);
     }
   };
   group(0);
@@ -2091,16 +2080,10 @@ void u_assemble(Ctx& x) {
     LAUNCH(k_llv_w_face, x.Fs, x.view(), twoByk, x.f("phi"), x.f("U"), gout, w);
     LAUNCH(k_llv_w_slot, x.B, x.view(), x.st("U"), twoByk, x.f("boundary_phi"), x.f("U"), gout, bw);
   }
-  if (face_hex(x) && x.on("fv.uasm_split"))   // the tensor divergence in its own face walk (option fv.uasm_split)
-    LAUNCH_AS("k_u_assemble", (k_u_assemble<-1, true>), x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"),
-              x.f("U_old"), x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
-              x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
-              A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
-  else
-    LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
-             x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
-             x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
-             A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
+  LAUNCH_W(k_u_assemble, x.C, x.view(), x.st("U"), x.st("p"), x.f("rho"), x.f("rho_old"), x.f("U_old"),
+           x.f("boundary_U"), x.f("phi"), x.f("boundary_phi"), x.f("mu"), x.f("boundary_mu"), x.f("p"),
+           x.f("boundary_p"), x.f("tauU"), x.f("boundary_tauU"), A.lower.p, A.upper.p, A.diag.p, A.source.p,
+           A.source_solve.p, A.ic.p, A.bc.p, x.f("rAU"), mixbc(x, "U"), x.sch_w(6), x.sch_w(7));
   k_bc_correct(x, "extrapolated", x.f("rAU"), x.f("boundary_rAU"), 1);
   halo_fields(x, {"rAU"});
 }

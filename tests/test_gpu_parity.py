@@ -106,13 +106,9 @@ def _oracle(m, t, st, pt, inert, dt):
 # (BASELINE config 4) -- every variant bitwise against the same oracle
 @pytest.fixture(scope="module", params=["es80", "burke9", "walls", "distorted", "burke9-generic", "walls-generic",
                                         "gri53", "gri53-walls", "burke9-morton", "burke9-bricks", "distorted-rcm", "walls-csr",
-                                        "mixed", "mixed-generic", "walls-trav", "walls-split", "mixed-split"])
+                                        "mixed", "mixed-generic", "walls-trav"])
 def periodic(request):
     from dfmi import lib
-    if request.param.endswith("-split"):   # k_u_assemble's split face walk (fv.uasm_split)
-        for k in ("fv.uasm_split",):
-            lib.DEFAULT_OPTIONS[k] = 1
-            request.addfinalizer(lambda k=k: lib.DEFAULT_OPTIONS.pop(k, None))
     generic = request.param.endswith("-generic")
     if generic:
         lib.DEFAULT_OPTIONS["fv.species_generic"] = 1
@@ -121,7 +117,7 @@ def periodic(request):
         lib.DEFAULT_OPTIONS["fv.csr_walk"] = 1
         request.addfinalizer(lambda: lib.DEFAULT_OPTIONS.pop("fv.csr_walk", None))
     traversal = request.param.endswith("-trav")
-    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "").replace("-split", "")
+    param = request.param.replace("-generic", "").replace("-csr", "").replace("-trav", "")
     renumber = None
     for meth in ("morton", "bricks", "rcm"):
         if param.endswith("-" + meth):
