@@ -246,7 +246,7 @@ bool step_overlap(const Ctx& x) {
 void do_U_Y_fork(Ctx& x) {
   if (!x.stream2) {
     DFMI_HIP(hipStreamCreateWithFlags(&x.stream2, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e, &x.ev_cw})
+    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e, &x.ev_cw, &x.ev_th, &x.ev_tr})
       DFMI_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
@@ -299,6 +299,25 @@ void do_U_Y_E(Ctx& x) {
   DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_e, 0));
   e_assemble_back(x);
   do_E_back(x);
+}
+// correctThermo split in two: the state the pressure corrector reads (T, he, psi, rho) on the main stream, and the
+// transport (mu, alpha, rhoD, hai) -- read by nothing before the next time step's equations -- on the side stream,
+// where it runs beside the p solves (their coarse AMG levels leave most CUs idle). Its inputs (T, Y) are not
+// written again in the step; the main stream waits for it at the end of the step. Option thermo.split (0: fused).
+bool do_thermo_split(Ctx& x) {
+  if (!step_overlap(x) || !x.on("thermo.split") || species_generic(x) || !x.stream2) {
+    thermo_correct(x, false);
+    return false;
+  }
+  thermo_correct(x, false, 1);
+  DFMI_HIP(hipEventRecord(x.ev_th, x.stream));
+  {
+    OnStream _os(x, x.stream2);
+    DFMI_HIP(hipStreamWaitEvent(x.stream2, x.ev_th, 0));
+    thermo_correct(x, false, 2);
+    DFMI_HIP(hipEventRecord(x.ev_tr, x.stream2));
+  }
+  return true;
 }
 void do_p(Ctx& x) {
   p_assemble(x);
@@ -680,7 +699,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     rho_process(x, false);          // rhoEqn (first PIMPLE iteration)
     do_U_Y_E(x);                    // UEqn, YEqn, EEqn (one rank: the chemistry and YEqn assembly beside the
                                     // UEqn, the EEqn assembly beside the Y solve)
-    thermo_correct(x, false);       // correctThermo
+    const bool tsplit = do_thermo_split(x);   // correctThermo (the transport half beside the p solves)
     for (int i = 0; i < n_corr; ++i) {   // pEqn_GPU.H
       thermo_rho_from_psi(x);
       thermo_psip0(x);
@@ -693,6 +712,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
     }
     thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
     if (x.chem.mode == 1) chem_check(x);   // the p solves' polls have already passed the chemistry
+    if (tsplit) DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_tr, 0));
     if (x.steptimer.on) x.steptimer.mark(x.stream);
     treset.done = true;
   });

@@ -577,6 +577,7 @@ __global__ void __launch_bounds__(LANES) k_chem(long n, const int* __restrict__ 
 #define DFMI_HD __device__   // the generated kinetics are plain C++; here they run on the device
 // between the reactions of the fused rates + Jacobian pass: nothing is scheduled across, so one reaction's
 // temporaries die before the next one's loads are issued (the register peak is J plus one reaction)
+// (the scheduler left free across reactions measured 13.90 -> 14.11 ms per step, 3 rounds each in one call, round 6)
 #define DFMI_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 // 1 / x for the generated kinetics (fall-off factors, LU pivots): the hardware reciprocal estimate refined by two
 // Newton steps instead of the ~10-instruction IEEE division sequence (x is a nonzero normal number there)

@@ -266,6 +266,8 @@ inline const OptDef* option_defs(int& n) {
     {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
     {"chem.binning", 2},              // cells launched in cost-binned order: 1 over the mesh, 2 inside 4096-cell tiles
     {"dnn.tuned_gemm", 1},            // DF-ODENet layers by the shape-tuned kernels (0: k_mlp_gemm for every layer)
+    {"thermo.split", 0},              // time step: the transport half of correctThermo on the side stream beside the p solve
+                                      // (13.89 -> 13.92 ms per step, 3 rounds each in one call, round 6: not the default)
     {"halo.overlap", 0},              // several ranks: solver halo exchanges on a comm stream while the interior rows run
                                       // (read per solve; DFMI_HALO_OVERLAP sets the default when the communicator is set)
   };
@@ -375,7 +377,8 @@ struct Ctx {
   SolverWs& sws() { return ws_is_y ? ws_y : ws; }
   // side stream of the time step (dfmi_time_step: chemistry + YEqn preparation beside the UEqn) and its events
   hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr, ev_cw = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr, ev_cw = nullptr, ev_th = nullptr,
+            ev_tr = nullptr;
   // final solver state of the last solve of each equation, copied asynchronously at the end of the
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };
@@ -503,7 +506,9 @@ void thermo_correct_psip_rho(Ctx& x);
 // thermo.hip
 void thermo_upload(Ctx& x);
 std::vector<double> heat_of_formation_per_mass(int S, const double* W, const double* nasa);   // hc_i (Qdot weights)
-void thermo_correct(Ctx& x, bool from_T);
+// part 0: the whole update; 1: the state (T, he, psi, rho); 2: the transport (mu, alpha, rhoD, hai) at the
+// current T -- the time step runs part 2 on the side stream beside the pressure corrector
+void thermo_correct(Ctx& x, bool from_T, int part = 0);
 // boundary_heGradient on gradientEnergy slots of he (0 elsewhere)
 void thermo_energy_gradient(Ctx& x);
 // linsolve.hip
@@ -565,7 +570,7 @@ struct CommTag {
   CommTag(Ctx& c, const std::string& t) : x(c), set(c.comm.on) { if (set) { prev = x.comm.tag; x.comm.tag = t; } }
   ~CommTag() { if (set) x.comm.tag = prev; }
 };
-inline void halo_fields(Ctx& x, std::initializer_list<const char*> names) {
+inline void halo_fields(Ctx& x, const std::vector<const char*>& names) {
   if (!halo_active(x)) return;
   std::string tag;
   if (x.comm.on) {

@@ -18,14 +18,12 @@
 #else
 #define DFMI_WAVES(n) __attribute__((amdgpu_waves_per_eu(n, 8)))
 #endif
-// Stores of the assembly kernels' outputs (matrix rows, LDU coefficients): -DDFMI_ST_DROP issues them as sc1
-// stores, which write through and drop the line from the XCD's L2 (MI355X_MICROARCH.md: plain / nt stores keep
-// it), leaving the L2 to the neighbour planes the face gathers re-read. A/B build (scripts/ab_arms.sh).
-#ifdef DFMI_ST_DROP
-__device__ __forceinline__ void st_out(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-#else
+// Stores of the YEqn assembly's ELL rows go out as sc1 stores (st_drop), which write through and drop the line from
+// the XCD's L2 (MI355X_MICROARCH.md: plain / nt stores keep it), leaving the L2 to the neighbour planes the face
+// gathers re-read: k_y_assemble_ell 661 -> 625 us, step 13.90 -> 13.86 ms (3 rounds each in one call, round 6,
+// gpurun_out r06d). The same stores in k_u_assemble measured slower (335 -> 359 us) and stay plain (st_out).
+__device__ __forceinline__ void st_drop(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ void st_out(double* p, double v) { *p = v; }
-#endif
 #include <cstdlib>
 
 namespace dfmi {
@@ -1443,7 +1441,7 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
         const double rn = rhoD[s * C + o2];
         const double UL = dcf * ((own ? interp_f(w, rc[j], rn) : interp_f(w, rn, rc[j])) * ms);
         dL[j] -= UL;
-        st_out(&val[((long)ss * W + k) * C + pc], own ? Us - UL : Ls - UL);
+        st_drop(&val[((long)ss * W + k) * C + pc], own ? Us - UL : Ls - UL);
       }
       ++k;
     });
@@ -1474,7 +1472,7 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
         const double icv = (bphi[b] * qc.vic + bphiUc[b] * qc.vic) - pG * ql.gic;
         const double bcv = (-bphi[b] * qc.vbc + -bphiUc[b] * qc.vbc) - (-pG * ql.gbc);
         dg[j] += icv;
-        if (cp) st_out(&val[((long)ss * W + k) * C + pc], -bcv);
+        if (cp) st_drop(&val[((long)ss * W + k) * C + pc], -bcv);
         else sr[j] += bcv;
       }
       if (cp) ++k;
@@ -1485,9 +1483,9 @@ __global__ void __launch_bounds__(TPB) DFMI_WAVES(5) k_y_assemble_ell(MeshView m
       if (s >= S) break;
       if (s == inert) continue;
       const int ss = s < inert ? s : s - 1;
-      for (int kk = k; kk < W; ++kk) st_out(&val[((long)ss * W + kk) * C + pc], 0.0);
-      st_out(&dS[ss * Ce + pc], dg[j]);
-      st_out(&rhs[ss * Ce + pc], sr[j]);
+      for (int kk = k; kk < W; ++kk) st_drop(&val[((long)ss * W + kk) * C + pc], 0.0);
+      st_drop(&dS[ss * Ce + pc], dg[j]);
+      st_drop(&rhs[ss * Ce + pc], sr[j]);
     }
   };
   group(0);

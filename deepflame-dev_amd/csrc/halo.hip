@@ -196,6 +196,8 @@ Ctx::~Ctx() {
   if (ev_u) (void)hipEventDestroy(ev_u);
   if (ev_e) (void)hipEventDestroy(ev_e);
   if (ev_cw) (void)hipEventDestroy(ev_cw);
+  if (ev_th) (void)hipEventDestroy(ev_th);
+  if (ev_tr) (void)hipEventDestroy(ev_tr);
 }
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }

@@ -66,13 +66,19 @@ __device__ __forceinline__ void hcp_mix(const TC& t, double T, const double* ryw
   }
 }
 
+// Which outputs one evaluation produces: the whole update (TH_ALL), the state the pressure equation needs
+// (TH_STATE: T, he, psi, rho) or the transport the next time step's equations need (TH_TRANSPORT: mu, alpha,
+// rhoD, hai at the given T; rhoD's rho / p is psi there, equal to rounding -- p and rho are the pressure
+// corrector's while the transport runs beside it)
+enum { TH_ALL = 0, TH_STATE = 1, TH_TRANSPORT = 2 };
+
 // state (T or he), p, Y -> T, he, psi, rho, mu, alpha, rhoD[S], hai[S]; mirrors oracle thermo_point
 // (same formulas; divisions hoisted out of the O(S^2) loops -- reciprocals of the species
 // viscosities, one reciprocal per binary-diffusion pair when the fit table is symmetric -- and the
 // per-species divisions as products with 1/W, T powers shared per temperature (tpow) and Newton-refined
 // reciprocals (rcp_nr), so the result agrees with the sequential evaluation to rounding, not bitwise;
 // the Newton step and its stopping test keep their divisions, so the iteration count is the oracle's)
-template <int S>
+template <int S, int PART = TH_ALL>
 __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, double& he, double p, const double* y,
                                              double& psi, double& rho, double& mu, double& alpha, double* rhoD,
                                              double* hai) {
@@ -87,8 +93,11 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   const double rsum = 1.0 / sum;
 #pragma unroll
   for (int i = 0; i < S; ++i) { X[i] = y[i] * t.rW[i] * rsum; Wm += X[i] * t.W[i]; }
-  double cpm;
-  if (fixT) {
+  double cpm = 0.;
+  if (PART == TH_TRANSPORT) {   // T given: only the mixture cp (alpha's), as the fixT branch computes it
+    double h_;
+    hcp_mix<S>(t, T, ryw, h_, cpm);
+  } else if (fixT) {
     hcp_mix<S>(t, T, ryw, he, cpm);
   } else {
     double tt = T;
@@ -107,7 +116,8 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   double poly[5];
   poly[0] = 1.0; poly[1] = lnT; poly[2] = poly[1] * poly[1]; poly[3] = poly[1] * poly[2]; poly[4] = poly[2] * poly[2];
   psi = Wm / (R_GAS * T);
-  rho = p * psi;
+  if (PART == TH_STATE) { rho = p * psi; return; }
+  if (PART == TH_ALL) rho = p * psi;
   // Wilke mixture viscosity
   double sv[S], rsv[S], xs[S];
 #pragma unroll
@@ -144,7 +154,7 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   }
   alpha = 0.5 * (sc + 1.0 / sic) / cpm;
   // mixture-averaged diffusion: s1_i = sum_j X_j / D_ij, s2_i = sum_j X_j W_j / D_ij (j != i, ascending j)
-  const double powT = T * sT, rdp = rho / p;
+  const double powT = T * sT, rdp = PART == TH_TRANSPORT ? psi : rho / p;
   double s1[S], s2[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) { s1[i] = 0.; s2[i] = 0.; }
@@ -191,10 +201,26 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
 // Register budget: S <= 9 is compiled for 3 waves per SIMD (S = 9: 167 VGPRs with 20 B/lane of spill, against the
 // compiler's own 172 VGPRs / 2 waves): k_thermo_cells<9> 506-508 -> 460-462 us on the 2M headline
 // (profiles/r04_thermo_waves_ab.json, two runs each). Larger register-resident mechanisms keep the compiler's choice.
-template <int S> constexpr int thermo_wv() { return S <= 9 ? 3 : 1; }
+// The transport half alone (TH_TRANSPORT) spills ~380 B/lane at that cap (its Wilke and diffusion rows keep the
+// whole X / sv / s1 / s2 set live with nothing to retire early), so it is compiled for 2 waves: it runs beside
+// the p solve, where occupancy is not what bounds it (256 VGPRs, no scratch).
+template <int S, int PART = 0> constexpr int thermo_wv() { return S <= 9 ? (PART == 2 ? 2 : 3) : 1; }
 
-template <int S>
-__global__ void __launch_bounds__(256, thermo_wv<S>()) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
+// T/he/psi/rho written unless PART is TH_TRANSPORT, mu/alpha/rhoD/hai unless it is TH_STATE
+template <int S, int PART>
+__device__ __forceinline__ void thermo_store(long i0, long n, double* T, double* he, double* psi, double* rho, double* mu,
+    double* alpha, double* rhoD, double* hai, double Tv, double hv, double ps, double r, double m, double a,
+    const double* rd, const double* ha) {
+  if (PART != TH_TRANSPORT) { T[i0] = Tv; he[i0] = hv; psi[i0] = ps; rho[i0] = r; }
+  if (PART != TH_STATE) {
+    mu[i0] = m; alpha[i0] = a;
+#pragma unroll
+    for (int i = 0; i < S; ++i) { rhoD[(long)i * n + i0] = rd[i]; hai[(long)i * n + i0] = ha[i]; }
+  }
+}
+
+template <int S, int PART>
+__global__ void __launch_bounds__(256, (thermo_wv<S, PART>())) k_thermo_cells(int n, TC t, int fixT, double* __restrict__ T, double* __restrict__ he,
     const double* __restrict__ p, const double* __restrict__ Y, double* __restrict__ psi, double* __restrict__ rho,
     double* __restrict__ mu, double* __restrict__ alpha, double* __restrict__ rhoD, double* __restrict__ hai) {
   const int c = xcd_block() * blockDim.x + threadIdx.x;
@@ -202,16 +228,15 @@ __global__ void __launch_bounds__(256, thermo_wv<S>()) k_thermo_cells(int n, TC 
   double y[S], rd[S], ha[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) y[i] = Y[(long)i * n + c];
-  double Tc = T[c], hc = he[c], ps, r, m, a;
-  thermo_point<S>(t, fixT != 0, Tc, hc, p[c], y, ps, r, m, a, rd, ha);
-  T[c] = Tc; he[c] = hc; psi[c] = ps; rho[c] = r; mu[c] = m; alpha[c] = a;
-#pragma unroll
-  for (int i = 0; i < S; ++i) { rhoD[(long)i * n + c] = rd[i]; hai[(long)i * n + c] = ha[i]; }
+  double Tc = T[c], hc = PART == TH_TRANSPORT ? 0. : he[c], ps, r, m, a;
+  thermo_point<S, PART>(t, PART == TH_TRANSPORT || fixT != 0, Tc, hc, PART == TH_TRANSPORT ? 0. : p[c], y, ps, r, m, a,
+                        rd, ha);
+  thermo_store<S, PART>(c, n, T, he, psi, rho, mu, alpha, rhoD, hai, Tc, hc, ps, r, m, a, rd, ha);
 }
 
 // boundary slots: fixedValue T patches evaluate from T (he from T), others from he (CPU
 // correctThermo boundary loop, dfChemistryModel.C:560-727); processor [internal n] slots copy cells.
-template <int S>
+template <int S, int PART>
 __global__ void __launch_bounds__(256) k_thermo_slots(MeshView m, TC t, const int8_t* __restrict__ tyT, int fromT,
     const double* __restrict__ cT, const double* __restrict__ che, const double* __restrict__ cpsi,
     const double* __restrict__ crho, const double* __restrict__ cmu, const double* __restrict__ calpha,
@@ -226,19 +251,21 @@ __global__ void __launch_bounds__(256) k_thermo_slots(MeshView m, TC t, const in
   if (bc_proc(ty) && !m.sprim[b]) {
     const int c = m.bfc[b];
     const long C = m.C;
-    T[b] = cT[c]; he[b] = che[c]; psi[b] = cpsi[c]; rho[b] = crho[c]; mu[b] = cmu[c]; alpha[b] = calpha[c];
+    if (PART != TH_TRANSPORT) { T[b] = cT[c]; he[b] = che[c]; psi[b] = cpsi[c]; rho[b] = crho[c]; }
+    if (PART != TH_STATE) {
+      mu[b] = cmu[c]; alpha[b] = calpha[c];
 #pragma unroll
-    for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = crhoD[i * C + c]; hai[(long)i * B + b] = chai[i * C + c]; }
+      for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = crhoD[i * C + c]; hai[(long)i * B + b] = chai[i * C + c]; }
+    }
     return;
   }
   double y[S], rd[S], ha[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) y[i] = Y[(long)i * B + b];
-  double Tb = T[b], hb = he[b], ps, r, mm, a;
-  thermo_point<S>(t, fromT != 0 || bc_fixes_value(ty), Tb, hb, p[b], y, ps, r, mm, a, rd, ha);
-  T[b] = Tb; he[b] = hb; psi[b] = ps; rho[b] = r; mu[b] = mm; alpha[b] = a;
-#pragma unroll
-  for (int i = 0; i < S; ++i) { rhoD[(long)i * B + b] = rd[i]; hai[(long)i * B + b] = ha[i]; }
+  double Tb = T[b], hb = PART == TH_TRANSPORT ? 0. : he[b], ps, r, mm, a;
+  thermo_point<S, PART>(t, PART == TH_TRANSPORT || fromT != 0 || bc_fixes_value(ty), Tb, hb,
+                        PART == TH_TRANSPORT ? 0. : p[b], y, ps, r, mm, a, rd, ha);
+  thermo_store<S, PART>(b, B, T, he, psi, rho, mu, alpha, rhoD, hai, Tb, hb, ps, r, mm, a, rd, ha);
 }
 
 // mixture enthalpy summed exactly as calculate_enthalpy_device_kernel (dfThermo.cu:257-274) and the
@@ -800,8 +827,11 @@ void thermo_energy_gradient(Ctx& x) {
   DFMI_HIP(hipGetLastError());
 }
 
-void thermo_correct(Ctx& x, bool from_T) {
+void thermo_correct(Ctx& x, bool from_T, int part) {
   Thermo& th = x.thermo;
+  DFMI_CHECK(part >= TH_ALL && part <= TH_TRANSPORT, "thermo_correct: part 0, 1 or 2");
+  // the species-generic (cooperative) kernel is not split: its TH_STATE call does the whole update
+  if (species_generic(x) && part == TH_TRANSPORT) return;
   DFMI_CHECK(th.S == x.S, "thermo coefficients not set or species count mismatch");
   int sym = 1;
   for (int i = 0; i < th.S && sym; ++i)
@@ -811,14 +841,17 @@ void thermo_correct(Ctx& x, bool from_T) {
   TC t{th.dW, th.drW, th.dnasa, th.dvisc, th.dcond, th.dbdiff, th.dvc1, th.dvc2, sym, th.dnasaT, th.dbdiffT, th.dvc1T, th.dvc2T,
        th.dvcP, sym && th.dbdR.n ? th.dbdR.p : nullptr};
   MeshView m = x.view();
-#define CALL(NS)                                                                                                   \
+#define CALL(NS) do { switch (part) { case TH_ALL: CALLP(NS, TH_ALL); break;                                  \
+    case TH_STATE: CALLP(NS, TH_STATE); break; default: CALLP(NS, TH_TRANSPORT); } } while (0)
+  static const char* kname[3] = {"k_thermo_cells", "k_thermo_state", "k_thermo_transport"};
+#define CALLP(NS, PART)                                                                                           \
   do {                                                                                                            \
-    if (x.C > 0) { KScope _ks(x, "k_thermo_cells");                                                              \
-      hipLaunchKernelGGL((k_thermo_cells<NS>), dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t,          \
+    if (x.C > 0) { KScope _ks(x, kname[PART]);                                                                    \
+      hipLaunchKernelGGL((k_thermo_cells<NS, PART>), dim3(blocks_for(x.C, 256)), dim3(256), 0, x.stream, x.C, t,    \
                          (int)from_T, x.f("T"), x.f("he"), x.f("p"), x.f("Y"), x.f("psi"), x.f("rho"), x.f("mu"),   \
                          x.f("alpha"), x.f("rhoD"), x.f("hai")); }                                              \
     DFMI_HIP(hipGetLastError());                                                                                  \
-    if (x.B > 0) hipLaunchKernelGGL(k_thermo_slots<NS>, dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t,  \
+    if (x.B > 0) hipLaunchKernelGGL((k_thermo_slots<NS, PART>), dim3(blocks_for(x.B, 256)), dim3(256), 0, x.stream, m, t,\
                        x.st("T"), (int)from_T, x.f("T"), x.f("he"), x.f("psi"), x.f("rho"), x.f("mu"), x.f("alpha"), \
                        x.f("rhoD"), x.f("hai"), x.f("boundary_T"), x.f("boundary_he"), x.f("boundary_p"),          \
                        x.f("boundary_Y"), x.f("boundary_psi"), x.f("boundary_rho"), x.f("boundary_mu"),            \
@@ -861,9 +894,14 @@ void thermo_correct(Ctx& x, bool from_T) {
     default: throw Error("dfmi: thermo species count " + std::to_string(x.S) + " not supported");
   }
 #undef CALL
+#undef CALLP
   // neighbour halves of the processor slots carry the neighbour rank's cell values
-  if (from_T) halo_fields(x, {"he", "T", "psi", "rho", "mu", "alpha", "rhoD", "hai"});
-  else halo_fields(x, {"T", "psi", "rho", "mu", "alpha", "rhoD", "hai"});
+  if (species_generic(x)) part = TH_ALL;
+  std::vector<const char*> names;
+  if (from_T && part != TH_TRANSPORT) names.push_back("he");
+  if (part != TH_TRANSPORT) for (const char* f : {"T", "psi", "rho"}) names.push_back(f);
+  if (part != TH_STATE) for (const char* f : {"mu", "alpha", "rhoD", "hai"}) names.push_back(f);
+  halo_fields(x, names);
 }
 
 }  // namespace dfmi
