@@ -27,8 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deepflame-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
-PMC_FILE = "r05_pmc_traffic.json"
-PMC_FLOPS_FILE = "r05_pmc_flops.json"   # scripts/pmc_flops.sh: FP64 FLOPs per dispatch (SQ_INSTS_VALU_FLOPS_FP64)
+PMC_FILE = "r06_pmc_traffic.json"
+PMC_FLOPS_FILE = "r06_pmc_flops.json"   # scripts/pmc_flops.sh: FP64 FLOPs per dispatch (SQ_INSTS_VALU_FLOPS_FP64)
 FP64_PEAK_TFS = 78.6                    # MI355X FP64 vector peak
 
 MECHS = {   # tests/golden: the reference's ES80 table, and the Burke 9-species table made by dfmi.transport_fit

@@ -13,6 +13,7 @@ uploaded mechanism is bitwise the one it was generated from.
 """
 from __future__ import annotations
 
+import math
 import struct
 import sys
 
@@ -59,6 +60,83 @@ def _dpow(var: str, nu: float) -> str:
     return f"{_f(nu)}*pow({var}, {_f(nu - 1)})"
 
 
+def _g_rt(row, T):
+    """g_i / RT of one NASA7 row at the temperatures T (array), as the generated header evaluates it."""
+    a = np.where((T > row[0])[:, None], row[1:8][None, :], row[8:15][None, :])
+    h = a[:, 0] + a[:, 1] / 2 * T + a[:, 2] / 3 * T ** 2 + a[:, 3] / 4 * T ** 3 + a[:, 4] / 5 * T ** 4 + a[:, 5] / T
+    s = a[:, 0] * np.log(T) + a[:, 1] * T + a[:, 2] / 2 * T ** 2 + a[:, 3] / 3 * T ** 3 + a[:, 4] / 4 * T ** 4 + a[:, 6]
+    return h - s
+
+
+def _net_nu(mech, r):
+    d = {}
+    for j in range(3):
+        if mech.prod[r, j] >= 0:
+            d[int(mech.prod[r, j])] = d.get(int(mech.prod[r, j]), 0.0) + mech.nu_p[r, j]
+        if mech.reac[r, j] >= 0:
+            d[int(mech.reac[r, j])] = d.get(int(mech.reac[r, j]), 0.0) - mech.nu_r[r, j]
+    return {i: v for i, v in d.items() if v != 0.0}
+
+
+def _eq_product_floor(mech, nasa, rev):
+    """Lowest temperature from which every reverse rate of `rev` can be formed as products of per-species
+    exp(g_i / RT) (integer net coefficients): each factor and each partial product of a reaction's numerator and
+    denominator stays within exp(+-600) up to 10000 K. None when some reaction never qualifies."""
+    T = np.geomspace(20.0, 10000.0, 4000)
+    ok = np.ones(T.size, dtype=bool)
+    for r in rev:
+        num = np.zeros(T.size); den = np.zeros(T.size)
+        for i, v in sorted(_net_nu(mech, r).items()):
+            g = _g_rt(nasa[i], T)
+            for _ in range(int(round(abs(v)))):
+                if v > 0:
+                    num = num + g
+                    ok &= np.abs(num) < 600.0
+                else:
+                    den = den + g
+                    ok &= np.abs(den) < 600.0
+            ok &= np.abs(g) < 600.0
+    if not ok[-1]:
+        return None
+    bad = np.nonzero(~ok)[0]
+    return float(T[bad[-1] + 1]) * 1.01 if bad.size else float(T[0])
+
+
+def _arrhenius(A, b, Ta):
+    """A T^b exp(-Ta / T) with the exponential only where it is needed (b integer or +-1/2 and Ta = 0: powers)."""
+    if Ta == 0:
+        n2 = 2 * b
+        if b == 0:
+            return _f(A)
+        if abs(n2 - round(n2)) < 1e-12 and -4 <= round(n2) <= 6:
+            n2 = int(round(n2))
+            f = {1: "T", 2: "T2", 3: "T3", 4: "T4"}
+            parts = []
+            if n2 % 2:
+                parts.append("sqrt(T)" if n2 > 0 else "sqrt(rT)")
+            q = abs(n2) // 2
+            if q:
+                parts.append(f[q] if n2 > 0 else "*".join(["rT"] * q))
+            return f"{_f(A)} * " + " * ".join(parts)
+    return f"{_f(A)} * exp({_f(b)}*lnT - {_f(Ta)}*rT)"
+
+
+def _troe_const(a, T3, T1, has_T2):
+    """log10 Fc when it does not depend on T in double precision: exp(-T / T3) is exactly 0 for T3 <= 1e-30 and
+    exp(-T / T1) exactly 1 for T1 >= 1e30 at every T below 1e13 K (T / T1 under half an ulp of 1). None otherwise."""
+    if has_T2:
+        return None
+    terms = []
+    for coef, Tx in ((1 - a, T3), (a, T1)):
+        if Tx <= 1e-30:
+            terms.append(0.0)
+        elif Tx >= 1e30:
+            terms.append(coef)
+        else:
+            return None
+    return math.log10(max(terms[0] + terms[1], 1e-300))
+
+
 def generate(mech, nasa, W, name: str) -> str:
     S, R = mech.S, mech.R
     nasa = np.asarray(nasa); W = np.asarray(W)
@@ -97,12 +175,17 @@ def generate(mech, nasa, W, name: str) -> str:
     # ---- constants: kf[r], kr[r] (reverse = kf / Kc, 0 if irreversible), k0[r] (fall-off)
     falloff = [r for r in range(R) if mech.itype[r] >= 2]
     troe = [r for r in range(R) if mech.itype[r] == 3]
+    troe_c = {r: _troe_const(mech.troe[r][0], mech.troe[r][1], mech.troe[r][2], mech.has_T2[r]) for r in troe}
     nK = 2 * R + len(falloff) + len(troe)
     emit(f"  static constexpr int NK = {nK};")
     # rate constants: k[r] forward (Arrhenius), k[R + r] reverse (= forward / Kc, 0 if irreversible), k[2R + i]
     # the fall-off low-pressure limits, then log10 Fc of the Troe reactions (a function of T alone, so it is
-    # evaluated once per cell here, not in every rate evaluation); the header (ln T, 1/T, powers, Gibbs terms)
-    # is shared
+    # evaluated once per cell here, not in every rate evaluation; a literal where T3 / T1 make it constant -- still
+    # stored with the others: read as a literal inside the rates it took the k_chem_gen wave 410 -> 418 registers,
+    # past the 416 that leave a 96-VGPR assembly kernel room on the SIMD beside it); the header (ln T, 1/T, powers, Gibbs terms) is shared. Transcendentals are most of this function's
+    # cost (~1,900 VALU instructions per cell for Burke 9, a third of the cell's integration): the forward rates
+    # take powers instead of exp where b is a (half-)integer and Ta = 0, and above T_eq the reverse rates are
+    # products of one exp(g_i / RT) per species instead of one exp per reaction
     head = ["    const double lnT = log(T), rT = 1.0 / T;",
             "    const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;"]
     needs_g = sorted({int(i) for r in range(R) if mech.reversible[r]
@@ -115,13 +198,19 @@ def generate(mech, nasa, W, name: str) -> str:
             return f"{h} - {s}"
         head.append(f"    const double g{i} = T > {_f(row[0])} ? {hs(row[1:8])} : {hs(row[8:15])};")
     head.append(f"    const double lc = log({_f(P_ATM / RU)} * rT);   // log(p_atm / RT)")
+    rev = [r for r in range(R) if mech.reversible[r]]
+    # the per-species form needs integer net coefficients; a mechanism with other orders keeps the per-reaction exp
+    prod_form = [r for r in rev if all(abs(v - round(v)) < 1e-12 and abs(v) <= 3 for v in _net_nu(mech, r).values())]
+    T_eq = _eq_product_floor(mech, nasa, prod_form) if prod_form else None
+    if T_eq is None:
+        prod_form = []
     fo = {}
     kdef = {}
+    kdef_eq = {}
     for r in range(R):
         lines = []
         A, b, Ta = mech.A[r], mech.b[r], mech.Ta[r]
-        expr = _f(A) if (b == 0 and Ta == 0) else f"{_f(A)} * exp({_f(b)}*lnT - {_f(Ta)}*rT)"
-        lines.append(f"    k[{r}] = {expr};")
+        lines.append(f"    k[{r}] = {_arrhenius(A, b, Ta)};")
         if mech.reversible[r]:
             dG = []
             dnu = 0.0
@@ -130,17 +219,35 @@ def generate(mech, nasa, W, name: str) -> str:
                     dG.append(f"+ {_f(mech.nu_p[r, j])}*g{mech.prod[r, j]}"); dnu += mech.nu_p[r, j]
                 if mech.reac[r, j] >= 0:
                     dG.append(f"- {_f(mech.nu_r[r, j])}*g{mech.reac[r, j]}"); dnu -= mech.nu_r[r, j]
-            lines.append(f"    k[{R + r}] = k[{r}] * exp(0.0 {' '.join(dG)} - {_f(dnu)}*lc);")
+            kexp = f"    k[{R + r}] = k[{r}] * exp(0.0 {' '.join(dG)} - {_f(dnu)}*lc);"
+            if r in prod_form:
+                # k_r = k_f exp(sum nu g) (p_atm / RT)^-dnu = k_f prod e_i^nu_i pc^-dnu, pc = p_atm / RT
+                num, den = [], []
+                for i, v in sorted(_net_nu(mech, r).items()):
+                    (num if v > 0 else den).extend([f"e{i}"] * int(round(abs(v))))
+                n = int(round(dnu))
+                (num if n < 0 else den).extend(["pc"] * abs(n))
+                expr = f"k[{r}]"
+                if num:
+                    expr += " * (" + " * ".join(num) + ")"
+                if den:
+                    expr += " * DFMI_RCP(" + " * ".join(den) + ")"
+                kdef_eq[r] = (f"      k[{R + r}] = {expr};", kexp.replace("    k[", "      k[", 1))
+            else:
+                lines.append(kexp)
         else:
             lines.append(f"    k[{R + r}] = 0.0;")
         if mech.itype[r] >= 2:
             fo[r] = 2 * R + len(fo)
             A0, b0, Ta0 = mech.A0[r], mech.b0[r], mech.Ta0[r]
-            lines.append(f"    k[{fo[r]}] = {_f(A0)} * exp({_f(b0)}*lnT - {_f(Ta0)}*rT);")
+            lines.append(f"    k[{fo[r]}] = {_arrhenius(A0, b0, Ta0)};")
         kdef[r] = lines
     ftroe = {}
     for r in troe:
         ftroe[r] = 2 * R + len(falloff) + len(ftroe)
+        if troe_c[r] is not None:
+            kdef[r].append(f"    k[{ftroe[r]}] = {_f(troe_c[r])};   // log10 Fc: T3 / T1 make it constant")
+            continue
         a, T3, T1, T2 = mech.troe[r]
         fc = f"{_f(1 - a)}*exp(-T / {_f(T3)}) + {_f(a)}*exp(-T / {_f(T1)})"
         if mech.has_T2[r]:
@@ -153,6 +260,18 @@ def generate(mech, nasa, W, name: str) -> str:
     L.extend(head)
     for r in range(R):
         L.extend(kdef[r])
+    if kdef_eq:
+        eq_sp = sorted({i for r in kdef_eq for i in _net_nu(mech, r)})
+        emit(f"    if (T >= {_f(T_eq)}) {{   // every factor and partial product within exp(+-600) (codegen T_eq)")
+        emit(f"      const double pc = {_f(P_ATM / RU)} * rT;   // p_atm / RT")
+        for i in eq_sp:
+            emit(f"      const double e{i} = exp(g{i});")
+        for r in sorted(kdef_eq):
+            emit(kdef_eq[r][0])
+        emit("    } else {")
+        for r in sorted(kdef_eq):
+            emit(kdef_eq[r][1])
+        emit("    }")
     emit("  }")
     def third_body(r):
         terms = []
