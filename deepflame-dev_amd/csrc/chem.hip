@@ -756,7 +756,7 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
   double* stats = x.f("chem_stats");
   const double* rho_rr = x.f(rho_field);
   if (h.fail.n == 0) h.fail.alloc(1);
-  DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
+  if (!h.batch) DFMI_HIP(hipMemsetAsync(h.fail.p, 0, sizeof(int), x.stream));
   h.method = (int)x.opt("chem.method");
   h.bin = (int)x.opt("chem.binning");
   const long ng = (x.C + GRP - 1) / GRP;   // binning groups
@@ -824,6 +824,7 @@ void chem_solve(Ctx& x, double dt, const char* rho_field) {
 // next host synchronisation point the caller already has (end of the time step's solver polls).
 void chem_fail_snapshot(Ctx& x) {
   Chem& h = x.chem;
+  if (h.batch) return;   // the batch's one snapshot follows its last step
   h.fail_host.ensure(1);
   if (!h.fail_ev) DFMI_HIP(hipEventCreateWithFlags(&h.fail_ev, hipEventDisableTiming));
   DFMI_HIP(hipMemcpyAsync(h.fail_host.p, h.fail.p, sizeof(int), hipMemcpyDeviceToHost, x.stream));
@@ -837,8 +838,9 @@ void chem_check(Ctx& x) {
   DFMI_HIP(hipEventSynchronize(h.fail_ev));
   h.fail_pending = false;
   const int nf = h.fail_host.p[0];
-  DFMI_CHECK(nf == 0, "chemistry: " + std::to_string(nf) + " cell(s) hit the integrator step limit (max_steps = " +
-                          std::to_string(h.max_steps) + "); their RR is not a completed integration");
+  DFMI_CHECK(nf == 0, "chemistry: " + std::to_string(nf) + " cell(s)" + (h.batch ? " (summed over the batch's steps)" : "") +
+                          " hit the integrator step limit (max_steps = " + std::to_string(h.max_steps) +
+                          "); their RR is not a completed integration");
 }
 
 }  // namespace dfmi

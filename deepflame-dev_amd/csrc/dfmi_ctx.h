@@ -161,6 +161,7 @@ struct Chem {
   PinnedBuf<int> fail_host;     // its copy, behind fail_ev
   hipEvent_t fail_ev = nullptr;
   bool fail_pending = false;
+  bool batch = false;           // dfmi_zero_d_step's loop: the counter sums over the batch, read once at its end
   ~Chem() { if (fail_ev) (void)hipEventDestroy(fail_ev); }
 };
 

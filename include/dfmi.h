@@ -243,7 +243,9 @@ int dfmi_chem_solve(dfmi_ctx* ctx, double dt);
 /* n_steps df0DFoam time steps (applications/solvers/df0DFoam/df0DFoam.C:99-113, YEqn.H, EEqn.H;
  * zeroDReactor constantProperty pressure): per step chemistry.solve(dt) on every cell, YEqn
  * ddt(rho, Yi) == RR_i (Yi.max(0), inert = 1 - sum), he held, correctThermo (T from he), rho = p psi.
- * Every cell is an independent 0D reactor (BASELINE config 1). */
+ * Every cell is an independent 0D reactor (BASELINE config 1). The steps are queued without a host
+ * synchronisation between them; a chemistry step-limit failure in any of them fails the call once the batch
+ * has run (the message gives the count summed over the steps). */
 int dfmi_zero_d_step(dfmi_ctx* ctx, double dt, int n_steps);
 /* integrator step budget per cell and solve (default 100000); exceeding it is an error of the call */
 int dfmi_chem_set_max_steps(dfmi_ctx* ctx, int max_steps);
