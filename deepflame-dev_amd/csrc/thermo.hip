@@ -198,8 +198,9 @@ __device__ __forceinline__ void thermo_point(const TC& t, bool fixT, double& T, 
   }
 }
 
-// Register budget: S <= 9 is compiled for 3 waves per SIMD (S = 9: 167 VGPRs with 20 B/lane of spill, against the
-// compiler's own 172 VGPRs / 2 waves): k_thermo_cells<9> 506-508 -> 460-462 us on the 2M headline
+// Register budget: S <= 9 is compiled for 3 waves per SIMD (S = 9: 167 VGPRs with 20 B/lane of spill when this was
+// set, 162 and none on the round-6 tree, against the compiler's own 172 VGPRs / 2 waves): k_thermo_cells<9>
+// 506-508 -> 460-462 us on the 2M headline
 // (profiles/r04_thermo_waves_ab.json, two runs each). Larger register-resident mechanisms keep the compiler's choice.
 // The transport half alone (TH_TRANSPORT) spills ~380 B/lane at that cap (its Wilke and diffusion rows keep the
 // whole X / sv / s1 / s2 set live with nothing to retire early), so it is compiled for 2 waves: it runs beside
