@@ -355,8 +355,8 @@ Stats bicgstab(const Sys& A, const double* b, double* xv, const SolverCfg& cfg) 
 }
 
 // ---- AMG (hierarchy from csrc/amg_graph.h, V-cycle as amg.hip's, fp64)
-constexpr double AMG_OMEGA = 0.9, AMG_OVERCORR = 1.35;
-constexpr int AMG_COARSE_SWEEPS = 8, AMG_COARSEST = 512;
+constexpr double AMG_OMEGA = 0.9, AMG_OVERCORR = 1.4;
+constexpr int AMG_COARSE_SWEEPS = 6, AMG_COARSEST = 512;
 
 void amg_setup(Ctx& x) {
   x.amg.clear();
@@ -1074,7 +1074,7 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) { return guard([&] { require_ready
 int dfmi_sync(dfmi_ctx*) { return 0; }
 // no device events on the CPU: the bench times CPU-A with host clocks
 int dfmi_step_timer(dfmi_ctx*, int) { return 0; }
-// CPU-A runs one fixed configuration (the GPU path's defaults: AMG omega 0.9, over-correction 1.35, ...)
+// CPU-A runs one fixed configuration (the GPU path's defaults: AMG omega 0.9, over-correction 1.4, 6 coarsest sweeps, ...)
 int dfmi_set_option(dfmi_ctx*, const char* key, double) {
   return guard([&] { throw Error(std::string("dfmi (CPU-A): option '") + key + "' is not configurable here"); });
 }
