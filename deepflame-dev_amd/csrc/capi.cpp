@@ -707,8 +707,10 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
       x.amg.reuse_ok = i > 0;         // a later corrector may precondition with this step's first hierarchy
       do_p(x);
       x.amg.reuse_ok = false;
-      thermo_correct_psip_rho(x);
-      rho_process(x, false);
+      // pEqn_GPU.H ends with thermo.correctPsipRho() and the rhoEqn; both write rho, which the next statement here
+      // -- rho = psi p at the next corrector's start, or after the loop (dfLowMachFoam.C:517) -- overwrites before
+      // anything reads it (the oracle's time_step runs them: the fields agree bitwise). dfmi_thermo_correct_psip_rho /
+      // dfmi_rho_process keep them for callers that read rho in between.
     }
     thermo_rho_from_psi(x);         // rho = thermo.rho() (dfLowMachFoam.C:517)
     if (x.chem.mode == 1) chem_check(x);   // the p solves' polls have already passed the chemistry
