@@ -701,8 +701,9 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
                                     // UEqn, the EEqn assembly beside the Y solve)
     const bool tsplit = do_thermo_split(x);   // correctThermo (the transport half beside the p solves)
     for (int i = 0; i < n_corr; ++i) {   // pEqn_GPU.H
-      thermo_rho_from_psi(x);
-      thermo_psip0(x);
+      // rho = psi p: the first corrector's is what correctThermo just wrote (the same product of the same p and psi,
+      // halo included); psip0 = psi p feeds only correctPsipRho, skipped below (the field is not updated here)
+      if (i > 0) thermo_rho_from_psi(x);
       u_hbya(x);
       x.amg.reuse_ok = i > 0;         // a later corrector may precondition with this step's first hierarchy
       do_p(x);

@@ -83,16 +83,25 @@ template <class T> struct DevBuf {
 // Owning pinned host allocation (device-visible; async copies into it need no staging).
 template <class T> struct PinnedBuf {
   T* p = nullptr;
+  T* d = nullptr;   // device view (ensure_mapped only)
   size_t n = 0;
   PinnedBuf() = default;
   PinnedBuf(const PinnedBuf&) = delete;
   PinnedBuf& operator=(const PinnedBuf&) = delete;
   ~PinnedBuf() { release(); }
-  void release() { if (p) { (void)hipHostFree(p); p = nullptr; n = 0; } }
+  void release() { if (p) { (void)hipHostFree(p); p = nullptr; n = 0; } d = nullptr; }
   void ensure(size_t count) {
     if (count <= n) return;
     release();
     DFMI_HIP(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+    n = count;
+  }
+  // mapped into the device's address space: kernels store into it directly (read by the host after a sync)
+  void ensure_mapped(size_t count) {
+    if (count <= n && d) return;
+    release();
+    DFMI_HIP(hipHostMalloc(&p, count * sizeof(T), hipHostMallocMapped));
+    DFMI_HIP(hipHostGetDevicePointer((void**)&d, p, 0));
     n = count;
   }
 };

@@ -1319,22 +1319,24 @@ int work_slot(const std::string& eqn) {
   throw Error("dfmi: unknown equation '" + eqn + "'");
 }
 
-__global__ void k_accum_iters(const double* scal, int nsys, double* acc) {
+// the solve's scalars stored straight into the mapped host snapshot (vector stores; one launch instead of a launch and
+// a copy), and its system-iterations summed into the equation's work counter
+__global__ void k_accum_iters(const double* scal, int nsys, double* acc, double* snap) {
+  for (int i = threadIdx.x; i < nsys * NSCAL; i += blockDim.x) snap[i] = scal[i];
   if (threadIdx.x != 0) return;
   double a = 0.0;
   for (int s = 0; s < nsys; ++s) a += scal[s * NSCAL + 7];
   *acc += a;
 }
 
-// final state of the solve, copied for dfmi_solver_stats without waiting; iterations summed into
-// the equation's work counter on the device
+// final state of the solve, recorded for dfmi_solver_stats without waiting (it synchronises before reading);
+// iterations summed into the equation's work counter on the device
 void record_stats(Ctx& x, const char* eqn, const double* scal, int nsys) {
   if (x.work.n == 0) { x.work.alloc(4); x.work.zero(x.stream); }
-  hipLaunchKernelGGL(k_accum_iters, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.work.p + work_slot(eqn));
   auto& sn = x.stat_snap[eqn];
-  sn.h.ensure((size_t)nsys * NSCAL);
+  sn.h.ensure_mapped((size_t)nsys * NSCAL);
   sn.nsys = nsys;
-  DFMI_HIP(hipMemcpyAsync(sn.h.p, scal, (size_t)nsys * NSCAL * sizeof(double), hipMemcpyDeviceToHost, x.stream));
+  hipLaunchKernelGGL(k_accum_iters, dim3(1), dim3(64), 0, x.stream, scal, nsys, x.work.p + work_slot(eqn), sn.h.d);
 }
 
 }  // namespace
