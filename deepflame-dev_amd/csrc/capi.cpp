@@ -198,7 +198,7 @@ void do_U(Ctx& x) {
 // synchronisation inside, so dfmi_time_step can issue it on the side stream beside the UEqn)
 // weights = false: the div(phi,Yi_h) weights are formed elsewhere (do_U_Y_fork) and `rows_after` (if set) is the
 // event the rows wait for on this stream
-void do_Y_front(Ctx& x, bool weights = true, hipEvent_t rows_after = nullptr, hipEvent_t prep_done = nullptr) {
+void do_Y_front(Ctx& x, bool weights = true, hipEvent_t rows_after = nullptr) {
   DFMI_CHECK(x.inert >= 0 && x.inert < x.S, "inert species index not set");
   YWs _yw(x);
   // chemistry->solve(deltaT) before YEqn (YEqn.H); the thermo density of that call is rho before this
@@ -206,7 +206,6 @@ void do_Y_front(Ctx& x, bool weights = true, hipEvent_t rows_after = nullptr, hi
   if (x.chem.mode == 1) chem_solve(x, 1.0 / x.rdt, "rho_old");
   else if (x.chem.mode == 2) dnn_solve(x, "rho_old");   // chemistrySolver_GPU.Inference (YEqn_GPU.H)
   y_prep(x, weights);
-  if (prep_done) DFMI_HIP(hipEventRecord(prep_done, x.stream));   // hDiffCorrFlux (and its halo) final
   if (rows_after) DFMI_HIP(hipStreamWaitEvent(x.stream, rows_after, 0));
   // production path: the assembly writes the solver's ELL rows directly (no LDU round trip)
   double *val, *dS, *rhs;
@@ -247,7 +246,7 @@ bool step_overlap(const Ctx& x) {
 void do_U_Y_fork(Ctx& x) {
   if (!x.stream2) {
     DFMI_HIP(hipStreamCreateWithFlags(&x.stream2, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e, &x.ev_cw, &x.ev_th, &x.ev_tr, &x.ev_yp})
+    for (hipEvent_t* e : {&x.ev_fork, &x.ev_join, &x.ev_u, &x.ev_e, &x.ev_cw, &x.ev_th, &x.ev_tr})
       DFMI_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   DFMI_HIP(hipEventRecord(x.ev_fork, x.stream));
@@ -260,7 +259,7 @@ void do_U_Y_fork(Ctx& x) {
   // rows only: 14.02 / 14.05 -> 14.52 / 14.40 ms per step, round 6 -- not kept)
   DFMI_HIP(hipEventRecord(x.ev_cw, x.stream));
   OnStream _os(x, x.stream2);
-  do_Y_front(x, false, x.ev_cw, x.ev_yp);
+  do_Y_front(x, false, x.ev_cw);
   DFMI_HIP(hipEventRecord(x.ev_join, x.stream2));
 }
 void do_U_Y(Ctx& x) {
@@ -288,19 +287,6 @@ void do_U_Y_E(Ctx& x) {
   if (!step_overlap(x)) { do_U_Y(x); do_E(x); return; }
   do_U_Y_fork(x);
   do_U(x);
-  if (x.on("overlap.e_front_main")) {
-    // the step timeline had the main stream idle ~0.55 ms at the join while the side stream assembled the YEqn rows
-    // alone: the EEqn scheme terms (K's limited weights from the UEqn's K; the cubic correction of the YEqn
-    // preparation's hDiffCorrFlux, waited for by event) fill that gap on the main stream, and the Y solve then runs
-    // without them beside it
-    DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_yp, 0));
-    e_assemble_front(x);
-    DFMI_HIP(hipStreamWaitEvent(x.stream, x.ev_join, 0));
-    do_Y_back(x);
-    e_assemble_back(x);
-    do_E_back(x);
-    return;
-  }
   DFMI_HIP(hipEventRecord(x.ev_u, x.stream));
   {
     OnStream _os(x, x.stream2);

@@ -269,8 +269,6 @@ inline const OptDef* option_defs(int& n) {
     {"chem.generated", 1},            // compiled-in kinetics when the mechanism's fingerprint matches
     {"chem.binning", 2},              // cells launched in cost-binned order: 1 over the mesh, 2 inside 4096-cell tiles
     {"dnn.tuned_gemm", 1},            // DF-ODENet layers by the shape-tuned kernels (0: k_mlp_gemm for every layer)
-    {"overlap.e_front_main", 0},      // the EEqn scheme terms on the main stream after the UEqn (waiting for the YEqn
-                                      // preparation's hDiffCorrFlux) instead of on the side stream after the YEqn rows
     {"thermo.split", 0},              // time step: the transport half of correctThermo on the side stream beside the p solve
                                       // (13.89 -> 13.92 ms per step, 3 rounds each in one call, round 6: not the default)
     {"halo.overlap", 0},              // several ranks: solver halo exchanges on a comm stream while the interior rows run
@@ -383,7 +381,7 @@ struct Ctx {
   // side stream of the time step (dfmi_time_step: chemistry + YEqn preparation beside the UEqn) and its events
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_u = nullptr, ev_e = nullptr, ev_cw = nullptr, ev_th = nullptr,
-            ev_tr = nullptr, ev_yp = nullptr;
+            ev_tr = nullptr;
   // final solver state of the last solve of each equation, copied asynchronously at the end of the
   // solve; dfmi_solver_stats synchronises and reads it (no host sync inside a time step)
   struct StatSnap { PinnedBuf<double> h; int nsys = 0; };

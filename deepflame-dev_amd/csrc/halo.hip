@@ -198,7 +198,6 @@ Ctx::~Ctx() {
   if (ev_cw) (void)hipEventDestroy(ev_cw);
   if (ev_th) (void)hipEventDestroy(ev_th);
   if (ev_tr) (void)hipEventDestroy(ev_tr);
-  if (ev_yp) (void)hipEventDestroy(ev_yp);
 }
 
 bool halo_active(const Ctx& x) { return x.halo != nullptr && x.H > 0; }
