@@ -28,6 +28,7 @@ struct AmgLevel {
 struct Amg {
   bool ready = false;
   bool reuse_ok = false;   // set by dfmi_time_step for its later correctors (option amg.reuse)
+  int age = 0;             // time steps since the V-cycle's operators were last rebuilt (option amg.reuse_steps)
   bool fp32 = true;
   double omega = 0.9;
   double overcorr = 1.35;  // coarse-correction scaling (plain aggregation under-corrects; 1 = plain V-cycle)

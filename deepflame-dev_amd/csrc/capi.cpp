@@ -705,7 +705,11 @@ int dfmi_time_step(dfmi_ctx* ctx, int n_corr) {
       // halo included); psip0 = psi p feeds only correctPsipRho, skipped below (the field is not updated here)
       if (i > 0) thermo_rho_from_psi(x);
       u_hbya(x);
-      x.amg.reuse_ok = i > 0;         // a later corrector may precondition with this step's first hierarchy
+      // a later corrector may precondition with this step's first hierarchy; with amg.reuse_steps = k > 1 the first
+      // corrector too, with the operators of up to k - 1 steps before (rebuilt when they are that old)
+      const int keep = (int)x.opt("amg.reuse_steps");
+      x.amg.reuse_ok = i > 0 || (keep > 1 && x.amg.ready && x.amg.age > 0 && x.amg.age < keep);
+      if (i == 0) x.amg.age = x.amg.reuse_ok ? x.amg.age + 1 : 1;
       do_p(x);
       x.amg.reuse_ok = false;
       // pEqn_GPU.H ends with thermo.correctPsipRho() and the rhoEqn; both write rho, which the next statement here

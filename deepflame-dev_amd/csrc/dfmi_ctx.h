@@ -254,6 +254,9 @@ inline const OptDef* option_defs(int& n) {
     {"amg.tail", 1},                  // the last two levels in one workgroup launch (k_vtail)
     {"amg.halo_l0", 1},               // several ranks: level 0 keeps its processor couplings
     {"amg.global_coarse", 0},         // several ranks: one agglomerated coarsest level
+    {"amg.reuse_steps", 8},           // > 1: the first corrector reuses the V-cycle operators of up to this many - 1
+                                      // earlier steps (1: rebuilt every step). 1 -> 8: 13.59 -> 13.42 ms per step, 3
+                                      // rounds each, 674 against 678 p system-iterations in 28 steps (r06u)
     {"amg.reuse", 1},                 // later correctors of a time step precondition with the step's first V-cycle
                                       // operators (level-0 fp32 copy, Galerkin levels) instead of rebuilding them
     {"solver.even_odd", 1},           // U/Y/E: BiCGStab on the even-odd Schur complement where the rows 2-colour
