@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 L=deepflame-dev_amd/libdfmi.so
 cp $L /tmp/libdfmi_tree.so
 cp scripts/tmp/libdfmi_split.so $L
-timeout -k 10 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 240 --timeout-method thread scripts/tmp/test_split_prolong.py \
+timeout -k 10 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 240 --timeout-method thread scripts/split_prolong_check.py \
   > gpurun_out/r06w_test.log 2>&1
 rc=$?; cp /tmp/libdfmi_tree.so $L; [ $rc -eq 0 ] || exit $rc
 TAG=r06w ROUNDS=3 ARMS="split=scripts/tmp/libdfmi_split.so: base=:" bash scripts/ab_arms.sh || exit 1
